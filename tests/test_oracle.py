@@ -1,0 +1,182 @@
+"""Pins the CPU oracle against the reference's own vectors (CPU only).
+
+The oracle is the checker for every GPU parity test, so it is pinned first:
+Keccak KATs (hashutil/hash_test.go:13-31), the permutation against FIPS
+SHA3-256 (hashlib), every ssz/hash_test.go vector, the merkleHash table and
+the example structs; the deposit-trie batch build against a literal
+dict-based restatement of UpdateDepositTrie (deposit_trie.go:29-40).
+"""
+import hashlib
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from oracle import ssz_ref as S
+
+
+def test_keccak_kats(ref_vectors):
+    for kat in ref_vectors["keccak256_kats"]:
+        assert O.keccak256(bytes.fromhex(kat["in"])).hex() == kat["out"], kat["ref"]
+        assert O.py_keccak256(bytes.fromhex(kat["in"])).hex() == kat["out"], kat["ref"]
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 64, 135, 136, 137, 200, 271, 272, 273, 1000])
+def test_permutation_vs_fips_sha3(n):
+    msg = os.urandom(n)
+    assert O.sha3_256(msg) == hashlib.sha3_256(msg).digest()
+    assert O.py_keccak256(msg, pad=0x06) == hashlib.sha3_256(msg).digest()
+    assert O.py_keccak256(msg) == O.keccak256(msg)
+
+
+def _pyval(t, v):
+    """Convert JSON fixture values into what ssz_ref expects."""
+    k = t[0]
+    if k in ("slice", "array"):
+        return [_pyval(t[1], e) for e in v]
+    if k == "struct":
+        return {name: _pyval(ft, v[name]) for name, ft in t[2]} if v is not None else None
+    if k == "ptr":
+        return None if v is None else _pyval(t[1], v)
+    return v
+
+
+def _pytype(t):
+    k = t[0]
+    if k == "hashable":
+        # hash_test.go:25-32: 28 zero bytes followed by the 4-byte value
+        return ("hashable", t[1], lambda v: (bytes(28) + bytes(v))[:32])
+    if k in ("slice", "ptr"):
+        return (k, _pytype(t[1]))
+    if k == "array":
+        return (k, _pytype(t[1]), t[2])
+    if k == "struct":
+        return (k, t[1], [(n, _pytype(ft)) for n, ft in t[2]])
+    return tuple(t)
+
+
+def test_tree_hash_vectors(ref_vectors):
+    assert len(ref_vectors["tree_hash"]) == 60
+    for vec in ref_vectors["tree_hash"]:
+        t = _pytype(vec["type"])
+        if vec["error"]:
+            with pytest.raises(S.HashError) as ei:
+                S.tree_hash(t, _pyval(vec["type"], vec["value"]))
+            assert str(ei.value) == vec["error"], vec["ref"]
+        else:
+            got = S.tree_hash(t, _pyval(vec["type"], vec["value"]))
+            assert got.hex() == vec["output"], vec["ref"]
+
+
+def test_merkle_hash_vectors(ref_vectors, res_vectors):
+    for vec in ref_vectors["merkle_hash"] + res_vectors["merkle_lists"]:
+        items = [bytes.fromhex(x) for x in vec["items"]]
+        assert O.merkle_hash(items).hex() == vec["output"]
+
+
+def test_merkle_root_vector(ref_vectors):
+    for vec in ref_vectors["merkle_root"]:
+        assert O.merkle_root([bytes.fromhex(v) for v in vec["values"]]).hex() == vec["output"]
+
+
+def test_flat_equals_list_semantics():
+    rng = np.random.default_rng(1)
+    for item_len in (1, 3, 8, 32, 48, 128, 200):
+        for n in (0, 1, 2, 4, 5, 9, 17, 40):
+            items = rng.integers(0, 256, n * item_len, dtype=np.uint8)
+            lst = [bytes(items[i * item_len:(i + 1) * item_len]) for i in range(n)]
+            assert O.merkle_hash_flat(items, n, item_len) == O.merkle_hash(lst)
+
+
+def _py_merkle_hash(lst):
+    """Literal list restatement of hash.go:194-239 with the pure-Python digest."""
+    lenc = struct.pack("<Q", len(lst)) + bytes(24)
+    empty = bytes(128)
+    if not lst:
+        chunks = [empty]
+    elif len(lst[0]) < 128:
+        p = 128 // len(lst[0])
+        chunks = [b"".join(lst[i:i + p]) for i in range(0, len(lst), p)]
+    else:
+        chunks = list(lst)
+    while len(chunks) > 1:
+        if len(chunks) % 2:
+            chunks.append(empty)
+        chunks = [O.py_keccak256(chunks[i] + chunks[i + 1]) for i in range(0, len(chunks), 2)]
+    return O.py_keccak256(chunks[0] + lenc)
+
+
+def test_c_oracle_equals_pure_python_restatement():
+    rng = np.random.default_rng(7)
+    for item_len, n in ((32, 9), (32, 13), (8, 40), (3, 50), (200, 5), (1, 300)):
+        lst = [bytes(rng.integers(0, 256, item_len, dtype=np.uint8)) for _ in range(n)]
+        assert O.merkle_hash(lst) == _py_merkle_hash(lst)
+
+
+class _DictTrie:
+    """Literal restatement of shared/trieutil/deposit_trie.go:13-63."""
+
+    def __init__(self, depth=32):
+        self.depth, self.count, self.m = depth, 0, {}
+
+    def update(self, data):
+        idx = self.count + (1 << self.depth)
+        self.m[idx] = O.keccak256(data)
+        for _ in range(self.depth):
+            idx //= 2
+            self.m[idx] = O.keccak256(self.m.get(idx * 2, bytes(32)) + self.m.get(idx * 2 + 1, bytes(32)))
+        self.count += 1
+
+    def branch(self, index):
+        idx = index + (1 << self.depth)
+        out = []
+        for _ in range(self.depth):
+            out.append(self.m.get(idx - 1 if idx % 2 else idx + 1, bytes(32)))
+            idx //= 2
+        return out
+
+    def root(self):
+        return self.m.get(1, bytes(32))
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 5, 8, 13])
+def test_deposit_trie_batch_equals_incremental(n):
+    deps = [os.urandom(1 + (i * 37) % 300) for i in range(n)]
+    t = _DictTrie()
+    for d in deps:
+        t.update(d)
+    root, levels = O.deposit_trie_levels(deps)
+    assert root == t.root()
+    for i in range(n):
+        br = [levels[d][(i >> d) ^ 1] if ((i >> d) ^ 1) < len(levels[d]) else bytes(32) for d in range(32)]
+        assert br == t.branch(i)
+        assert O.verify_merkle_branch(O.keccak256(deps[i]), br, 32, i, root)
+        assert not O.verify_merkle_branch(O.keccak256(deps[i] + b"x"), br, 32, i, root)
+
+
+def test_restatement_fixtures_reproduce(res_vectors):
+    for c in res_vectors["merkle_flat"][::17]:
+        items = O.splitmix_bytes(c["n"] * c["item_len"], c["seed"])
+        assert O.merkle_hash_flat(items, c["n"], c["item_len"]).hex() == c["root"]
+    sm = res_vectors["splitmix"]
+    assert [O.lib().or_splitmix64_word(sm["seed"], k) for k in range(8)] == sm["words"]
+
+
+def test_generator_and_subtree_oracles_agree():
+    seed = 0x5EED000000000004
+    for n, item_len in ((4 * 64, 32), (4 * 64 + 12, 32), (1000, 8), (333, 32)):
+        items = O.splitmix_bytes(n * item_len, seed)
+        full = O.merkle_hash_flat(items, n, item_len)
+        assert O.merkle_hash_gen(n, item_len, seed) == full
+    # shard roots folded with the reference loop give the same root
+    n, item_len, H = 4 * 40 + 3, 32, 3  # 41 chunks, shards of 8 chunks -> 6 shards
+    roots = [O.merkle_subtree_gen(n, item_len, seed, s, H) for s in range(6)]
+    chunks = roots
+    while len(chunks) > 1:
+        if len(chunks) % 2:
+            chunks = chunks + [bytes(128)]
+        chunks = [O.keccak256(chunks[i] + chunks[i + 1]) for i in range(0, len(chunks), 2)]
+    final = O.keccak256(chunks[0] + struct.pack("<Q", n) + bytes(24))
+    assert final == O.merkle_hash_gen(n, item_len, seed)
