@@ -1,0 +1,195 @@
+"""Headline benchmark: ssz.merkleHash of 2^28 x 32-B synthetic items (8 GiB,
+BASELINE.json configs[3]) on N MI355X, subtree-sharded.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--log2n 28] [--item-len 32]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One step = one complete Merkleization of the whole tree (every rank reduces
+its shard, one 32-B-per-rank RCCL all-gather, rank 0 finishes the top levels
+and the length mix-in).  Inputs are generated on the device before timing and
+stay resident in HBM.  Total work is fixed as N grows ("strong" scaling);
+value = 2^log2n leaves x K / max-over-ranks wall time.  Rank 0 prints one
+JSON line; progress goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+INT_OPS_PER_PERM = 4320  # 24 rounds x 180 int32 VALU ops
+# gfx950 integer VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md:
+# SIMD-32, 2-cycle wave64 issue; = FP32 vector peak 157.3 TFLOPS / 2 flops per FMA).
+PEAK_INT_OPS = 256 * 4 * 32 * 2.4e9
+SEED = 0x5EED000000000000 + 4  # seed = 0x5EED.. + config_id
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(item_len: int, log2n_sample: int):
+    """The oracle (a C port of hash.go:194-239, 1 thread = the reference's
+    single-goroutine shape) on a bounded sample of the same workload."""
+    from oracle import oracle as O
+
+    n = 1 << log2n_sample
+    items = O.splitmix_bytes(n * item_len, SEED)
+    t0 = time.perf_counter()
+    O.merkle_hash_flat(items, n, item_len, nthreads=1)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "leaves/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/merkle_ref.c or_merkle_hash, 2^{log2n_sample} x {item_len}-B items "
+                      f"(same SplitMix64 stream), 1 thread, {dt:.1f} s"}
+
+
+def load_pmc_traffic():
+    """HBM bytes per leaf-kernel launch from the committed rocprofv3 PMC
+    summary (profiles/*_pmc.json written by tools/pmc_summary.py), if any."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    if not files:
+        return None
+    try:
+        with open(files[-1]) as f:
+            return json.load(f).get("hbm_bytes_per_leaf_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log2n", type=int, default=28)
+    ap.add_argument("--item-len", type=int, default=32)
+    ap.add_argument("--cpu-sample-log2n", type=int, default=24)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from prysm_amd import device as D
+    from prysm_amd import parallel as P
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n, item_len = 1 << args.log2n, args.item_len
+    sp = P.plan(n, item_len, world)
+    lo, hi = sp.items(rank)
+    local_n = hi - lo
+    nbytes = local_n * item_len
+    items = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
+    if nbytes:
+        assert (lo * item_len) % 8 == 0 and nbytes % 8 == 0
+        D.synth_fill(items[:nbytes], SEED, word0=lo * item_len // 8)
+    ws = D.subtree_workspace(local_n, item_len, dev) if sp.nonempty > 1 else D.merkle_workspace(n, item_len, dev)
+    root_buf = torch.empty(32, dtype=torch.uint8, device=dev)
+    gather_buf = torch.empty(world * 32, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    log(f"rank {rank}/{world}: {local_n} items ({nbytes / 2**30:.2f} GiB), shard height {sp.height}, "
+        f"nonempty {sp.nonempty}")
+
+    def step():
+        return P.sharded_merkle_hash(
+            items, n, item_len, sp, rank, world,
+            subtree_fn=lambda it, sn, il, h, pad: D.merkle_subtree(it, sn, il, h, pad, out=root_buf, ws=ws),
+            full_fn=lambda it, nn, il: D.merkle_hash(it, nn, il, out=root_buf, ws=ws),
+            finish_fn=lambda g, nr, nt: D.merkle_finish(g, nr, nt),
+            gather_buf=gather_buf)
+
+    for i in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    root_hex = None
+
+    D.prof_enable(True)
+    D.prof_read()  # reset
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last_log = t0
+    for i in range(args.steps):
+        r = step()
+        if time.perf_counter() - last_log > 30:
+            log(f"step {i + 1}/{args.steps}")
+            last_log = time.perf_counter()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    D.prof_enable(False)
+    leaf_ms, leaf_launches, leaf_perms = D.prof_read()
+    if rank == 0 and r is not None:
+        root_hex = bytes(r.cpu().numpy()).hex()
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t_max = t.item()
+
+    if rank == 0:
+        value = n * args.steps / t_max
+        avg_leaf_s = (leaf_ms / 1e3) / max(leaf_launches, 1)
+        perms_per_launch = leaf_perms / max(leaf_launches, 1)
+        achieved = perms_per_launch * INT_OPS_PER_PERM / avg_leaf_s if avg_leaf_s > 0 else 0.0
+        traffic = load_pmc_traffic() if world == 1 and args.log2n == 28 else None
+        out = {
+            "metric": "tree-hash leaves/sec @2^28 chunks (ssz.merkleHash, 32-B leaves)",
+            "value": value,
+            "unit": "leaves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u64 (Keccak lanes as u32 pairs)",
+            "data": "synthetic (device SplitMix64, seed 0x5EED000000000004)",
+            "config": {"workload": f"C4: ssz.merkleHash of 2^{args.log2n} x {item_len}-B items "
+                                   f"({n * item_len / 2**30:.0f} GiB), subtree-sharded",
+                       "n_items": n, "item_len": item_len, "parallelism": f"subtree{world}",
+                       "shard_height": sp.height, "root": root_hex},
+            "roofline": {
+                "bound": "valu-int",
+                "kernel": "k_reduce<LEAF> (leaf pass: 256-B windows + 4 fused levels)",
+                "achieved": achieved / 1e12,
+                "peak": PEAK_INT_OPS / 1e12,
+                "unit": "Tops/s (int32 VALU)",
+                "frac": achieved / PEAK_INT_OPS,
+                "traffic": traffic,
+                "perms_per_launch": perms_per_launch,
+                "avg_launch_ms": avg_leaf_s * 1e3,
+                "hbm_GBps_algorithmic": (local_n * item_len) / avg_leaf_s / 1e9 if avg_leaf_s > 0 else None,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("timing CPU baseline ...")
+            out["cpu_baseline"] = cpu_baseline(item_len, args.cpu_sample_log2n)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

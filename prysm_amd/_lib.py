@@ -1,0 +1,103 @@
+"""ctypes binding of libprysm_merkle.so (include/prysm_merkle.h).
+
+This is the Python-side twin of the cgo binding a Go maintainer would add
+(INTEGRATION.md).  The library is built in-tree (``prysm_amd/lib/``) by
+``__graft_entry__.build()`` / ``make -C prysm_amd/csrc``.  There is no CPU
+fallback anywhere in the product path: if the library is missing, or no
+gfx950 device is visible, calls raise ``MerkleError`` loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libprysm_merkle.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "prysm_merkle.h")
+
+MK_OK = 0
+MK_EINVAL = -22
+MK_ENODEV = -19
+MK_ENOMEM = -12
+MK_EHIP = -5
+MK_ECOMM = -71
+
+
+class MerkleError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{msg} (code {code})")
+        self.code = code
+
+
+_c = ctypes
+_vp = _c.c_void_p
+_u64, _u32, _int = _c.c_uint64, _c.c_uint32, _c.c_int
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "mk_init": (_int, [_int]),
+    "mk_device_count": (_int, []),
+    "mk_strerror": (_c.c_char_p, [_int]),
+    "mk_last_error": (_c.c_char_p, []),
+    "mk_version": (_c.c_char_p, []),
+    "mk_hash": (_int, [_vp, _u64, _vp]),
+    "mk_hash_batch": (_int, [_vp, _u64, _u32, _vp]),
+    "mk_hash_batch_var": (_int, [_vp, _vp, _u64, _vp]),
+    "mk_dev_hash_batch": (_int, [_vp, _u64, _u32, _vp, _vp]),
+    "mk_dev_hash_batch_var": (_int, [_vp, _vp, _u64, _vp, _vp]),
+    "mk_ssz_merkle_hash": (_int, [_vp, _u64, _u32, _vp]),
+    "mk_ssz_merkle_workspace_bytes": (_u64, [_u64, _u32]),
+    "mk_dev_ssz_merkle_hash": (_int, [_vp, _u64, _u32, _vp, _vp, _u64, _vp]),
+    "mk_ssz_merkle_shard_plan": (_int, [_u64, _u32, _u32, _vp, _vp, _vp]),
+    "mk_dev_ssz_merkle_subtree": (_int, [_vp, _u64, _u32, _u32, _int, _vp, _vp, _u64, _vp]),
+    "mk_dev_ssz_merkle_finish": (_int, [_vp, _u64, _u64, _vp, _vp]),
+    "mk_ssz_merkle_hash_multi": (_int, [_vp, _u64, _u32, _int, _vp]),
+    "mk_deposit_trie_levels_bytes": (_u64, [_u64, _u32]),
+    "mk_deposit_trie_build": (_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
+    "mk_verify_merkle_branches": (_int, [_vp, _vp, _vp, _u64, _u32, _u32, _vp, _vp]),
+    "mk_dev_synth_fill": (_int, [_vp, _u64, _u64, _u64, _vp]),
+    "mk_prof_enable": (_int, [_int]),
+    "mk_prof_read": (_int, [_vp, _vp, _vp]),
+}
+
+_lib = None
+
+
+def header_symbols():
+    """Every mk_* function declared in include/prysm_merkle.h."""
+    with open(HEADER) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|const char\*)\s+(mk_[a-z0-9_]+)\s*\(", txt, re.M)))
+
+
+def load():
+    """Load the HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MerkleError(MK_ENODEV, f"{LIB_PATH} missing: run __graft_entry__.build() "
+                                     "(no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != MK_OK:
+        L = load()
+        detail = L.mk_last_error().decode(errors="replace")
+        raise MerkleError(rc, f"{what}: {L.mk_strerror(rc).decode()}: {detail}")
+
+
+def device_count() -> int:
+    return load().mk_device_count()
+
+
+def init(device: int = 0) -> None:
+    check(load().mk_init(device), "mk_init")

@@ -1,0 +1,692 @@
+// C-ABI of the MI355X Merkleization engine: device management, the
+// merkleHash pass planner, and the host/device entry points declared in
+// include/prysm_merkle.h.  Compiled with hipcc into libprysm_merkle.so.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "merkle_kernels.hpp"
+#include "prysm_merkle.h"
+
+namespace {
+
+using mk::ReduceArgs;
+using mk::kReduceSpan1;
+using mk::kReduceThreads;
+
+thread_local std::string t_err;
+thread_local int t_dev = -1;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    return code;
+}
+
+#define HIPCHK(x)                                                                            \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) return fail(MK_EHIP, "%s: %s", #x, hipGetErrorString(e_));     \
+    } while (0)
+
+// ---- devices ---------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+struct DevCtx {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    DevBuf in, out, ws, aux, aux2;
+};
+
+std::mutex g_mu;
+int g_ndev = -1;
+std::vector<DevCtx*> g_ctx;
+
+int probe_devices() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ndev >= 0) return g_ndev;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    int good = 0;
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d) != hipSuccess) break;
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) break;  // gfx950 only
+        ++good;
+    }
+    g_ndev = good;
+    g_ctx.resize(good, nullptr);
+    return g_ndev;
+}
+
+int bind(int dev) {
+    if (probe_devices() <= 0) return fail(MK_ENODEV, "no gfx950 device visible");
+    if (dev < 0) dev = t_dev >= 0 ? t_dev : 0;
+    if (dev >= g_ndev) return fail(MK_ENODEV, "device %d out of range (%d visible)", dev, g_ndev);
+    HIPCHK(hipSetDevice(dev));
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!g_ctx[dev]) {
+            auto* c = new DevCtx();
+            if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+                delete c;
+                return fail(MK_EHIP, "hipStreamCreate failed on device %d", dev);
+            }
+            g_ctx[dev] = c;
+        }
+    }
+    t_dev = dev;
+    return MK_OK;
+}
+
+int grow(DevBuf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return MK_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    if (hipMalloc(&b.p, bytes) != hipSuccess) return fail(MK_ENOMEM, "hipMalloc(%zu) failed", bytes);
+    b.cap = bytes;
+    return MK_OK;
+}
+
+#define TRY(x)                      \
+    do {                            \
+        int rc_ = (x);              \
+        if (rc_ != MK_OK) return rc_; \
+    } while (0)
+
+// ---- measurement -------------------------------------------------------------
+struct ProfRec {
+    hipEvent_t a, b;
+    double perms;
+};
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfRec> g_prof;
+
+// ---- merkleHash planner ---------------------------------------------------------
+uint64_t chunk_bytes(uint32_t item_len) {
+    return item_len < 128 ? (uint64_t)(128 / item_len) * item_len : item_len;
+}
+uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+uint64_t perms_for_len(uint64_t len) { return len / 136 + 1; }
+
+struct Pass {
+    bool leaf;
+    uint64_t nwg, nfast;
+    ReduceArgs a;
+    int in_ws;   // -1 = user input, else ping-pong slot
+    int out_ws;  // -1 = user output, else ping-pong slot
+    double perms;
+};
+
+struct Plan {
+    bool small = false;  // <= 1 chunk: one final hash of the raw bytes
+    std::vector<Pass> passes;
+    uint64_t slot_nodes[2] = {0, 0};
+    uint64_t total = 0, n = 0;
+};
+
+// Hashing levels from `count` nodes down to one (reference loop length).
+uint32_t levels_to_one(uint64_t count) {
+    uint32_t l = 0;
+    while (count > 1) {
+        count = (count + 1) / 2;
+        ++l;
+    }
+    return l;
+}
+
+// Builds the pass sequence.  subtree=false: full merkleHash with the length
+// mix-in; subtree=true: exactly `height` levels above the chunks, output one
+// node (pad_at_one keeps the odd rule alive at count 1).
+int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool pad_at_one,
+              bool aligned16, Plan& p) {
+    p = Plan();
+    p.n = n;
+    if (n > 0 && item_len == 0) return fail(MK_EINVAL, "item_len == 0 (reference: integer divide by zero)");
+    const uint64_t total = n * (uint64_t)item_len;
+    const uint64_t cb = n ? chunk_bytes(item_len) : 128;
+    const uint64_t nchunks = n ? ceil_div(total, cb) : 0;
+    p.total = total;
+    if (!subtree && nchunks <= 1) {
+        p.small = true;
+        return MK_OK;
+    }
+    if (subtree && (height == 0 || nchunks == 0 || nchunks > (1ull << height)))
+        return fail(MK_EINVAL, "subtree: bad height %u for %llu chunks", height, (unsigned long long)nchunks);
+
+    uint32_t remaining = subtree ? height : levels_to_one(nchunks);
+    bool leaf = true;
+    uint64_t cin = nchunks;  // leaf: chunks; node: input nodes
+    int slot = 0;
+    int in_slot = -1;
+    while (true) {
+        Pass ps{};
+        ps.leaf = leaf;
+        ReduceArgs& a = ps.a;
+        const uint64_t c1 = (cin > 1 || pad_at_one) ? ceil_div(cin, 2) : 1;
+        a.c1 = c1;
+        a.pad_at_one = pad_at_one ? 1 : 0;
+        a.n_items = n;
+        if (leaf) {
+            a.total = total;
+            a.cb = cb;
+            a.nchunks = nchunks;
+            a.c1_full = (cb == 128 && aligned16) ? total / 256 : 0;
+        } else {
+            a.cin = cin;
+            a.c1_full = cin / 2;
+        }
+        // algorithmic permutations of this pass (first level + fused levels)
+        double perms = 0;
+        if (leaf) {
+            const uint64_t full = total / (2 * cb);
+            perms += (double)std::min<uint64_t>(full, c1) * perms_for_len(2 * cb);
+            for (uint64_t j = full; j < c1; ++j) {  // at most one ragged window
+                const uint64_t lo = j * 2 * cb;
+                const uint64_t len = (2 * j + 1 < nchunks) ? std::min(total, lo + 2 * cb) - lo : total - lo + 128;
+                perms += (double)perms_for_len(len);
+            }
+        } else if (cin > 1 || pad_at_one) {
+            perms += (double)(cin / 2) + (cin % 2 ? 2.0 : 0.0);
+        }
+        uint64_t c = c1;
+        const bool final_pass = c1 <= kReduceSpan1;
+        uint32_t lv = final_pass ? remaining : std::min<uint32_t>(mk::kMaxPassLevels, remaining);
+        for (uint32_t l = 1; l < lv; ++l) {  // fused levels above the first
+            if (c <= 1 && !pad_at_one) break;
+            perms += (double)(c / 2) + (c % 2 ? 2.0 : 0.0);
+            c = ceil_div(c, 2);
+        }
+        ps.perms = perms;
+        a.levels = lv;
+        ps.nwg = ceil_div(c1, kReduceSpan1);
+        ps.nfast = std::min<uint64_t>(ps.nwg, a.c1_full / kReduceSpan1);
+        ps.in_ws = in_slot;
+        if (final_pass) {
+            if (!subtree) {
+                a.finalize = 1;
+                a.levels = 64;
+            } else if (c1 > kReduceSpan1 / 2 && lv < 2) {
+                return fail(MK_EINVAL, "planner: unsupported single-level pass");
+            }
+            ps.out_ws = -1;
+            p.passes.push_back(ps);
+            break;
+        }
+        ps.out_ws = slot;
+        p.slot_nodes[slot] = std::max<uint64_t>(p.slot_nodes[slot], c);
+        p.passes.push_back(ps);
+        remaining -= lv;
+        in_slot = slot;
+        slot ^= 1;
+        leaf = false;
+        cin = c;
+        if (remaining == 0) return fail(MK_EINVAL, "planner: ran out of levels");
+    }
+    return MK_OK;
+}
+
+uint64_t plan_ws_bytes(const Plan& p) { return 32 * (p.slot_nodes[0] + p.slot_nodes[1]) + 256; }
+
+int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t* d_ws, uint64_t ws_bytes,
+                hipStream_t st) {
+    if (p.small) {
+        hipLaunchKernelGGL(mk::k_final_small, dim3(1), dim3(64), 0, st, d_items, p.total, p.n, d_out32);
+        HIPCHK(hipGetLastError());
+        return MK_OK;
+    }
+    if (ws_bytes < plan_ws_bytes(p)) return fail(MK_ENOMEM, "workspace too small: %llu < %llu",
+                                                 (unsigned long long)ws_bytes, (unsigned long long)plan_ws_bytes(p));
+    uint8_t* slots[2] = {d_ws, d_ws + 32 * p.slot_nodes[0]};
+    bool prof;
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        prof = g_prof_on;
+    }
+    for (const Pass& ps : p.passes) {
+        ReduceArgs a = ps.a;
+        a.items = ps.in_ws < 0 ? d_items : slots[ps.in_ws];
+        a.out = ps.out_ws < 0 ? d_out32 : slots[ps.out_ws];
+        ProfRec rec{};
+        const bool rec_this = prof && ps.leaf;
+        if (rec_this) {
+            HIPCHK(hipEventCreate(&rec.a));
+            HIPCHK(hipEventCreate(&rec.b));
+            HIPCHK(hipEventRecord(rec.a, st));
+        }
+        if (ps.nfast) {
+            a.wg_base = 0;
+            if (ps.leaf)
+                hipLaunchKernelGGL((mk::k_reduce<true, true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+            else
+                hipLaunchKernelGGL((mk::k_reduce<false, true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+            HIPCHK(hipGetLastError());
+        }
+        if (ps.nwg > ps.nfast) {
+            a.wg_base = ps.nfast;
+            if (ps.leaf)
+                hipLaunchKernelGGL((mk::k_reduce<true, false>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads), 0,
+                                   st, a);
+            else
+                hipLaunchKernelGGL((mk::k_reduce<false, false>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads), 0,
+                                   st, a);
+            HIPCHK(hipGetLastError());
+        }
+        if (rec_this) {
+            HIPCHK(hipEventRecord(rec.b, st));
+            rec.perms = ps.perms;
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            g_prof.push_back(rec);
+        }
+    }
+    return MK_OK;
+}
+
+struct Locked {
+    DevCtx* c;
+    std::unique_lock<std::mutex> lk;
+};
+
+int lock_current(Locked& L) {
+    TRY(bind(-1));
+    L.c = g_ctx[t_dev];
+    L.lk = std::unique_lock<std::mutex>(L.c->mu);
+    return MK_OK;
+}
+
+int shard_plan(uint64_t n, uint32_t item_len, uint32_t nshards, uint32_t* height, uint32_t* nonempty,
+               uint64_t* begin) {
+    if (nshards == 0) return fail(MK_EINVAL, "nshards == 0");
+    if (n > 0 && item_len == 0) return fail(MK_EINVAL, "item_len == 0");
+    const uint64_t total = n * (uint64_t)item_len;
+    const uint64_t cb = n ? chunk_bytes(item_len) : 128;
+    const uint64_t per_chunk_items = item_len < 128 ? 128 / item_len : 1;
+    const uint64_t nchunks = n ? ceil_div(total, cb) : 0;
+    uint32_t h = 0;
+    while ((1ull << h) * nshards < nchunks) ++h;
+    uint64_t ne = nchunks ? ceil_div(nchunks, 1ull << h) : 0;
+    if (h == 0 || ne <= 1) {  // too small to shard: everything on shard 0
+        *height = h;
+        *nonempty = 1;
+        for (uint32_t s = 0; s <= nshards; ++s) begin[s] = s == 0 ? 0 : n;
+        return MK_OK;
+    }
+    *height = h;
+    *nonempty = (uint32_t)ne;
+    for (uint32_t s = 0; s <= nshards; ++s) {
+        const uint64_t item = (uint64_t)s * (1ull << h) * per_chunk_items;
+        begin[s] = item < n ? item : n;
+    }
+    return MK_OK;
+}
+
+}  // namespace
+
+// =============================================================================
+extern "C" {
+
+const char* mk_version(void) { return "prysm_merkle 0.1 (gfx950)"; }
+
+const char* mk_strerror(int code) {
+    switch (code) {
+        case MK_OK: return "ok";
+        case MK_EINVAL: return "invalid argument";
+        case MK_ENODEV: return "no usable gfx950 device";
+        case MK_ENOMEM: return "out of memory";
+        case MK_EHIP: return "HIP runtime error";
+        case MK_ECOMM: return "RCCL error";
+        default: return "unknown error";
+    }
+}
+
+const char* mk_last_error(void) { return t_err.c_str(); }
+
+int mk_device_count(void) { return probe_devices(); }
+
+int mk_init(int device) { return bind(device < 0 ? 0 : device); }
+
+// ---- hashing ------------------------------------------------------------------
+int mk_dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, void* stream) {
+    TRY(bind(-1));
+    if (n == 0) return MK_OK;
+    if (!d_in || !d_out) return fail(MK_EINVAL, "null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    const uint64_t grid = ceil_div(n, 256);
+    if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0)
+        hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
+    else
+        hipLaunchKernelGGL(mk::k_keccak_fixed, dim3(grid), dim3(256), 0, st, (const uint8_t*)d_in, n, msg_len,
+                           (uint4*)d_out);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
+int mk_dev_hash_batch_var(const void* d_in, const uint64_t* d_offs, uint64_t n, void* d_out, void* stream) {
+    TRY(bind(-1));
+    if (n == 0) return MK_OK;
+    hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t*)d_in, d_offs, n, (uint4*)d_out);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
+int mk_hash_batch(const uint8_t* in, uint64_t n, uint32_t msg_len, uint8_t* out) {
+    if (n && (!in && msg_len) ) return fail(MK_EINVAL, "null input");
+    if (n && !out) return fail(MK_EINVAL, "null output");
+    Locked L;
+    TRY(lock_current(L));
+    if (n == 0) return MK_OK;
+    const size_t inb = n * (size_t)msg_len;
+    TRY(grow(L.c->in, inb));
+    TRY(grow(L.c->out, 32 * n));
+    hipStream_t st = L.c->stream;
+    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, in, inb, hipMemcpyHostToDevice, st));
+    TRY(mk_dev_hash_batch(L.c->in.p, n, msg_len, L.c->out.p, st));
+    HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+int mk_hash(const uint8_t* data, uint64_t len, uint8_t out[32]) {
+    if (len > UINT32_MAX) {
+        uint64_t offs[2] = {0, len};
+        return mk_hash_batch_var(data, offs, 1, out);
+    }
+    static const uint8_t empty = 0;
+    return mk_hash_batch(len ? data : &empty, 1, (uint32_t)len, out);
+}
+
+int mk_hash_batch_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint8_t* out) {
+    if (n && (!offs || !out)) return fail(MK_EINVAL, "null pointer");
+    Locked L;
+    TRY(lock_current(L));
+    if (n == 0) return MK_OK;
+    const size_t inb = offs[n];
+    TRY(grow(L.c->in, inb));
+    TRY(grow(L.c->aux, 8 * (n + 1)));
+    TRY(grow(L.c->out, 32 * n));
+    hipStream_t st = L.c->stream;
+    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, in, inb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(L.c->aux.p, offs, 8 * (n + 1), hipMemcpyHostToDevice, st));
+    TRY(mk_dev_hash_batch_var(L.c->in.p, (const uint64_t*)L.c->aux.p, n, L.c->out.p, st));
+    HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+// ---- merkleHash ---------------------------------------------------------------
+uint64_t mk_ssz_merkle_workspace_bytes(uint64_t n, uint32_t item_len) {
+    Plan p;
+    if (make_plan(n, item_len, false, 0, false, true, p) != MK_OK) return 0;
+    return p.small ? 256 : plan_ws_bytes(p);
+}
+
+int mk_dev_ssz_merkle_hash(const void* d_items, uint64_t n, uint32_t item_len, void* d_out32, void* d_ws,
+                           uint64_t ws_bytes, void* stream) {
+    TRY(bind(-1));
+    if (!d_out32 || (n && !d_items)) return fail(MK_EINVAL, "null pointer");
+    Plan p;
+    TRY(make_plan(n, item_len, false, 0, false, ((uintptr_t)d_items % 16) == 0, p));
+    return launch_plan(p, (const uint8_t*)d_items, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes,
+                       (hipStream_t)stream);
+}
+
+int mk_ssz_merkle_hash(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t out[32]) {
+    if (!out || (n && item_len && !items)) return fail(MK_EINVAL, "null pointer");
+    Locked L;
+    TRY(lock_current(L));
+    Plan p;
+    TRY(make_plan(n, item_len, false, 0, false, true, p));
+    const size_t inb = n * (size_t)item_len;
+    TRY(grow(L.c->in, inb));
+    TRY(grow(L.c->out, 32));
+    TRY(grow(L.c->ws, p.small ? 256 : plan_ws_bytes(p)));
+    hipStream_t st = L.c->stream;
+    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, items, inb, hipMemcpyHostToDevice, st));
+    TRY(launch_plan(p, (const uint8_t*)L.c->in.p, (uint8_t*)L.c->out.p, (uint8_t*)L.c->ws.p, L.c->ws.cap, st));
+    HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+// ---- sharding -------------------------------------------------------------------
+int mk_ssz_merkle_shard_plan(uint64_t n, uint32_t item_len, uint32_t nshards, uint32_t* height,
+                             uint32_t* nonempty, uint64_t* item_begin) {
+    if (!height || !nonempty || !item_begin) return fail(MK_EINVAL, "null pointer");
+    return shard_plan(n, item_len, nshards, height, nonempty, item_begin);
+}
+
+int mk_dev_ssz_merkle_subtree(const void* d_shard_items, uint64_t shard_n, uint32_t item_len, uint32_t height,
+                              int pad_at_one, void* d_out32, void* d_ws, uint64_t ws_bytes, void* stream) {
+    TRY(bind(-1));
+    Plan p;
+    TRY(make_plan(shard_n, item_len, true, height, pad_at_one != 0, ((uintptr_t)d_shard_items % 16) == 0, p));
+    return launch_plan(p, (const uint8_t*)d_shard_items, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes,
+                       (hipStream_t)stream);
+}
+
+int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32, void* stream) {
+    TRY(bind(-1));
+    if (nroots == 0 || nroots > mk::kReduceSpan2) return fail(MK_EINVAL, "nroots %llu out of range",
+                                                                  (unsigned long long)nroots);
+    hipLaunchKernelGGL(mk::k_finish_roots, dim3(1), dim3(kReduceThreads), 0, (hipStream_t)stream,
+                       (const uint4*)d_roots, nroots, n_total, (uint4*)d_out32);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
+int mk_ssz_merkle_hash_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int ndev, uint8_t out[32]) {
+    if (ndev <= 1) return mk_ssz_merkle_hash(items, n, item_len, out);
+    if (probe_devices() < ndev) return fail(MK_ENODEV, "%d devices requested, %d visible", ndev, g_ndev);
+    uint32_t h = 0, ne = 0;
+    std::vector<uint64_t> begin(ndev + 1);
+    TRY(shard_plan(n, item_len, (uint32_t)ndev, &h, &ne, begin.data()));
+    if (ne <= 1) return mk_ssz_merkle_hash(items, n, item_len, out);
+
+    static std::mutex comm_mu;
+    static std::vector<ncclComm_t> comms;
+    std::lock_guard<std::mutex> clk(comm_mu);
+    if ((int)comms.size() != ndev) {
+        for (auto c : comms) ncclCommDestroy(c);
+        comms.assign(ndev, nullptr);
+        std::vector<int> devs(ndev);
+        for (int d = 0; d < ndev; ++d) devs[d] = d;
+        if (ncclCommInitAll(comms.data(), ndev, devs.data()) != ncclSuccess) {
+            comms.clear();
+            return fail(MK_ECOMM, "ncclCommInitAll(%d) failed", ndev);
+        }
+    }
+    std::vector<std::unique_lock<std::mutex>> locks;
+    std::vector<DevCtx*> ctx(ndev);
+    for (int d = 0; d < ndev; ++d) {
+        TRY(bind(d));
+        ctx[d] = g_ctx[d];
+        locks.emplace_back(ctx[d]->mu);
+    }
+    // per device: shard upload + subtree reduce into roots slot `d`
+    for (int d = 0; d < ndev; ++d) {
+        TRY(bind(d));
+        DevCtx* c = ctx[d];
+        const uint64_t sn = begin[d + 1] - begin[d];
+        const size_t inb = sn * (size_t)item_len;
+        TRY(grow(c->in, inb));
+        TRY(grow(c->out, 32 * (size_t)ndev + 32));
+        uint8_t* roots = (uint8_t*)c->out.p;
+        if (sn) {
+            Plan p;
+            TRY(make_plan(sn, item_len, true, h, true, true, p));
+            TRY(grow(c->ws, plan_ws_bytes(p)));
+            HIPCHK(hipMemcpyAsync(c->in.p, items + begin[d] * item_len, inb, hipMemcpyHostToDevice, c->stream));
+            TRY(launch_plan(p, (const uint8_t*)c->in.p, roots + 32 * d, (uint8_t*)c->ws.p, c->ws.cap, c->stream));
+        } else {
+            HIPCHK(hipMemsetAsync(roots + 32 * d, 0, 32, c->stream));
+        }
+    }
+    // gather the 32-B shard roots over RCCL (in place: slot d of every device)
+    if (ncclGroupStart() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupStart");
+    for (int d = 0; d < ndev; ++d) {
+        uint8_t* roots = (uint8_t*)ctx[d]->out.p;
+        if (ncclAllGather(roots + 32 * d, roots, 32, ncclUint8, comms[d], ctx[d]->stream) != ncclSuccess) {
+            ncclGroupEnd();
+            return fail(MK_ECOMM, "ncclAllGather on device %d", d);
+        }
+    }
+    if (ncclGroupEnd() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupEnd");
+    TRY(bind(0));
+    uint8_t* roots0 = (uint8_t*)ctx[0]->out.p;
+    TRY(mk_dev_ssz_merkle_finish(roots0, ne, n, roots0 + 32 * ndev, ctx[0]->stream));
+    HIPCHK(hipMemcpyAsync(out, roots0 + 32 * ndev, 32, hipMemcpyDeviceToHost, ctx[0]->stream));
+    for (int d = 0; d < ndev; ++d) {
+        TRY(bind(d));
+        HIPCHK(hipStreamSynchronize(ctx[d]->stream));
+    }
+    TRY(bind(0));
+    return MK_OK;
+}
+
+// ---- deposit trie -------------------------------------------------------------------
+uint64_t mk_deposit_trie_levels_bytes(uint64_t n, uint32_t depth) {
+    if (n == 0) return 0;
+    uint64_t nodes = 0, c = n;
+    for (uint32_t d = 0; d <= depth; ++d) {
+        nodes += c;
+        c = (c + 1) / 2;
+    }
+    return 32 * nodes;
+}
+
+int mk_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
+                          uint8_t* levels_out, uint8_t root[32]) {
+    if (!root || (n && !offs)) return fail(MK_EINVAL, "null pointer");
+    if (depth > 63) return fail(MK_EINVAL, "depth %u > 63", depth);
+    Locked L;
+    TRY(lock_current(L));
+    if (n == 0) {
+        std::memset(root, 0, 32);
+        return MK_OK;
+    }
+    hipStream_t st = L.c->stream;
+    const size_t inb = offs[n];
+    const uint64_t lv_bytes = mk_deposit_trie_levels_bytes(n, depth);
+    TRY(grow(L.c->in, inb));
+    TRY(grow(L.c->aux, 8 * (n + 1)));
+    TRY(grow(L.c->ws, lv_bytes));
+    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, data, inb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(L.c->aux.p, offs, 8 * (n + 1), hipMemcpyHostToDevice, st));
+    uint4* lv = (uint4*)L.c->ws.p;
+    hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)L.c->in.p,
+                       (const uint64_t*)L.c->aux.p, n, lv);
+    HIPCHK(hipGetLastError());
+    uint64_t c = n;
+    uint4* cur = lv;
+    uint32_t d = 0;
+    while (d < depth && c > 1) {
+        uint4* nxt = cur + 2 * c;
+        const uint64_t cn = (c + 1) / 2;
+        hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(cn, 256)), dim3(256), 0, st, cur, c, nxt);
+        HIPCHK(hipGetLastError());
+        cur = nxt;
+        c = cn;
+        ++d;
+    }
+    uint4* root_node = cur;
+    if (d < depth) {  // single node left: (node || 0^32) up to the top
+        uint4* tail = cur + 2;
+        hipLaunchKernelGGL(mk::k_trie_tail, dim3(1), dim3(64), 0, st, cur, depth - d, tail);
+        HIPCHK(hipGetLastError());
+        root_node = tail + 2 * (depth - d - 1);
+    }
+    HIPCHK(hipMemcpyAsync(root, root_node, 32, hipMemcpyDeviceToHost, st));
+    if (levels_out) HIPCHK(hipMemcpyAsync(levels_out, lv, lv_bytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+int mk_verify_merkle_branches(const uint8_t* leaves, const uint8_t* branches, const uint64_t* indices, uint64_t n,
+                              uint32_t depth, uint32_t tree_depth, const uint8_t* roots, uint8_t* ok) {
+    if (n && (!leaves || !indices || !roots || !ok || (depth && !branches))) return fail(MK_EINVAL, "null pointer");
+    Locked L;
+    TRY(lock_current(L));
+    if (n == 0) return MK_OK;
+    hipStream_t st = L.c->stream;
+    const size_t bb = 32 * (size_t)depth * n;
+    TRY(grow(L.c->in, bb + 64 * n + 16));
+    TRY(grow(L.c->aux, 8 * n));
+    TRY(grow(L.c->out, n));
+    uint8_t* base = (uint8_t*)L.c->in.p;
+    uint8_t* d_leaves = base;
+    uint8_t* d_roots = base + 32 * n;
+    uint8_t* d_br = base + 64 * n;
+    HIPCHK(hipMemcpyAsync(d_leaves, leaves, 32 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_roots, roots, 32 * n, hipMemcpyHostToDevice, st));
+    if (bb) HIPCHK(hipMemcpyAsync(d_br, branches, bb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(L.c->aux.p, indices, 8 * n, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(mk::k_verify_branches, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint4*)d_leaves,
+                       (const uint4*)d_br, (const uint64_t*)L.c->aux.p, depth, tree_depth, (const uint4*)d_roots, n,
+                       (uint8_t*)L.c->out.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(ok, L.c->out.p, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+// ---- synthetic inputs -------------------------------------------------------------
+int mk_dev_synth_fill(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t word0, void* stream) {
+    TRY(bind(-1));
+    if (nbytes % 8) return fail(MK_EINVAL, "nbytes %% 8 != 0");
+    if ((uintptr_t)d_dst % 8) return fail(MK_EINVAL, "destination not 8-byte aligned");
+    const uint64_t nwords = nbytes / 8;
+    if (!nwords) return MK_OK;
+    const uint64_t grid = std::min<uint64_t>(ceil_div(nwords, 256), 256 * 64);
+    hipLaunchKernelGGL(mk::k_synth, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint64_t*)d_dst, nwords, seed,
+                       word0);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
+// ---- measurement ----------------------------------------------------------------------
+int mk_prof_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_on = on != 0;
+    return MK_OK;
+}
+
+int mk_prof_read(double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms) {
+    std::vector<ProfRec> recs;
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        recs.swap(g_prof);
+    }
+    double ms = 0, perms = 0;
+    for (auto& r : recs) {
+        HIPCHK(hipEventSynchronize(r.b));
+        float t = 0;
+        HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
+        ms += t;
+        perms += r.perms;
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    if (leaf_ms) *leaf_ms = ms;
+    if (leaf_launches) *leaf_launches = recs.size();
+    if (leaf_perms) *leaf_perms = perms;
+    return MK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,182 @@
+// Keccak-f[1600] for gfx950 (CDNA4), one permutation state per lane.
+//
+// Replaces the digest under shared/hashutil/hash.go:11-25 (legacy
+// Keccak-256 from golang.org/x/crypto/sha3 @ b8fe1690c613: rate 136 B,
+// pad 0x01 .. 0x80, 24 rounds).
+//
+// Layout: the 25 64-bit lanes live in 50 VGPRs as (lo, hi) 32-bit halves.
+// Every instruction is an integer VALU op chosen for the gfx950 ISA:
+//   theta column parity  2 x v_bitop3_b32 (xor3, LUT 0x96) per half
+//   theta D rotation     2 x v_alignbit_b32 per column
+//   theta apply          1 x v_bitop3_b32 (a ^ c[x-1] ^ rot(c[x+1])) per half
+//   rho                  2 x v_alignbit_b32 per lane (no offset is 0 mod 32
+//                        except lane 0, which is free)
+//   pi                   register renaming (no instructions)
+//   chi                  1 x v_bitop3_b32 (a ^ (~b & c), LUT 0xD2) per half
+//   iota                 <= 2 x v_xor_b32 with a scalar round constant
+// = 180 VALU per round, 4320 per permutation (BASELINE.md §2 op model).
+// hipcc does not select bitop3/alignbit from plain C++, so
+// the builtins are used explicitly.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mk {
+
+__constant__ uint32_t kRcLo[24] = {
+    0x00000001u, 0x00008082u, 0x0000808Au, 0x80008000u, 0x0000808Bu, 0x80000001u,
+    0x80008081u, 0x00008009u, 0x0000008Au, 0x00000088u, 0x80008009u, 0x8000000Au,
+    0x8000808Bu, 0x0000008Bu, 0x00008089u, 0x00008003u, 0x00008002u, 0x00000080u,
+    0x0000800Au, 0x8000000Au, 0x80008081u, 0x00008080u, 0x80000001u, 0x80008008u};
+__constant__ uint32_t kRcHi[24] = {
+    0x00000000u, 0x00000000u, 0x80000000u, 0x80000000u, 0x00000000u, 0x00000000u,
+    0x80000000u, 0x80000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u,
+    0x00000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u,
+    0x00000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0x00000000u, 0x80000000u};
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// a ^ (~b & c): LUT index = (a << 2) | (b << 1) | c  ->  0b11010010
+__device__ __forceinline__ uint32_t chi3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xD2);
+}
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t s) {
+    return __builtin_amdgcn_alignbit(hi, lo, s);  // (hi:lo >> s)[31:0]
+}
+
+// 64-bit rotate-left by a compile-time N of the pair (lo, hi).
+template <int N>
+__device__ __forceinline__ void rotl64(uint32_t lo, uint32_t hi, uint32_t& olo, uint32_t& ohi) {
+    if constexpr (N == 0) {
+        olo = lo;
+        ohi = hi;
+    } else if constexpr (N == 32) {
+        olo = hi;
+        ohi = lo;
+    } else if constexpr (N < 32) {
+        ohi = funnel(hi, lo, 32 - N);
+        olo = funnel(lo, hi, 32 - N);
+    } else {
+        ohi = funnel(lo, hi, 64 - N);
+        olo = funnel(hi, lo, 64 - N);
+    }
+}
+
+struct State {
+    uint32_t lo[25];
+    uint32_t hi[25];
+};
+
+__device__ __forceinline__ void zero(State& s) {
+#pragma unroll
+    for (int i = 0; i < 25; ++i) {
+        s.lo[i] = 0u;
+        s.hi[i] = 0u;
+    }
+}
+
+// rho offsets r[x][y], lane index x + 5y
+#define MK_RHO(i)                                                                          \
+    ((i) == 0 ? 0 : (i) == 1 ? 1 : (i) == 2 ? 62 : (i) == 3 ? 28 : (i) == 4 ? 27          \
+   : (i) == 5 ? 36 : (i) == 6 ? 44 : (i) == 7 ? 6 : (i) == 8 ? 55 : (i) == 9 ? 20          \
+   : (i) == 10 ? 3 : (i) == 11 ? 10 : (i) == 12 ? 43 : (i) == 13 ? 25 : (i) == 14 ? 39    \
+   : (i) == 15 ? 41 : (i) == 16 ? 45 : (i) == 17 ? 15 : (i) == 18 ? 21 : (i) == 19 ? 8    \
+   : (i) == 20 ? 18 : (i) == 21 ? 2 : (i) == 22 ? 61 : (i) == 23 ? 56 : 14)
+
+template <int I>
+__device__ __forceinline__ void rho_pi_one(const State& a, uint32_t (&blo)[25], uint32_t (&bhi)[25]) {
+    constexpr int x = I % 5, y = I / 5;
+    constexpr int dst = y + 5 * ((2 * x + 3 * y) % 5);
+    rotl64<MK_RHO(I)>(a.lo[I], a.hi[I], blo[dst], bhi[dst]);
+}
+
+template <int... Is>
+__device__ __forceinline__ void rho_pi_all(const State& a, uint32_t (&blo)[25], uint32_t (&bhi)[25],
+                                           std::integer_sequence<int, Is...>) {
+    (rho_pi_one<Is>(a, blo, bhi), ...);
+}
+
+__device__ __forceinline__ void round_fn(State& s, uint32_t rclo, uint32_t rchi) {
+    uint32_t clo[5], chi_[5];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+        clo[x] = xor3(xor3(s.lo[x], s.lo[x + 5], s.lo[x + 10]), s.lo[x + 15], s.lo[x + 20]);
+        chi_[x] = xor3(xor3(s.hi[x], s.hi[x + 5], s.hi[x + 10]), s.hi[x + 15], s.hi[x + 20]);
+    }
+    uint32_t rlo[5], rhi[5];  // rotl(C[x], 1)
+#pragma unroll
+    for (int x = 0; x < 5; ++x) rotl64<1>(clo[x], chi_[x], rlo[x], rhi[x]);
+#pragma unroll
+    for (int i = 0; i < 25; ++i) {
+        const int x = i % 5;
+        s.lo[i] = xor3(s.lo[i], clo[(x + 4) % 5], rlo[(x + 1) % 5]);
+        s.hi[i] = xor3(s.hi[i], chi_[(x + 4) % 5], rhi[(x + 1) % 5]);
+    }
+    uint32_t blo[25], bhi[25];
+    rho_pi_all(s, blo, bhi, std::make_integer_sequence<int, 25>{});
+#pragma unroll
+    for (int y = 0; y < 5; ++y) {
+#pragma unroll
+        for (int x = 0; x < 5; ++x) {
+            const int i = x + 5 * y;
+            const int i1 = (x + 1) % 5 + 5 * y, i2 = (x + 2) % 5 + 5 * y;
+            s.lo[i] = chi3(blo[i], blo[i1], blo[i2]);
+            s.hi[i] = chi3(bhi[i], bhi[i1], bhi[i2]);
+        }
+    }
+    s.lo[0] ^= rclo;
+    s.hi[0] ^= rchi;
+}
+
+#ifndef MK_ROUND_UNROLL
+#define MK_ROUND_UNROLL 4
+#endif
+constexpr int kRoundUnroll = MK_ROUND_UNROLL;
+
+// The round loop is only partially unrolled: pi is a pure renaming and chi
+// writes the canonical lane positions, so a rolled loop needs no moves, and
+// one permutation stays ~6 KB of code instead of ~35 KB (several copies of
+// it live in one kernel).  Round constants come from the scalar cache.
+__device__ __forceinline__ void keccak_f(State& s) {
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < 24; ++r) round_fn(s, kRcLo[r], kRcHi[r]);
+}
+
+// ---- absorb helpers --------------------------------------------------------
+__device__ __forceinline__ void xor_lane(State& s, int i, uint2 w) {
+    s.lo[i] ^= w.x;
+    s.hi[i] ^= w.y;
+}
+
+// Final-block padding for legacy Keccak: byte `pos` (< 136) of the block gets
+// 0x01, byte 135 gets 0x80.  pos is a compile-time constant here.
+template <int POS>
+__device__ __forceinline__ void pad_const(State& s) {
+    constexpr int lane = POS / 8, sh = (POS % 8) * 8;
+    if constexpr (sh < 32)
+        s.lo[lane] ^= 1u << sh;
+    else
+        s.hi[lane] ^= 1u << (sh - 32);
+    s.hi[16] ^= 0x80000000u;
+}
+
+// Streaming (non-temporal) loads of input that is read exactly once.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 ld_nt(const uint2* p) {
+    const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+    return make_uint2(v.x, v.y);
+}
+
+// Squeeze the 32-byte digest (lanes 0..3, little-endian).
+__device__ __forceinline__ void digest(const State& s, uint4& d0, uint4& d1) {
+    d0 = make_uint4(s.lo[0], s.hi[0], s.lo[1], s.hi[1]);
+    d1 = make_uint4(s.lo[2], s.hi[2], s.lo[3], s.hi[3]);
+}
+
+}  // namespace mk

@@ -1,0 +1,497 @@
+// HIP kernels of the MI355X Merkleization engine (gfx950 only).
+//
+// Hot path: ssz.merkleHash (reference shared/ssz/hash.go:194-239) over a flat
+// array of n items of `item_len` bytes, plus the digest it is built on
+// (hashutil.Hash, shared/hashutil/hash.go:11-25) and the deposit trie
+// (shared/trieutil/deposit_trie.go:29-81).
+//
+// Tree shape of merkleHash, restated for a flat buffer:
+//   cb      = item_len < 128 ? (128 / item_len) * item_len : item_len
+//   chunk i = bytes [i*cb, min(total, (i+1)*cb))          (last may be short)
+//   level 1 = "windows": node j = K(chunk 2j || chunk 2j+1), or
+//             K(chunk 2j || 0^128) when 2j+1 == nchunks (odd count)
+//   level l>1: node j = K(n[2j] || n[2j+1]) or K(n[2j] || 0^128) when odd;
+//             a level with a single node is the root (no more hashing)
+//   final   = K(root || le64(n) || 0^24)
+// For item_len | 128 every window is 256 contiguous bytes of the input, so
+// level 1 is a pure streaming pass (2 Keccak blocks per window).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "keccak_dev.hpp"
+#include "merkle_kernels.hpp"
+
+namespace mk {
+
+// ----------------------------------------------------------------------------
+// Generic byte-addressed sponge (edge windows, odd sizes, var-len messages).
+// Message = A (global bytes [p, p+la)) || 0^lz || (lenc ? le64(nval)||0^24 : -)
+__device__ __noinline__ void sponge_generic(const uint8_t* __restrict__ p, uint64_t la, uint32_t lz,
+                                            bool lenc, uint64_t nval, uint4& d0, uint4& d1) {
+    const uint64_t len = la + lz + (lenc ? 32u : 0u);
+    const uint64_t nb = len / 136 + 1;
+    const bool aligned = (((uintptr_t)p) & 7u) == 0;
+    State s;
+    zero(s);
+    for (uint64_t b = 0; b < nb; ++b) {
+        const uint64_t base = b * 136;
+#pragma unroll
+        for (int w = 0; w < 17; ++w) {
+            const uint64_t m0 = base + 8u * w;
+            uint32_t lo = 0, hi = 0;
+            if (aligned && m0 + 8 <= la) {
+                const uint2 v = *reinterpret_cast<const uint2*>(p + m0);
+                lo = v.x;
+                hi = v.y;
+            } else if (m0 < len) {
+#pragma unroll 1
+                for (int k = 0; k < 8; ++k) {
+                    const uint64_t m = m0 + k;
+                    uint32_t byte = 0;
+                    if (m < la) {
+                        byte = p[m];
+                    } else if (m >= la + lz && m < len) {
+                        const uint64_t e = m - la - lz;  // lenc byte
+                        byte = e < 8 ? (uint32_t)((nval >> (8 * e)) & 0xFF) : 0u;
+                    }
+                    if (k < 4)
+                        lo |= byte << (8 * k);
+                    else
+                        hi |= byte << (8 * (k - 4));
+                }
+            }
+            if (m0 <= len && len < m0 + 8) {  // domain pad byte 0x01
+                const uint32_t k = (uint32_t)(len - m0);
+                if (k < 4)
+                    lo ^= 1u << (8 * k);
+                else
+                    hi ^= 1u << (8 * (k - 4));
+            }
+            if (b == nb - 1 && w == 16) hi ^= 0x80000000u;
+            s.lo[w] ^= lo;
+            s.hi[w] ^= hi;
+        }
+        keccak_f(s);
+    }
+    digest(s, d0, d1);
+}
+
+// K(L || R) (64 B, 1 permutation) or K(L || 0^128) (160 B, 2 permutations)
+// with a single keccak_f copy; `padded` may differ between lanes.
+__device__ __forceinline__ void hash_pair(uint4 l0, uint4 l1, uint4 r0, uint4 r1, bool padded,
+                                          uint4& d0, uint4& d1) {
+    State s;
+    zero(s);
+    xor_lane(s, 0, make_uint2(l0.x, l0.y));
+    xor_lane(s, 1, make_uint2(l0.z, l0.w));
+    xor_lane(s, 2, make_uint2(l1.x, l1.y));
+    xor_lane(s, 3, make_uint2(l1.z, l1.w));
+    if (!padded) {
+        xor_lane(s, 4, make_uint2(r0.x, r0.y));
+        xor_lane(s, 5, make_uint2(r0.z, r0.w));
+        xor_lane(s, 6, make_uint2(r1.x, r1.y));
+        xor_lane(s, 7, make_uint2(r1.z, r1.w));
+    }
+    const int nperm = padded ? 2 : 1;
+#pragma unroll 1
+    for (int r = 0; r < nperm; ++r) {
+        if (r == nperm - 1) {
+            if (padded)
+                s.lo[3] ^= 1u;  // byte 160 = byte 24 of block 1
+            else
+                s.lo[8] ^= 1u;  // byte 64
+            s.hi[16] ^= 0x80000000u;
+        }
+        keccak_f(s);
+    }
+    digest(s, d0, d1);
+}
+
+// K(root || le64(n) || 0^24)
+__device__ __forceinline__ void hash_final(uint4 r0, uint4 r1, uint64_t n, uint4& d0, uint4& d1) {
+    State s;
+    zero(s);
+    xor_lane(s, 0, make_uint2(r0.x, r0.y));
+    xor_lane(s, 1, make_uint2(r0.z, r0.w));
+    xor_lane(s, 2, make_uint2(r1.x, r1.y));
+    xor_lane(s, 3, make_uint2(r1.z, r1.w));
+    xor_lane(s, 4, make_uint2((uint32_t)n, (uint32_t)(n >> 32)));
+    s.lo[8] ^= 1u;
+    s.hi[16] ^= 0x80000000u;
+    keccak_f(s);
+    digest(s, d0, d1);
+}
+
+// ----------------------------------------------------------------------------
+// Fast 256-B window (two Keccak blocks).  The block loop is rolled so the
+// kernel keeps one keccak_f copy in its hot loop (I-cache).
+__device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint4& d0, uint4& d1) {
+    State s;
+    zero(s);
+#pragma unroll 1
+    for (int b = 0; b < 2; ++b) {
+        if (b == 0) {
+            uint4 v[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) v[k] = ld_nt(w + k);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                s.lo[2 * k] ^= v[k].x;
+                s.hi[2 * k] ^= v[k].y;
+                s.lo[2 * k + 1] ^= v[k].z;
+                s.hi[2 * k + 1] ^= v[k].w;
+            }
+            s.lo[16] ^= v[8].x;
+            s.hi[16] ^= v[8].y;
+        } else {
+            const uint2 t = ld_nt(reinterpret_cast<const uint2*>(w + 8) + 1);
+            uint4 v[7];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) v[k] = ld_nt(w + 9 + k);
+            s.lo[0] ^= t.x;
+            s.hi[0] ^= t.y;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) {
+                s.lo[1 + 2 * k] ^= v[k].x;
+                s.hi[1 + 2 * k] ^= v[k].y;
+                s.lo[2 + 2 * k] ^= v[k].z;
+                s.hi[2 + 2 * k] ^= v[k].w;
+            }
+            s.lo[15] ^= 1u;  // byte 256 = byte 120 of block 1
+            s.hi[16] ^= 0x80000000u;
+        }
+        keccak_f(s);
+    }
+    digest(s, d0, d1);
+}
+
+// ----------------------------------------------------------------------------
+// First-level node j of a reduce pass.
+//   LEAF: window j of the item buffer.
+//   NODE: pair j of the 32-B input nodes (count cin).
+template <bool LEAF>
+__device__ __forceinline__ void first_level_generic(const ReduceArgs& a, uint64_t j, uint4& d0, uint4& d1) {
+    if constexpr (LEAF) {
+        const uint64_t lo = j * 2 * a.cb;
+        uint64_t la;
+        uint32_t lz;
+        if (2 * j + 1 < a.nchunks) {
+            la = (lo + 2 * a.cb < a.total ? lo + 2 * a.cb : a.total) - lo;
+            lz = 0;
+        } else {
+            la = a.total - lo;
+            lz = 128;
+        }
+        sponge_generic(a.items + lo, la, lz, false, 0, d0, d1);
+    } else {
+        const uint4* in = reinterpret_cast<const uint4*>(a.items);
+        const uint4 l0 = in[4 * j], l1 = in[4 * j + 1];
+        if (a.cin == 1 && !a.pad_at_one) {  // single node: it is the root
+            d0 = l0;
+            d1 = l1;
+            return;
+        }
+        const bool padded = !(2 * j + 1 < a.cin);
+        uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+        if (!padded) {
+            r0 = in[4 * j + 2];
+            r1 = in[4 * j + 3];
+        }
+        hash_pair(l0, l1, r0, r1, padded, d0, d1);
+    }
+}
+
+// One fused reduce pass.  256 threads; the workgroup owns first-level nodes
+// [1024*wg, 1024*wg+1024), folds them pairwise in registers into 512
+// level-2 nodes in LDS, then reduces further levels in LDS (one node per
+// thread per level, read -> barrier -> permute -> write -> barrier).
+// Non-final passes write 512 >> (levels-2) nodes per workgroup; the final
+// pass (one workgroup) reduces to the root and applies the length mix-in.
+template <bool LEAF, bool FAST>
+__global__ __launch_bounds__(kReduceThreads) void k_reduce(ReduceArgs a) {
+    __shared__ uint4 lds[2 * kReduceSpan2];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t wg = a.wg_base + blockIdx.x;
+    const uint64_t lo1 = wg * kReduceSpan1;
+    const uint64_t c1 = a.c1;
+    const uint64_t m1 = (c1 - lo1) < kReduceSpan1 ? (c1 - lo1) : kReduceSpan1;
+    const bool pair = a.levels >= 2 && (c1 > 1 || a.pad_at_one);
+    const uint64_t c2 = pair ? (c1 + 1) / 2 : c1;
+    const uint64_t m2 = pair ? (m1 + 1) / 2 : m1;
+
+    // ---- phase A: first level (+ pair level) from global memory ----------
+    if constexpr (FAST) {
+        // Full workgroup of full windows / complete node pairs (host-checked):
+        // no bounds checks, no odd padding, one keccak_f copy per call site.
+#pragma unroll 1
+        for (int i = 0; i < 2; ++i) {
+            const uint32_t q = i * kReduceThreads + tid;
+            const uint64_t j0 = lo1 + 2 * (uint64_t)q;
+            uint4 l0, l1, r0, r1, d0, d1;
+            if constexpr (LEAF) {
+                const uint4* w = reinterpret_cast<const uint4*>(a.items) + j0 * 16;
+                hash_window256(w, l0, l1);
+                hash_window256(w + 16, r0, r1);
+            } else {
+                const uint4* in = reinterpret_cast<const uint4*>(a.items) + j0 * 4;
+                hash_pair(ld_nt(in), ld_nt(in + 1), ld_nt(in + 2), ld_nt(in + 3), false, l0, l1);
+                hash_pair(ld_nt(in + 4), ld_nt(in + 5), ld_nt(in + 6), ld_nt(in + 7), false, r0, r1);
+            }
+            hash_pair(l0, l1, r0, r1, false, d0, d1);
+            lds[2 * q] = d0;
+            lds[2 * q + 1] = d1;
+        }
+    } else if (pair) {
+#pragma unroll 1
+        for (int i = 0; i < 2; ++i) {
+            const uint32_t q = i * kReduceThreads + tid;
+            if (q < m2) {
+                const uint64_t j0 = lo1 + 2 * (uint64_t)q;
+                uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0, d0, d1;
+                first_level_generic<LEAF>(a, j0, l0, l1);
+                const bool padded = !(2 * (uint64_t)q + 1 < m1);
+                if (!padded) first_level_generic<LEAF>(a, j0 + 1, r0, r1);
+                hash_pair(l0, l1, r0, r1, padded, d0, d1);
+                lds[2 * q] = d0;
+                lds[2 * q + 1] = d1;
+            }
+        }
+    } else {
+        // no pair level (levels == 1, or a single first-level node); the host
+        // guarantees m1 <= kReduceSpan2 here.
+#pragma unroll 1
+        for (int i = 0; i < 2; ++i) {
+            const uint32_t q = i * kReduceThreads + tid;
+            if (q < m1) {
+                uint4 d0, d1;
+                first_level_generic<LEAF>(a, lo1 + q, d0, d1);
+                lds[2 * q] = d0;
+                lds[2 * q + 1] = d1;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- phase B: levels in LDS -------------------------------------------
+    uint64_t c = c2, m = m2;
+    int left = a.finalize ? 64 : (int)a.levels - (pair ? 2 : 1);
+    int done = 0;
+    while (left > 0 && (c > 1 || a.pad_at_one)) {
+        const uint64_t mn = (m + 1) / 2;
+        const bool act = tid < mn;
+        uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+        bool padded = false;
+        if (act) {
+            l0 = lds[4 * tid];
+            l1 = lds[4 * tid + 1];
+            padded = !(2 * (uint64_t)tid + 1 < m);
+            if (!padded) {
+                r0 = lds[4 * tid + 2];
+                r1 = lds[4 * tid + 3];
+            }
+        }
+        __syncthreads();
+        if (act) {
+            uint4 d0, d1;
+            hash_pair(l0, l1, r0, r1, padded, d0, d1);
+            lds[2 * tid] = d0;
+            lds[2 * tid + 1] = d1;
+        }
+        __syncthreads();
+        c = (c + 1) / 2;
+        m = mn;
+        --left;
+        ++done;
+    }
+
+    // ---- output ------------------------------------------------------------
+    uint4* out = reinterpret_cast<uint4*>(a.out);
+    if (a.finalize) {
+        if (tid == 0) {
+            uint4 d0, d1;
+            hash_final(lds[0], lds[1], a.n_items, d0, d1);
+            out[0] = d0;
+            out[1] = d1;
+        }
+    } else {
+        const uint64_t lo_out = ((pair ? wg * kReduceSpan2 : wg * kReduceSpan1)) >> done;
+        for (uint32_t k = tid; k < m; k += kReduceThreads) {
+            out[2 * (lo_out + k)] = lds[2 * k];
+            out[2 * (lo_out + k) + 1] = lds[2 * k + 1];
+        }
+    }
+}
+
+template __global__ void k_reduce<true, true>(ReduceArgs);
+template __global__ void k_reduce<true, false>(ReduceArgs);
+template __global__ void k_reduce<false, true>(ReduceArgs);
+template __global__ void k_reduce<false, false>(ReduceArgs);
+
+// ----------------------------------------------------------------------------
+// Final hash for trees with <= 1 chunk: K(bytes[0,total) || [0^128 if n==0] || lenc)
+__global__ void k_final_small(const uint8_t* __restrict__ items, uint64_t total, uint64_t n, uint8_t* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint4 d0, d1;
+    sponge_generic(items, total, n == 0 ? 128u : 0u, true, n, d0, d1);
+    reinterpret_cast<uint4*>(out)[0] = d0;
+    reinterpret_cast<uint4*>(out)[1] = d1;
+}
+
+// Multi-GPU finisher: the reference loop over `nroots` 32-B subtree roots
+// (odd -> 0^128 pad), then the length mix-in.  One workgroup.
+__global__ __launch_bounds__(kReduceThreads) void k_finish_roots(const uint4* __restrict__ roots, uint64_t nroots,
+                                                               uint64_t n_items, uint4* out) {
+    __shared__ uint4 lds[2 * kReduceSpan2];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = tid; k < nroots; k += kReduceThreads) {
+        lds[2 * k] = roots[2 * k];
+        lds[2 * k + 1] = roots[2 * k + 1];
+    }
+    __syncthreads();
+    uint64_t m = nroots;
+    while (m > 1) {
+        const uint64_t mn = (m + 1) / 2;
+        const bool act = tid < mn;
+        uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+        bool padded = false;
+        if (act) {
+            l0 = lds[4 * tid];
+            l1 = lds[4 * tid + 1];
+            padded = !(2 * (uint64_t)tid + 1 < m);
+            if (!padded) {
+                r0 = lds[4 * tid + 2];
+                r1 = lds[4 * tid + 3];
+            }
+        }
+        __syncthreads();
+        if (act) {
+            uint4 d0, d1;
+            hash_pair(l0, l1, r0, r1, padded, d0, d1);
+            lds[2 * tid] = d0;
+            lds[2 * tid + 1] = d1;
+        }
+        __syncthreads();
+        m = mn;
+    }
+    if (tid == 0) {
+        uint4 d0, d1;
+        hash_final(lds[0], lds[1], n_items, d0, d1);
+        out[0] = d0;
+        out[1] = d1;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Batched hashutil.Hash: n messages of 64 B (one permutation each).
+__global__ __launch_bounds__(256) void k_keccak64(const uint4* __restrict__ in, uint64_t n, uint4* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4* p = in + 4 * i;
+    const uint4 v0 = ld_nt(p), v1 = ld_nt(p + 1);
+    const uint4 v2 = ld_nt(p + 2), v3 = ld_nt(p + 3);
+    uint4 d0, d1;
+    hash_pair(v0, v1, v2, v3, false, d0, d1);
+    out[2 * i] = d0;
+    out[2 * i + 1] = d1;
+}
+
+// n messages of fixed msg_len bytes (any length / alignment).
+__global__ __launch_bounds__(256) void k_keccak_fixed(const uint8_t* __restrict__ in, uint64_t n, uint32_t msg_len,
+                                                      uint4* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint4 d0, d1;
+    sponge_generic(in + i * msg_len, msg_len, 0, false, 0, d0, d1);
+    out[2 * i] = d0;
+    out[2 * i + 1] = d1;
+}
+
+// n variable-length messages: message i = in[offs[i], offs[i+1]).
+__global__ __launch_bounds__(256) void k_keccak_var(const uint8_t* __restrict__ in, const uint64_t* __restrict__ offs,
+                                                    uint64_t n, uint4* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t a = offs[i], b = offs[i + 1];
+    uint4 d0, d1;
+    sponge_generic(in + a, b - a, 0, false, 0, d0, d1);
+    out[2 * i] = d0;
+    out[2 * i + 1] = d1;
+}
+
+// ----------------------------------------------------------------------------
+// Deposit trie level: node j = K(in[2j] || (2j+1 < cin ? in[2j+1] : 0^32)),
+// the map-miss-reads-zero rule of deposit_trie.go:35-37.
+__global__ __launch_bounds__(256) void k_trie_level(const uint4* __restrict__ in, uint64_t cin, uint4* __restrict__ out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t cout = (cin + 1) / 2;
+    if (j >= cout) return;
+    const uint4 l0 = in[4 * j], l1 = in[4 * j + 1];
+    uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+    if (2 * j + 1 < cin) {
+        r0 = in[4 * j + 2];
+        r1 = in[4 * j + 3];
+    }
+    uint4 d0, d1;
+    hash_pair(l0, l1, r0, r1, false, d0, d1);
+    out[2 * j] = d0;
+    out[2 * j + 1] = d1;
+}
+
+// Levels above the last populated one: node = K(node || 0^32), `count` times;
+// levels[i] receives the node of the i-th level above `node` (the last one is
+// the root).
+__global__ void k_trie_tail(uint4* __restrict__ node, uint32_t count, uint4* __restrict__ levels) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint4 a0 = node[0], a1 = node[1];
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = 0; i < count; ++i) {
+        hash_pair(a0, a1, z, z, false, a0, a1);
+        if (levels) {
+            levels[2 * i] = a0;
+            levels[2 * i + 1] = a1;
+        }
+    }
+}
+
+// Batched VerifyMerkleBranch (deposit_trie.go:68-81): thread i folds its
+// `depth` siblings into leaf i and compares with root i.
+__global__ __launch_bounds__(256) void k_verify_branches(const uint4* __restrict__ leaves, const uint4* __restrict__ branches,
+                                                         const uint64_t* __restrict__ indices, uint32_t depth,
+                                                         uint32_t tree_depth, const uint4* __restrict__ roots,
+                                                         uint64_t n, uint8_t* __restrict__ ok) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t idx = indices[i] + (tree_depth >= 64 ? 0ull : (1ull << tree_depth));
+    uint4 v0 = leaves[2 * i], v1 = leaves[2 * i + 1];
+    const uint4* br = branches + 2 * (uint64_t)depth * i;
+    for (uint32_t d = 0; d < depth; ++d) {
+        const uint4 b0 = br[2 * d], b1 = br[2 * d + 1];
+        if (idx & 1)
+            hash_pair(b0, b1, v0, v1, false, v0, v1);
+        else
+            hash_pair(v0, v1, b0, b1, false, v0, v1);
+        idx >>= 1;
+    }
+    const uint4 r0 = roots[2 * i], r1 = roots[2 * i + 1];
+    ok[i] = (v0.x == r0.x && v0.y == r0.y && v0.z == r0.z && v0.w == r0.w && v1.x == r1.x && v1.y == r1.y &&
+             v1.z == r1.z && v1.w == r1.w);
+}
+
+// ----------------------------------------------------------------------------
+// Synthetic SplitMix64 stream: word k = mix(seed + k*gamma),
+// byte b of the stream = byte b%8 (LE) of word b/8.  Writes words
+// [word0, word0 + nwords) to dst.  Identical to oracle/merkle_ref.c.
+__device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t k) {
+    uint64_t z = seed + k * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_synth(uint64_t* __restrict__ dst, uint64_t nwords, uint64_t seed, uint64_t word0) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nwords; k += stride)
+        dst[k] = splitmix(seed, word0 + k);
+}
+
+}  // namespace mk

@@ -1,0 +1,43 @@
+// Shared declarations between the HIP kernels and the host planner / C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mk {
+
+constexpr uint32_t kReduceThreads = 256;             // 4 waves
+constexpr uint64_t kReduceSpan1 = 4 * kReduceThreads;  // first-level nodes per workgroup
+constexpr uint64_t kReduceSpan2 = kReduceSpan1 / 2;    // level-2 nodes per workgroup (LDS)
+constexpr uint32_t kMaxPassLevels = 5;               // levels per non-final pass (1024 -> 64)
+
+struct ReduceArgs {
+    const uint8_t* items;  // LEAF: item bytes; NODE: 32-B input nodes
+    uint64_t total;        // LEAF: item bytes in the tree (shard)
+    uint64_t cb;           // LEAF: chunk bytes
+    uint64_t nchunks;      // LEAF: chunks in the tree (shard)
+    uint64_t cin;          // NODE: input node count
+    uint64_t c1;           // first-level node count (windows / input pairs)
+    uint64_t c1_full;      // first-level nodes eligible for the fast path
+    uint8_t* out;          // output nodes (or the 32-B digest when finalize)
+    uint64_t n_items;      // length mix-in value (finalize)
+    uint32_t levels;       // hashing levels this pass performs
+    uint32_t finalize;     // reduce to the root and mix in the length
+    uint32_t pad_at_one;   // subtree mode: keep hashing (x || 0^128) at count 1
+    uint64_t wg_base;      // workgroup index offset of this launch
+};
+
+template <bool LEAF, bool FAST>
+__global__ void k_reduce(ReduceArgs a);
+__global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
+__global__ void k_finish_roots(const uint4* roots, uint64_t nroots, uint64_t n_items, uint4* out);
+__global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);
+__global__ void k_keccak_fixed(const uint8_t* in, uint64_t n, uint32_t msg_len, uint4* out);
+__global__ void k_keccak_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint4* out);
+__global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
+__global__ void k_trie_tail(uint4* node, uint32_t count, uint4* levels);
+__global__ void k_verify_branches(const uint4* leaves, const uint4* branches, const uint64_t* indices,
+                                  uint32_t depth, uint32_t tree_depth, const uint4* roots, uint64_t n,
+                                  uint8_t* ok);
+__global__ void k_synth(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t word0);
+
+}  // namespace mk

@@ -1,0 +1,121 @@
+"""Device-resident entry points (inputs already in HBM), torch as plumbing.
+
+torch provides device memory, the current HIP stream and torch.distributed;
+every hash is computed by the HIP kernels behind the C-ABI
+(``mk_dev_*`` in include/prysm_merkle.h).  Work is enqueued on torch's
+current stream of the tensor's device and is not synchronised here.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+def _stream(dev: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _p(t: torch.Tensor):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _bind(t: torch.Tensor):
+    if t.device.type != "cuda":
+        raise _lib.MerkleError(_lib.MK_EINVAL, "device entry points need a GPU tensor")
+    _lib.init(t.device.index or 0)
+
+
+def synth_fill(dst: torch.Tensor, seed: int, word0: int = 0) -> torch.Tensor:
+    """Fill ``dst`` (uint8, nbytes % 8 == 0) with bytes [8*word0, ...) of the
+    SplitMix64 stream."""
+    _bind(dst)
+    _lib.check(_lib.load().mk_dev_synth_fill(_p(dst), dst.numel() * dst.element_size(), seed, word0,
+                                             _stream(dst.device)), "mk_dev_synth_fill")
+    return dst
+
+
+def merkle_workspace(n: int, item_len: int, device) -> torch.Tensor:
+    nbytes = _lib.load().mk_ssz_merkle_workspace_bytes(n, item_len)
+    return torch.empty(max(256, nbytes), dtype=torch.uint8, device=device)
+
+
+def merkle_hash(items: torch.Tensor, n: int, item_len: int, out: torch.Tensor = None,
+                ws: torch.Tensor = None) -> torch.Tensor:
+    """ssz.merkleHash of n items of item_len bytes held in ``items`` (uint8,
+    device).  Returns a (32,) uint8 device tensor."""
+    _bind(items)
+    if items.numel() < n * item_len:
+        raise ValueError("items tensor shorter than n*item_len")
+    if out is None:
+        out = torch.empty(32, dtype=torch.uint8, device=items.device)
+    if ws is None:
+        ws = merkle_workspace(n, item_len, items.device)
+    _lib.check(_lib.load().mk_dev_ssz_merkle_hash(_p(items), n, item_len, _p(out), _p(ws), ws.numel(),
+                                                  _stream(items.device)), "mk_dev_ssz_merkle_hash")
+    return out
+
+
+def shard_plan(n: int, item_len: int, nshards: int):
+    """(height, nonempty, item_begin[nshards+1]) of the subtree sharding."""
+    h = ctypes.c_uint32()
+    ne = ctypes.c_uint32()
+    begin = (ctypes.c_uint64 * (nshards + 1))()
+    _lib.check(_lib.load().mk_ssz_merkle_shard_plan(n, item_len, nshards, ctypes.byref(h), ctypes.byref(ne),
+                                                    begin), "mk_ssz_merkle_shard_plan")
+    return h.value, ne.value, list(begin)
+
+
+def subtree_workspace(shard_n: int, item_len: int, device) -> torch.Tensor:
+    # the full-tree plan of the same item count bounds the subtree plan
+    nbytes = _lib.load().mk_ssz_merkle_workspace_bytes(max(shard_n, 1), item_len) + 4096
+    return torch.empty(nbytes, dtype=torch.uint8, device=device)
+
+
+def merkle_subtree(items: torch.Tensor, shard_n: int, item_len: int, height: int, pad_at_one: bool,
+                   out: torch.Tensor = None, ws: torch.Tensor = None) -> torch.Tensor:
+    """32-B root of one shard at `height` levels above its chunks."""
+    _bind(items)
+    if out is None:
+        out = torch.empty(32, dtype=torch.uint8, device=items.device)
+    if ws is None:
+        ws = subtree_workspace(shard_n, item_len, items.device)
+    _lib.check(_lib.load().mk_dev_ssz_merkle_subtree(_p(items), shard_n, item_len, height, int(pad_at_one), _p(out),
+                                                     _p(ws), ws.numel(), _stream(items.device)),
+               "mk_dev_ssz_merkle_subtree")
+    return out
+
+
+def merkle_finish(roots: torch.Tensor, nroots: int, n_total: int, out: torch.Tensor = None) -> torch.Tensor:
+    """Reference level loop over gathered shard roots + length mix-in."""
+    _bind(roots)
+    if out is None:
+        out = torch.empty(32, dtype=torch.uint8, device=roots.device)
+    _lib.check(_lib.load().mk_dev_ssz_merkle_finish(_p(roots), nroots, n_total, _p(out), _stream(roots.device)),
+               "mk_dev_ssz_merkle_finish")
+    return out
+
+
+def hash_batch(msgs: torch.Tensor, n: int, msg_len: int, out: torch.Tensor = None) -> torch.Tensor:
+    """Batched Hash of n fixed-length messages resident on the device."""
+    _bind(msgs)
+    if out is None:
+        out = torch.empty(n * 32, dtype=torch.uint8, device=msgs.device)
+    _lib.check(_lib.load().mk_dev_hash_batch(_p(msgs), n, msg_len, _p(out), _stream(msgs.device)),
+               "mk_dev_hash_batch")
+    return out
+
+
+def prof_enable(on: bool = True) -> None:
+    _lib.check(_lib.load().mk_prof_enable(int(on)), "mk_prof_enable")
+
+
+def prof_read():
+    """(summed ms, launches, algorithmic permutations) of the recorded leaf passes."""
+    ms = ctypes.c_double()
+    cnt = ctypes.c_uint64()
+    perms = ctypes.c_double()
+    _lib.check(_lib.load().mk_prof_read(ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(perms)), "mk_prof_read")
+    return ms.value, cnt.value, perms.value

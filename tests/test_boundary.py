@@ -1,0 +1,102 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads, exports
+every symbol include/prysm_merkle.h declares, and its pure-host logic (the
+shard planner, workspace sizing, argument errors) behaves — no GPU compute."""
+import ctypes
+import os
+
+import pytest
+
+from prysm_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        import __graft_entry__
+
+        __graft_entry__.build()
+    return _lib.load()
+
+
+def test_header_declares_the_boundary():
+    syms = _lib.header_symbols()
+    for s in ("mk_init", "mk_hash", "mk_hash_batch", "mk_ssz_merkle_hash", "mk_dev_ssz_merkle_hash",
+              "mk_dev_ssz_merkle_subtree", "mk_dev_ssz_merkle_finish", "mk_ssz_merkle_hash_multi",
+              "mk_deposit_trie_build", "mk_verify_merkle_branches"):
+        assert s in syms
+    assert set(syms) == set(_lib._SIGS), "ctypes signature table out of sync with the header"
+
+
+def test_library_exports_every_header_symbol(lib):
+    missing = [s for s in _lib.header_symbols() if not hasattr(lib, s)]
+    assert not missing
+    assert lib.mk_version().decode().startswith("prysm_merkle")
+    assert lib.mk_strerror(_lib.MK_ENODEV) == b"no usable gfx950 device"
+
+
+def test_library_is_gfx950_code_object(lib):
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob
+    assert b"k_reduce" in blob
+
+
+def _plan(lib, n, item_len, world):
+    h, ne = ctypes.c_uint32(), ctypes.c_uint32()
+    begin = (ctypes.c_uint64 * (world + 1))()
+    rc = lib.mk_ssz_merkle_shard_plan(n, item_len, world, ctypes.byref(h), ctypes.byref(ne), begin)
+    return rc, h.value, ne.value, list(begin)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_shard_plan_c4(lib, world):
+    n = 1 << 28
+    rc, h, ne, begin = _plan(lib, n, 32, world)
+    assert rc == 0
+    chunks = n // 4
+    assert (1 << h) * world == chunks or world == 1
+    assert begin[0] == 0 and begin[-1] == n
+    if world > 1:
+        assert ne == world
+        assert all(begin[i + 1] - begin[i] == n // world for i in range(world))
+
+
+@pytest.mark.parametrize("n,item_len,world", [(4099, 32, 8), (1000, 8, 3), (41 * 4 + 3, 32, 4), (5, 32, 8),
+                                              (0, 32, 4), (100, 200, 8), (10**6, 32, 8)])
+def test_shard_plan_properties(lib, n, item_len, world):
+    rc, h, ne, begin = _plan(lib, n, item_len, world)
+    assert rc == 0
+    per = 128 // item_len if item_len < 128 else 1
+    chunks = -(-n * item_len // (per * item_len)) if n else 0
+    assert begin[0] == 0 and begin[-1] == n and begin == sorted(begin)
+    if ne > 1:
+        assert (1 << h) * (ne - 1) < chunks <= (1 << h) * ne
+        assert (1 << h) * world >= chunks
+        for s in range(ne - 1):  # every non-last non-empty shard is full
+            assert begin[s + 1] - begin[s] == (1 << h) * per
+    else:
+        assert begin[1] == n
+
+
+def test_workspace_sizing(lib):
+    assert lib.mk_ssz_merkle_workspace_bytes(0, 32) >= 32
+    ws = lib.mk_ssz_merkle_workspace_bytes(1 << 28, 32)
+    # pass outputs: 2^21 + 2^16 nodes of 32 B
+    assert ws >= 32 * ((1 << 21) + (1 << 16))
+    assert ws < 80 << 20
+    assert lib.mk_ssz_merkle_workspace_bytes(10, 0) == 0  # item_len 0 is invalid
+    assert lib.mk_deposit_trie_levels_bytes(0, 32) == 0
+    assert lib.mk_deposit_trie_levels_bytes(5, 2) == 32 * (5 + 3 + 2)
+
+
+def test_oracle_is_not_imported_by_product():
+    """The product package never touches oracle/ (it is test infrastructure)."""
+    pkg = os.path.join(ROOT, "prysm_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".cpp", ".hip", ".hpp", ".h")):
+                txt = open(os.path.join(dp, f)).read()
+                assert "import oracle" not in txt and "from oracle" not in txt, f
+                assert "liboracle" not in txt, f

@@ -1,0 +1,109 @@
+"""The N>1 path (subtree sharding + one all-gather + rank-0 finish) with the
+gloo backend on CPU, world_size 2 and 4.  The per-shard compute is the
+oracle here (the HIP kernels are covered by tests/test_gpu_parity.py); this
+checks the orchestration, the shard plan and the collective."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+SEED = 0x5EED000000000000 + 81
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _plan_cpu(n, item_len, world):
+    """Shard plan restated in Python (the C planner is checked against this
+    in test_boundary)."""
+    per = 128 // item_len if item_len < 128 else 1
+    cb = per * item_len
+    chunks = -(-n * item_len // cb) if n else 0
+    h = 0
+    while (1 << h) * world < chunks:
+        h += 1
+    ne = -(-chunks // (1 << h)) if chunks else 0
+    if h == 0 or ne <= 1:
+        return h, 1, [0] + [n] * world
+    return h, ne, [min(n, s * (1 << h) * per) for s in range(world + 1)]
+
+
+def _worker(rank, world, port, n, item_len, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from oracle import oracle as O
+        from prysm_amd import parallel as P
+
+        sp = P.plan(n, item_len, world, plan_fn=_plan_cpu)
+        lo, hi = sp.items(rank)
+        full = O.splitmix_bytes(n * item_len, SEED)
+        local = torch.from_numpy(full[lo * item_len:hi * item_len].copy())
+
+        def subtree(items, sn, il, h, pad):
+            # oracle subtree of shard `rank` of the synthetic tree
+            return torch.frombuffer(bytearray(O.merkle_subtree_gen(n, il, SEED, rank, h)), dtype=torch.uint8)
+
+        def full_fn(items, nn, il):
+            return torch.frombuffer(bytearray(O.merkle_hash_flat(items.numpy(), nn, il)), dtype=torch.uint8)
+
+        def finish(g, nr, nt):
+            roots = [bytes(g[32 * i:32 * i + 32].numpy()) for i in range(nr)]
+            chunks = roots
+            while len(chunks) > 1:
+                if len(chunks) % 2:
+                    chunks = chunks + [bytes(128)]
+                chunks = [O.keccak256(chunks[i] + chunks[i + 1]) for i in range(0, len(chunks), 2)]
+            lenc = nt.to_bytes(8, "little") + bytes(24)
+            return torch.frombuffer(bytearray(O.keccak256(chunks[0] + lenc)), dtype=torch.uint8)
+
+        root = P.sharded_merkle_hash(local, n, item_len, sp, rank, world, subtree_fn=subtree, full_fn=full_fn,
+                                     finish_fn=finish)
+        if rank == 0:
+            q.put(bytes(root.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 4 * 1000 + 3), (2, 1 << 14), (4, 4 * 37), (4, 9), (4, 1 << 12)])
+def test_sharded_root_equals_full_root(world, n):
+    from oracle import oracle as O
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, 32, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    root = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert root == O.merkle_hash_gen(n, 32, SEED)
+
+
+@pytest.mark.parametrize("n,item_len,world", [(4099, 32, 8), (1000, 8, 3), (41 * 4 + 3, 32, 4), (5, 32, 8),
+                                              (100, 200, 8), (10**6, 32, 8), (1 << 28, 32, 8)])
+def test_python_plan_matches_c_planner(n, item_len, world):
+    import ctypes
+
+    from prysm_amd import _lib
+
+    h, ne = ctypes.c_uint32(), ctypes.c_uint32()
+    begin = (ctypes.c_uint64 * (world + 1))()
+    assert _lib.load().mk_ssz_merkle_shard_plan(n, item_len, world, ctypes.byref(h), ctypes.byref(ne), begin) == 0
+    ph, pne, pbegin = _plan_cpu(n, item_len, world)
+    assert (ne.value, list(begin)) == (pne, pbegin)
+    if pne > 1:
+        assert h.value == ph

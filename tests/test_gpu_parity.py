@@ -1,0 +1,310 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle and the
+reference's own vectors.  Bit-exact everywhere (integer/byte work)."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED000000000000
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+
+    from prysm_amd import _lib
+
+    assert torch.cuda.is_available()
+    assert _lib.device_count() >= 1, "libprysm_merkle.so sees no gfx950 device"
+    _lib.init(0)
+    return torch.device("cuda:0")
+
+
+# ------------------------------------------------------------------ Keccak
+def test_hash_kats(gpu, ref_vectors):
+    from prysm_amd import hashutil as H
+
+    for kat in ref_vectors["keccak256_kats"]:
+        assert H.Hash(bytes.fromhex(kat["in"])).hex() == kat["out"], kat["ref"]
+
+
+@pytest.mark.parametrize("msg_len", [1, 8, 31, 32, 36, 52, 63, 64, 65, 135, 136, 137, 144, 200, 256, 271, 272,
+                                     280, 1000])
+def test_hash_batch_fixed(gpu, msg_len):
+    from oracle import oracle as O
+    from prysm_amd import hashutil as H
+
+    n = 777
+    msgs = O.splitmix_bytes(n * msg_len, SEED + msg_len)
+    assert np.array_equal(H.hash_batch(msgs, msg_len), O.keccak256_batch(msgs, msg_len))
+
+
+def test_hash_batch_var(gpu):
+    from oracle import oracle as O
+    from prysm_amd import hashutil as H
+
+    rng = np.random.default_rng(3)
+    msgs = [bytes(rng.integers(0, 256, int(L), dtype=np.uint8)) for L in rng.integers(0, 700, 500)]
+    msgs += [b"", b"\x00", b"abc"]
+    got = H.hash_batch_var(msgs)
+    want = [bytes(r) for r in O.keccak256_var(msgs)]
+    assert got == want
+
+
+def test_dev_hash_batch_64(gpu):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    n = (1 << 16) + 5
+    buf = torch.empty(n * 64, dtype=torch.uint8, device=gpu)
+    D.synth_fill(buf, SEED + 11)
+    out = D.hash_batch(buf, n, 64)
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy()
+    assert np.array_equal(host, O.splitmix_bytes(n * 64, SEED + 11))
+    assert np.array_equal(out.cpu().numpy().reshape(n, 32), O.keccak256_batch(host, 64))
+
+
+# ------------------------------------------------------------------ merkleHash
+def test_merkle_reference_vectors(gpu, ref_vectors, res_vectors):
+    from prysm_amd import ssz
+
+    for vec in ref_vectors["merkle_hash"] + res_vectors["merkle_lists"]:
+        items = [bytes.fromhex(x) for x in vec["items"]]
+        assert ssz.merkle_hash(items).hex() == vec["output"], vec.get("ref")
+
+
+def test_merkle_restatement_fixtures(gpu, res_vectors):
+    from oracle import oracle as O
+    from prysm_amd import ssz
+
+    for c in res_vectors["merkle_flat"]:
+        items = O.splitmix_bytes(c["n"] * c["item_len"], c["seed"])
+        assert ssz.merkle_hash_flat(items, c["n"], c["item_len"]).hex() == c["root"], (c["n"], c["item_len"])
+
+
+def test_merkle_edge_errors(gpu):
+    from prysm_amd import ssz
+
+    with pytest.raises(ZeroDivisionError):
+        ssz.merkle_hash([b"", b"x"])
+    with pytest.raises(ZeroDivisionError):
+        ssz.merkle_hash_flat(np.zeros(0, np.uint8), 3, 0)
+
+
+def test_merkle_ragged_list(gpu):
+    from oracle import oracle as O
+    from prysm_amd import ssz
+
+    lst = [bytes([i]) * (1 + (i * 7) % 50) for i in range(37)]
+    assert ssz.merkle_hash(lst) == O.merkle_hash(lst)
+
+
+@pytest.mark.parametrize("n", [2048 * 4, 2048 * 4 + 4, 1 << 16, (1 << 16) + 3, (1 << 18) + 4 * 1024 + 1,
+                               (1 << 20) - 1, 1 << 20, 3_000_001])
+def test_dev_merkle_vs_oracle(gpu, n):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    item_len = 32
+    items = torch.empty(n * item_len, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 21)
+    root = D.merkle_hash(items, n, item_len)
+    torch.cuda.synchronize()
+    assert bytes(root.cpu().numpy()) == O.merkle_hash_gen(n, item_len, SEED + 21, nthreads=16)
+
+
+@pytest.mark.parametrize("item_len,n", [(8, 1 << 18), (8, 250_001), (1, 100_003), (48, 30_001), (128, 20_000),
+                                        (200, 9_999), (3, 77_777)])
+def test_dev_merkle_item_sizes(gpu, item_len, n):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    nb = n * item_len
+    items = torch.empty(nb + (-nb) % 8, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 22)
+    root = D.merkle_hash(items, n, item_len)
+    torch.cuda.synchronize()
+    host = items.cpu().numpy()[:nb]
+    assert bytes(root.cpu().numpy()) == O.merkle_hash_flat(host, n, item_len, nthreads=16)
+
+
+def test_dev_merkle_unaligned_input(gpu):
+    """An input pointer that is not 16-B aligned takes the generic path."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    n = 70_001
+    buf = torch.empty(n * 32 + 64, dtype=torch.uint8, device=gpu)
+    D.synth_fill(buf, SEED + 23)
+    items = buf[8:8 + n * 32]
+    root = D.merkle_hash(items, n, 32)
+    torch.cuda.synchronize()
+    assert bytes(root.cpu().numpy()) == O.merkle_hash_flat(items.cpu().numpy(), n, 32, nthreads=16)
+
+
+# ------------------------------------------------------------------ sharding
+@pytest.mark.parametrize("n,world", [(1 << 16, 2), (1 << 16, 8), ((1 << 16) + 12, 8), (41 * 4 + 3, 4),
+                                     (999_999, 3), (5, 8), (4099, 8), (1 << 20, 8)])
+def test_subtree_sharding_equals_full(gpu, n, world):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    item_len = 32
+    h, ne, begin = D.shard_plan(n, item_len, world)
+    items = torch.empty(max(16, n * item_len), dtype=torch.uint8, device=gpu)
+    D.synth_fill(items[:n * item_len], SEED + 31)
+    full = D.merkle_hash(items, n, item_len)
+    want = O.merkle_hash_gen(n, item_len, SEED + 31, nthreads=16)
+    if ne > 1:
+        roots = torch.zeros(world * 32, dtype=torch.uint8, device=gpu)
+        for s in range(ne):
+            sh = items[begin[s] * item_len:begin[s + 1] * item_len]
+            D.merkle_subtree(sh, begin[s + 1] - begin[s], item_len, h, True, out=roots[32 * s:32 * s + 32])
+        got = D.merkle_finish(roots, ne, n)
+        torch.cuda.synchronize()
+        for s in range(ne):  # every shard root against the oracle's subtree
+            assert bytes(roots[32 * s:32 * s + 32].cpu().numpy()) == O.merkle_subtree_gen(
+                n, item_len, SEED + 31, s, h, nthreads=16), s
+        assert bytes(got.cpu().numpy()) == want
+    torch.cuda.synchronize()
+    assert bytes(full.cpu().numpy()) == want
+
+
+def test_multi_device_entry_single_gpu(gpu):
+    """mk_ssz_merkle_hash_multi with ndev=1 is the plain path."""
+    import ctypes
+
+    from oracle import oracle as O
+    from prysm_amd import _lib
+
+    n = 12345
+    items = O.splitmix_bytes(n * 32, SEED + 41)
+    out = ctypes.create_string_buffer(32)
+    _lib.check(_lib.load().mk_ssz_merkle_hash_multi(items.ctypes.data_as(ctypes.c_void_p), n, 32, 1, out))
+    assert out.raw == O.merkle_hash_flat(items, n, 32)
+
+
+# ------------------------------------------------------------------ TreeHash host mirror
+def test_tree_hash_reference_vectors(gpu, ref_vectors):
+    from prysm_amd import ssz
+    from tests.ssz_types import to_ssz_type, to_value
+
+    assert len(ref_vectors["tree_hash"]) == 60
+    for vec in ref_vectors["tree_hash"]:
+        t = to_ssz_type(vec["type"])
+        v = to_value(vec["type"], vec["value"])
+        if vec["error"]:
+            with pytest.raises(ssz.HashError) as ei:
+                ssz.tree_hash(v, t)
+            assert str(ei.value) == vec["error"], vec["ref"]
+        else:
+            assert ssz.tree_hash(v, t).hex() == vec["output"], vec["ref"]
+
+
+def test_tree_hash_registry_matches_oracle(gpu):
+    """A synthetic validator registry (pb.Validator field order, StatusFlags
+    widened to uint64 — SURVEY.md §8d) through TreeHash vs the oracle."""
+    from oracle import ssz_ref as S
+    from prysm_amd import ssz
+    from tests.ssz_types import validator_registry
+
+    t_ref, t_ssz, vals = validator_registry(300, SEED + 51)
+    assert ssz.tree_hash(vals, t_ssz) == S.tree_hash(t_ref, vals)
+
+
+# ------------------------------------------------------------------ hashutil.MerkleRoot
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 5, 7, 8, 13, 100, 8192])
+def test_merkle_root(gpu, n):
+    from oracle import oracle as O
+    from prysm_amd import hashutil as H
+
+    vals = [struct.pack("<Q", i) * (1 + i % 3) for i in range(n)]
+    want = O.merkle_root(vals)
+    mutated = list(vals)
+    assert H.MerkleRoot(mutated) == want
+    assert mutated == [O.keccak256(v) for v in vals]  # merkleRoot.go:16-19 side effect
+
+
+def test_merkle_root_reference_vector(gpu, ref_vectors):
+    from prysm_amd import hashutil as H
+
+    for vec in ref_vectors["merkle_root"]:
+        assert H.MerkleRoot([bytes.fromhex(v) for v in vec["values"]]).hex() == vec["output"]
+
+
+# ------------------------------------------------------------------ deposit trie
+def test_deposit_trie_fixtures(gpu, res_vectors):
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    for c in res_vectors["deposit_tries"]:
+        deps = [bytes(O.splitmix_bytes(c["deposit_len"], c["seed"], c["word_stride"] * i)) for i in range(c["n"])]
+        assert T.DepositTrie.build(deps).root().hex() == c["root"], c["n"]
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 5, 8, 33, 1000, 4097])
+def test_deposit_trie_levels_branches(gpu, n):
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    deps = [bytes(O.splitmix_bytes(280, SEED + 61, 35 * i)) for i in range(n)]
+    root, levels = O.deposit_trie_levels(deps)
+    t = T.DepositTrie()
+    for d in deps:
+        t.update_deposit_trie(d)
+    assert t.root() == root
+    for i in sorted({0, n // 2, max(n - 1, 0)}) if n else []:
+        br = t.generate_merkle_branch(i)
+        want = [levels[d][(i >> d) ^ 1] if ((i >> d) ^ 1) < len(levels[d]) else bytes(32) for d in range(32)]
+        assert br == want
+        assert T.verify_merkle_branch(O.keccak256(deps[i]), br, 32, i, root)
+        assert not T.verify_merkle_branch(O.keccak256(deps[i] + b"!"), br, 32, i, root)
+
+
+def test_deposit_trie_reference_shapes(gpu):
+    """deposit_trie_test.go:10-65 shapes: 2 x 4-byte deposits, 3 x 3-byte."""
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    for deps in ([bytes([1, 2, 3, 4]), bytes([5, 6, 7, 8])], [bytes(4), bytes(4)],
+                 [bytes([1, 2, 3]), bytes([5, 6, 7]), bytes([8, 9, 10])]):
+        t = T.DepositTrie()
+        for d in deps:
+            t.UpdateDepositTrie(d)
+        assert t.deposit_count == len(deps)
+        assert t.leaf(len(deps) - 1) == O.keccak256(deps[-1])
+        idx = len(deps) - 1
+        assert T.VerifyMerkleBranch(O.keccak256(deps[-1]), t.GenerateMerkleBranch(idx), 32, idx, t.Root())
+        assert t.Root() == O.deposit_trie_levels(deps)[0]
+
+
+def test_verify_branches_batch(gpu):
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    n = 2000
+    deps = [bytes(O.splitmix_bytes(280, SEED + 71, 35 * i)) for i in range(n)]
+    t = T.DepositTrie.build(deps)
+    idx = list(range(0, n, 7))
+    leaves = [O.keccak256(deps[i]) for i in idx]
+    branches = [t.generate_merkle_branch(i) for i in idx]
+    roots = [t.root()] * len(idx)
+    assert all(T.verify_merkle_branches(leaves, branches, 32, idx, roots))
+    bad = list(idx)
+    bad[3] += 1
+    res = T.verify_merkle_branches(leaves, branches, 32, bad, roots)
+    assert res[3] is False and sum(res) == len(idx) - 1
