@@ -125,9 +125,47 @@ __device__ __forceinline__ void hash_final(uint4 r0, uint4 r1, uint64_t n, uint4
 // ----------------------------------------------------------------------------
 // Fast 256-B window (two Keccak blocks).  The block loop is rolled so the
 // kernel keeps one keccak_f copy in its hot loop (I-cache).
+#ifndef MK_LOAD_ALL
+#define MK_LOAD_ALL 0
+#endif
+#ifndef MK_MIN_WAVES
+#define MK_MIN_WAVES 1
+#endif
+
 __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint4& d0, uint4& d1) {
     State s;
     zero(s);
+#if MK_LOAD_ALL
+    // whole window in registers before the first permutation: each 128-B
+    // line is fetched once (no L2 re-fetch of the line shared by both blocks)
+    uint4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = ld_nt(w + k);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        s.lo[2 * k] ^= v[k].x;
+        s.hi[2 * k] ^= v[k].y;
+        s.lo[2 * k + 1] ^= v[k].z;
+        s.hi[2 * k + 1] ^= v[k].w;
+    }
+    s.lo[16] ^= v[8].x;
+    s.hi[16] ^= v[8].y;
+    keccak_f(s);
+    s.lo[0] ^= v[8].z;
+    s.hi[0] ^= v[8].w;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        s.lo[1 + 2 * k] ^= v[9 + k].x;
+        s.hi[1 + 2 * k] ^= v[9 + k].y;
+        s.lo[2 + 2 * k] ^= v[9 + k].z;
+        s.hi[2 + 2 * k] ^= v[9 + k].w;
+    }
+    s.lo[15] ^= 1u;
+    s.hi[16] ^= 0x80000000u;
+    keccak_f(s);
+    digest(s, d0, d1);
+    return;
+#endif
 #pragma unroll 1
     for (int b = 0; b < 2; ++b) {
         if (b == 0) {
@@ -208,7 +246,7 @@ __device__ __forceinline__ void first_level_generic(const ReduceArgs& a, uint64_
 // Non-final passes write 512 >> (levels-2) nodes per workgroup; the final
 // pass (one workgroup) reduces to the root and applies the length mix-in.
 template <bool LEAF, bool FAST>
-__global__ __launch_bounds__(kReduceThreads) void k_reduce(ReduceArgs a) {
+__global__ __launch_bounds__(kReduceThreads, MK_MIN_WAVES) void k_reduce(ReduceArgs a) {
     __shared__ uint4 lds[2 * kReduceSpan2];
     const uint32_t tid = threadIdx.x;
     const uint64_t wg = a.wg_base + blockIdx.x;

@@ -1,0 +1,85 @@
+"""A/B timing of libprysm_merkle variants in ONE process (cdna guide §5.4
+rule 24): interleaved rounds, same device, same data; reports the median
+time of a full merkleHash and of its leaf pass per variant, and checks that
+every variant returns the same root.
+
+  python tools/ab_leaf.py [--log2n 26] [--rounds 7] base loadall w5 ...
+(variants are prysm_amd/lib/variants/libprysm_merkle_<name>.so; "main" is
+the in-tree library)."""
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def load(path):
+    from prysm_amd import _lib
+
+    L = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+    for name, (res, args) in _lib._SIGS.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    return L
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--log2n", type=int, default=26)
+    ap.add_argument("--item-len", type=int, default=32)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("variants", nargs="+")
+    a = ap.parse_args()
+    import torch
+
+    dev = torch.device("cuda:0")
+    libs = {}
+    for v in a.variants:
+        p = os.path.join(ROOT, "prysm_amd", "lib", "libprysm_merkle.so") if v == "main" else \
+            os.path.join(ROOT, "prysm_amd", "lib", "variants", f"libprysm_merkle_{v}.so")
+        libs[v] = load(p)
+        assert libs[v].mk_init(0) == 0
+    n, il = 1 << a.log2n, a.item_len
+    items = torch.empty(n * il, dtype=torch.uint8, device=dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    first = libs[a.variants[0]]
+    assert first.mk_dev_synth_fill(ctypes.c_void_p(items.data_ptr()), n * il, 0x5EED000000000004, 0, st) == 0
+    ws = torch.empty(first.mk_ssz_merkle_workspace_bytes(n, il) + 4096, dtype=torch.uint8, device=dev)
+    outs = {v: torch.empty(32, dtype=torch.uint8, device=dev) for v in a.variants}
+    times = {v: [] for v in a.variants}
+    leaf = {v: [] for v in a.variants}
+    for r in range(a.rounds + 1):
+        for v, L in libs.items():
+            L.mk_prof_enable(1)
+            L.mk_prof_read(None, None, None)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = L.mk_dev_ssz_merkle_hash(ctypes.c_void_p(items.data_ptr()), n, il,
+                                          ctypes.c_void_p(outs[v].data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                          ws.numel(), st)
+            e1.record()
+            torch.cuda.synchronize()
+            assert rc == 0, (v, rc)
+            ms = ctypes.c_double()
+            cnt = ctypes.c_uint64()
+            perms = ctypes.c_double()
+            L.mk_prof_read(ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(perms))
+            L.mk_prof_enable(0)
+            if r:  # round 0 is warmup
+                times[v].append(e0.elapsed_time(e1))
+                leaf[v].append(ms.value)
+    roots = {v: bytes(o.cpu().numpy()).hex() for v, o in outs.items()}
+    assert len(set(roots.values())) == 1, roots
+    for v in a.variants:
+        print(json.dumps({"variant": v, "log2n": a.log2n, "median_ms": statistics.median(times[v]),
+                          "min_ms": min(times[v]), "leaf_median_ms": statistics.median(leaf[v]),
+                          "leaves_per_s": n / (statistics.median(times[v]) / 1e3)}))
+    print(json.dumps({"root": roots[a.variants[0]]}))
+
+
+if __name__ == "__main__":
+    main()
