@@ -72,7 +72,13 @@ def main():
     ap.add_argument("--item-len", type=int, default=32)
     ap.add_argument("--cpu-sample-log2n", type=int, default=24)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5"],
+                    help="BASELINE.json config: c4 = headline (default); c2/c3/c5 = single-GPU side benches")
     args = ap.parse_args()
+    if args.config != "c4":
+        from tools.bench_configs import run_config
+
+        return run_config(args)
 
     import torch
     import torch.distributed as dist

@@ -101,6 +101,32 @@ int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_to
 int mk_ssz_merkle_hash_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int ndev,
                              uint8_t out[32]);
 
+/* ---- struct hashing (hash.go:141-159) for flat fixed-layout records ------ */
+/* The typed-registry path behind ssz.Hashable (hash.go:18-20, 57-58): a Go
+ * wrapper flattens []*ValidatorRecord into n records of record_len bytes once
+ * and describes the fields in declaration order ("XXX" fields omitted, as
+ * structFields does, ssz_utils_cache.go:100).  Field hash = MK_FIELD_BYTES:
+ * Keccak(le32(len) || bytes) (offset must be 4-byte aligned, record_len too);
+ * MK_FIELD_RAW: raw little-endian scalar of len 1/2/4/8 (not hashed).
+ * The struct root is Keccak(concat of field outputs). */
+#define MK_FIELD_BYTES 1
+#define MK_FIELD_RAW 2
+typedef struct mk_field {
+    uint32_t kind;
+    uint32_t offset;
+    uint32_t len;
+} mk_field;
+uint64_t mk_ssz_struct_msg_len(const mk_field* fields, uint32_t nfields);
+/* roots of n records -> n x 32 bytes (one struct hash per record). */
+int mk_ssz_struct_roots(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
+                        uint32_t nfields, uint8_t* roots);
+/* TreeHash of a list of such structs: merkleHash over the n struct roots. */
+uint64_t mk_ssz_struct_list_workspace_bytes(uint64_t n, const mk_field* fields, uint32_t nfields);
+int mk_dev_ssz_struct_list_root(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
+                                uint32_t nfields, void* d_out32, void* d_ws, uint64_t ws_bytes, void* stream);
+int mk_ssz_struct_list_root(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
+                            uint32_t nfields, uint8_t out[32]);
+
 /* ---- trieutil deposit trie (deposit_trie.go:29-81) ---------------------- */
 /* Batch build of the depth-`depth` sparse trie over n deposits (message i =
  * data[offs[i], offs[i+1])).  Equals n calls of UpdateDepositTrie: empty nodes
@@ -110,6 +136,10 @@ int mk_ssz_merkle_hash_multi(const uint8_t* items, uint64_t n, uint32_t item_len
 uint64_t mk_deposit_trie_levels_bytes(uint64_t n, uint32_t depth);
 int mk_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
                           uint8_t* levels_out, uint8_t root[32]);
+/* Device-resident build: d_offs (n+1 u64) and d_levels
+ * (mk_deposit_trie_levels_bytes) in device memory; root to d_root32. */
+int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t depth,
+                              void* d_levels, void* d_root32, void* stream);
 /* Batched VerifyMerkleBranch: ok[i] = fold(leaves[i], branches[i*depth..],
  * indices[i] + 2^tree_depth) == roots[i]. */
 int mk_verify_merkle_branches(const uint8_t* leaves, const uint8_t* branches, const uint64_t* indices,

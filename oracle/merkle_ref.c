@@ -327,3 +327,41 @@ int or_merkle_root(const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_
     free(o);
     return 0;
 }
+
+/* ---- flat fixed-layout structs (ssz/hash.go:141-159) -------------------
+ * kind 1: bytes field -> Keccak(le32(len) || bytes)  (hash.go:100-107,
+ *         encode.go:148-159); kind 2: raw little-endian scalar (hash.go:84-98).
+ * roots (n x 32) = Keccak(concat of field outputs) per record. */
+int or_struct_roots(const uint8_t* rec, uint64_t n, uint32_t rec_len, const uint32_t* kind,
+                    const uint32_t* off, const uint32_t* len, uint32_t nf, uint8_t* roots, int nthreads) {
+    uint32_t msg_len = 0, maxb = 0;
+    for (uint32_t f = 0; f < nf; ++f) {
+        msg_len += kind[f] == 1 ? 32 : len[f];
+        if (kind[f] == 1 && len[f] > maxb) maxb = len[f];
+    }
+#pragma omp parallel num_threads(nthreads > 0 ? nthreads : 1)
+    {
+        uint8_t* msg = (uint8_t*)malloc(msg_len + 1);
+        uint8_t* fb = (uint8_t*)malloc(maxb + 4);
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < (int64_t)n; ++i) {
+            const uint8_t* r = rec + (uint64_t)i * rec_len;
+            uint32_t o = 0;
+            for (uint32_t f = 0; f < nf; ++f) {
+                if (kind[f] == 1) {
+                    for (int b = 0; b < 4; ++b) fb[b] = (uint8_t)(len[f] >> (8 * b));
+                    memcpy(fb + 4, r + off[f], len[f]);
+                    or_keccak256(fb, len[f] + 4, msg + o);
+                    o += 32;
+                } else {
+                    memcpy(msg + o, r + off[f], len[f]);
+                    o += len[f];
+                }
+            }
+            or_keccak256(msg, msg_len, roots + 32 * (uint64_t)i);
+        }
+        free(msg);
+        free(fb);
+    }
+    return 0;
+}

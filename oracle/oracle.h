@@ -25,5 +25,7 @@ int or_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n,
 int or_verify_merkle_branch(const uint8_t leaf[32], const uint8_t* branch, uint32_t depth,
                             uint64_t index, uint32_t tree_depth, const uint8_t root[32]);
 int or_merkle_root(const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_t out[32]);
+int or_struct_roots(const uint8_t* rec, uint64_t n, uint32_t rec_len, const uint32_t* kind,
+                    const uint32_t* off, const uint32_t* len, uint32_t nf, uint8_t* roots, int nthreads);
 
 #endif

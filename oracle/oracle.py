@@ -57,6 +57,8 @@ def lib():
         L.or_verify_merkle_branch.argtypes = [u8p, u8p, ctypes.c_uint32, ctypes.c_uint64,
                                               ctypes.c_uint32, u8p]
         L.or_merkle_root.argtypes = [u8p, u8p, ctypes.c_uint64, u8p]
+        L.or_struct_roots.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint32,
+                                      u8p, ctypes.c_int]
         for name in ("or_merkle_hash", "or_merkle_hash_var", "or_merkle_hash_gen",
                      "or_merkle_subtree_gen", "or_deposit_trie_build", "or_verify_merkle_branch",
                      "or_merkle_root"):
@@ -188,6 +190,18 @@ def merkle_root(values) -> bytes:
     if lib().or_merkle_root(_ptr(data), _ptr(offs), len(values), out) != 0:
         raise IndexError("index out of range")
     return out.raw
+
+
+# --------------------------------------------------------------- flat structs
+def struct_roots(records: np.ndarray, n: int, rec_len: int, fields, nthreads: int = 1) -> np.ndarray:
+    """fields: [(kind, offset, len)] with kind 1 = bytes (hashed), 2 = raw."""
+    rec = np.ascontiguousarray(records, dtype=np.uint8).reshape(-1)
+    kind = np.array([f[0] for f in fields], dtype=np.uint32)
+    off = np.array([f[1] for f in fields], dtype=np.uint32)
+    ln = np.array([f[2] for f in fields], dtype=np.uint32)
+    out = np.empty((n, 32), dtype=np.uint8)
+    lib().or_struct_roots(_ptr(rec), n, rec_len, _ptr(kind), _ptr(off), _ptr(ln), len(fields), _ptr(out), nthreads)
+    return out
 
 
 # --------------------------------------------------------------- pure Python (small inputs)

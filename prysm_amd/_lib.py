@@ -53,13 +53,28 @@ _SIGS = {
     "mk_dev_ssz_merkle_subtree": (_int, [_vp, _u64, _u32, _u32, _int, _vp, _vp, _u64, _vp]),
     "mk_dev_ssz_merkle_finish": (_int, [_vp, _u64, _u64, _vp, _vp]),
     "mk_ssz_merkle_hash_multi": (_int, [_vp, _u64, _u32, _int, _vp]),
+    "mk_ssz_struct_msg_len": (_u64, [_vp, _u32]),
+    "mk_ssz_struct_roots": (_int, [_vp, _u64, _u32, _vp, _u32, _vp]),
+    "mk_ssz_struct_list_workspace_bytes": (_u64, [_u64, _vp, _u32]),
+    "mk_dev_ssz_struct_list_root": (_int, [_vp, _u64, _u32, _vp, _u32, _vp, _vp, _u64, _vp]),
+    "mk_ssz_struct_list_root": (_int, [_vp, _u64, _u32, _vp, _u32, _vp]),
     "mk_deposit_trie_levels_bytes": (_u64, [_u64, _u32]),
     "mk_deposit_trie_build": (_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
+    "mk_dev_deposit_trie_build": (_int, [_vp, _vp, _u64, _u32, _vp, _vp, _vp]),
     "mk_verify_merkle_branches": (_int, [_vp, _vp, _vp, _u64, _u32, _u32, _vp, _vp]),
     "mk_dev_synth_fill": (_int, [_vp, _u64, _u64, _u64, _vp]),
     "mk_prof_enable": (_int, [_int]),
     "mk_prof_read": (_int, [_vp, _vp, _vp]),
 }
+
+MK_FIELD_BYTES = 1
+MK_FIELD_RAW = 2
+
+
+class Field(ctypes.Structure):
+    """mk_field: one field of a flat fixed-layout record."""
+    _fields_ = [("kind", ctypes.c_uint32), ("offset", ctypes.c_uint32), ("len", ctypes.c_uint32)]
+
 
 _lib = None
 

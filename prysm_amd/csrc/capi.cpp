@@ -127,6 +127,7 @@ uint64_t perms_for_len(uint64_t len) { return len / 136 + 1; }
 
 struct Pass {
     bool leaf;
+    bool wave;  // latency pass (k_wave) instead of the throughput pass (k_reduce)
     uint64_t nwg, nfast;
     ReduceArgs a;
     int in_ws;   // -1 = user input, else ping-pong slot
@@ -206,23 +207,27 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
             perms += (double)(cin / 2) + (cin % 2 ? 2.0 : 0.0);
         }
         uint64_t c = c1;
-        const bool final_pass = c1 <= kReduceSpan1;
-        uint32_t lv = final_pass ? remaining : std::min<uint32_t>(mk::kMaxPassLevels, remaining);
+        const bool wave = c1 <= mk::kWaveMaxC1;
+        const uint64_t span = wave ? mk::kWaveThreads : kReduceSpan1;
+        const bool final_pass = c1 <= span;
+        const uint32_t max_lv = wave ? mk::kWaveLevels : mk::kMaxPassLevels;
+        uint32_t lv = final_pass ? remaining : std::min<uint32_t>(max_lv, remaining);
         for (uint32_t l = 1; l < lv; ++l) {  // fused levels above the first
             if (c <= 1 && !pad_at_one) break;
             perms += (double)(c / 2) + (c % 2 ? 2.0 : 0.0);
             c = ceil_div(c, 2);
         }
         ps.perms = perms;
+        ps.wave = wave;
         a.levels = lv;
-        ps.nwg = ceil_div(c1, kReduceSpan1);
-        ps.nfast = std::min<uint64_t>(ps.nwg, a.c1_full / kReduceSpan1);
+        ps.nwg = ceil_div(c1, span);
+        ps.nfast = wave ? 0 : std::min<uint64_t>(ps.nwg, a.c1_full / kReduceSpan1);
         ps.in_ws = in_slot;
         if (final_pass) {
             if (!subtree) {
                 a.finalize = 1;
                 a.levels = 64;
-            } else if (c1 > kReduceSpan1 / 2 && lv < 2) {
+            } else if (!wave && c1 > kReduceSpan1 / 2 && lv < 2) {
                 return fail(MK_EINVAL, "planner: unsupported single-level pass");
             }
             ps.out_ws = -1;
@@ -270,7 +275,14 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
             HIPCHK(hipEventCreate(&rec.b));
             HIPCHK(hipEventRecord(rec.a, st));
         }
-        if (ps.nfast) {
+        if (ps.wave) {
+            a.wg_base = 0;
+            if (ps.leaf)
+                hipLaunchKernelGGL((mk::k_wave<true>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
+            else
+                hipLaunchKernelGGL((mk::k_wave<false>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
+            HIPCHK(hipGetLastError());
+        } else if (ps.nfast) {
             a.wg_base = 0;
             if (ps.leaf)
                 hipLaunchKernelGGL((mk::k_reduce<true, true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
@@ -278,7 +290,7 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                 hipLaunchKernelGGL((mk::k_reduce<false, true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
             HIPCHK(hipGetLastError());
         }
-        if (ps.nwg > ps.nfast) {
+        if (!ps.wave && ps.nwg > ps.nfast) {
             a.wg_base = ps.nfast;
             if (ps.leaf)
                 hipLaunchKernelGGL((mk::k_reduce<true, false>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads), 0,
@@ -560,6 +572,118 @@ int mk_ssz_merkle_hash_multi(const uint8_t* items, uint64_t n, uint32_t item_len
     return MK_OK;
 }
 
+// ---- struct hashing ---------------------------------------------------------------
+static int make_spec(const mk_field* fields, uint32_t nfields, uint32_t record_len, mk::StructSpec& sp) {
+    if (!fields || nfields == 0 || nfields > mk::kMaxStructFields)
+        return fail(MK_EINVAL, "nfields %u out of range (1..%u)", nfields, mk::kMaxStructFields);
+    std::memset(&sp, 0, sizeof sp);
+    uint32_t out = 0;
+    for (uint32_t f = 0; f < nfields; ++f) {
+        const mk_field& fd = fields[f];
+        if (fd.kind == MK_FIELD_BYTES) {
+            if (fd.offset % 4) return fail(MK_EINVAL, "bytes field %u: offset not 4-byte aligned", f);
+        } else if (fd.kind == MK_FIELD_RAW) {
+            if (fd.len != 1 && fd.len != 2 && fd.len != 4 && fd.len != 8)
+                return fail(MK_EINVAL, "raw field %u: len %u not in {1,2,4,8}", f, fd.len);
+        } else {
+            return fail(MK_EINVAL, "field %u: unknown kind %u", f, fd.kind);
+        }
+        if (record_len && (uint64_t)fd.offset + fd.len > record_len)
+            return fail(MK_EINVAL, "field %u exceeds the record", f);
+        sp.kind[f] = fd.kind;
+        sp.off[f] = fd.offset;
+        sp.len[f] = fd.len;
+        sp.out_off[f] = out;
+        out += fd.kind == MK_FIELD_BYTES ? 32 : fd.len;
+    }
+    if (record_len % 4) return fail(MK_EINVAL, "record_len %u not a multiple of 4", record_len);
+    sp.nfields = nfields;
+    sp.rec_len = record_len;
+    sp.msg_len = out;
+    return MK_OK;
+}
+
+// roots of n records into d_roots (n x 32); d_msg holds n x msg_len bytes
+static int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp, void* d_msg, void* d_roots,
+                               hipStream_t st) {
+    if (n == 0) return MK_OK;
+    hipLaunchKernelGGL(mk::k_struct_fields, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_rec, n, sp,
+                       (uint8_t*)d_msg);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(mk::k_keccak_fixed, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_msg, n,
+                       sp.msg_len, (uint4*)d_roots);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
+extern "C" uint64_t mk_ssz_struct_msg_len(const mk_field* fields, uint32_t nfields) {
+    mk::StructSpec sp;
+    if (make_spec(fields, nfields, 0, sp) != MK_OK) return 0;
+    return sp.msg_len;
+}
+
+static uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+
+extern "C" uint64_t mk_ssz_struct_list_workspace_bytes(uint64_t n, const mk_field* fields, uint32_t nfields) {
+    mk::StructSpec sp;
+    if (make_spec(fields, nfields, 0, sp) != MK_OK) return 0;
+    return align256(n * sp.msg_len) + align256(32 * n) + mk_ssz_merkle_workspace_bytes(n, 32);
+}
+
+extern "C" int mk_dev_ssz_struct_list_root(const void* d_records, uint64_t n, uint32_t record_len,
+                                           const mk_field* fields, uint32_t nfields, void* d_out32, void* d_ws,
+                                           uint64_t ws_bytes, void* stream) {
+    TRY(bind(-1));
+    mk::StructSpec sp;
+    TRY(make_spec(fields, nfields, record_len, sp));
+    if (ws_bytes < mk_ssz_struct_list_workspace_bytes(n, fields, nfields)) return fail(MK_ENOMEM, "workspace too small");
+    uint8_t* ws = (uint8_t*)d_ws;
+    uint8_t* msg = ws;
+    uint8_t* roots = ws + align256(n * sp.msg_len);
+    uint8_t* mws = roots + align256(32 * n);
+    hipStream_t st = (hipStream_t)stream;
+    TRY(launch_struct_roots(d_records, n, sp, msg, roots, st));
+    return mk_dev_ssz_merkle_hash(roots, n, 32, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), stream);
+}
+
+extern "C" int mk_ssz_struct_roots(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
+                                   uint32_t nfields, uint8_t* roots) {
+    mk::StructSpec sp;
+    TRY(make_spec(fields, nfields, record_len, sp));
+    if (n && (!records || !roots)) return fail(MK_EINVAL, "null pointer");
+    Locked L;
+    TRY(lock_current(L));
+    if (n == 0) return MK_OK;
+    hipStream_t st = L.c->stream;
+    TRY(grow(L.c->in, n * (size_t)record_len));
+    TRY(grow(L.c->ws, align256(n * sp.msg_len)));
+    TRY(grow(L.c->out, 32 * n));
+    HIPCHK(hipMemcpyAsync(L.c->in.p, records, n * (size_t)record_len, hipMemcpyHostToDevice, st));
+    TRY(launch_struct_roots(L.c->in.p, n, sp, L.c->ws.p, L.c->out.p, st));
+    HIPCHK(hipMemcpyAsync(roots, L.c->out.p, 32 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+extern "C" int mk_ssz_struct_list_root(const uint8_t* records, uint64_t n, uint32_t record_len,
+                                       const mk_field* fields, uint32_t nfields, uint8_t out[32]) {
+    mk::StructSpec sp;
+    TRY(make_spec(fields, nfields, record_len, sp));
+    if (!out || (n && !records)) return fail(MK_EINVAL, "null pointer");
+    Locked L;
+    TRY(lock_current(L));
+    hipStream_t st = L.c->stream;
+    const uint64_t wsb = mk_ssz_struct_list_workspace_bytes(n, fields, nfields);
+    TRY(grow(L.c->in, n * (size_t)record_len));
+    TRY(grow(L.c->ws, wsb));
+    TRY(grow(L.c->out, 32));
+    if (n) HIPCHK(hipMemcpyAsync(L.c->in.p, records, n * (size_t)record_len, hipMemcpyHostToDevice, st));
+    TRY(mk_dev_ssz_struct_list_root(L.c->in.p, n, record_len, fields, nfields, L.c->out.p, L.c->ws.p, wsb, st));
+    HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
 // ---- deposit trie -------------------------------------------------------------------
 uint64_t mk_deposit_trie_levels_bytes(uint64_t n, uint32_t depth) {
     if (n == 0) return 0;
@@ -571,27 +695,19 @@ uint64_t mk_deposit_trie_levels_bytes(uint64_t n, uint32_t depth) {
     return 32 * nodes;
 }
 
-int mk_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
-                          uint8_t* levels_out, uint8_t root[32]) {
-    if (!root || (n && !offs)) return fail(MK_EINVAL, "null pointer");
+int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t depth,
+                              void* d_levels, void* d_root32, void* stream) {
+    TRY(bind(-1));
+    if (!d_root32 || (n && (!d_offs || !d_levels))) return fail(MK_EINVAL, "null pointer");
     if (depth > 63) return fail(MK_EINVAL, "depth %u > 63", depth);
-    Locked L;
-    TRY(lock_current(L));
+    hipStream_t st = (hipStream_t)stream;
     if (n == 0) {
-        std::memset(root, 0, 32);
+        HIPCHK(hipMemsetAsync(d_root32, 0, 32, st));
         return MK_OK;
     }
-    hipStream_t st = L.c->stream;
-    const size_t inb = offs[n];
-    const uint64_t lv_bytes = mk_deposit_trie_levels_bytes(n, depth);
-    TRY(grow(L.c->in, inb));
-    TRY(grow(L.c->aux, 8 * (n + 1)));
-    TRY(grow(L.c->ws, lv_bytes));
-    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, data, inb, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(L.c->aux.p, offs, 8 * (n + 1), hipMemcpyHostToDevice, st));
-    uint4* lv = (uint4*)L.c->ws.p;
-    hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)L.c->in.p,
-                       (const uint64_t*)L.c->aux.p, n, lv);
+    uint4* lv = (uint4*)d_levels;
+    hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, d_offs, n,
+                       lv);
     HIPCHK(hipGetLastError());
     uint64_t c = n;
     uint4* cur = lv;
@@ -612,8 +728,32 @@ int mk_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n,
         HIPCHK(hipGetLastError());
         root_node = tail + 2 * (depth - d - 1);
     }
-    HIPCHK(hipMemcpyAsync(root, root_node, 32, hipMemcpyDeviceToHost, st));
-    if (levels_out) HIPCHK(hipMemcpyAsync(levels_out, lv, lv_bytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(d_root32, root_node, 32, hipMemcpyDeviceToDevice, st));
+    return MK_OK;
+}
+
+int mk_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
+                          uint8_t* levels_out, uint8_t root[32]) {
+    if (!root || (n && !offs)) return fail(MK_EINVAL, "null pointer");
+    if (depth > 63) return fail(MK_EINVAL, "depth %u > 63", depth);
+    Locked L;
+    TRY(lock_current(L));
+    if (n == 0) {
+        std::memset(root, 0, 32);
+        return MK_OK;
+    }
+    hipStream_t st = L.c->stream;
+    const size_t inb = offs[n];
+    const uint64_t lv_bytes = mk_deposit_trie_levels_bytes(n, depth);
+    TRY(grow(L.c->in, inb));
+    TRY(grow(L.c->aux, 8 * (n + 1)));
+    TRY(grow(L.c->ws, lv_bytes));
+    TRY(grow(L.c->out, 32));
+    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, data, inb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(L.c->aux.p, offs, 8 * (n + 1), hipMemcpyHostToDevice, st));
+    TRY(mk_dev_deposit_trie_build(L.c->in.p, (const uint64_t*)L.c->aux.p, n, depth, L.c->ws.p, L.c->out.p, st));
+    HIPCHK(hipMemcpyAsync(root, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
+    if (levels_out) HIPCHK(hipMemcpyAsync(levels_out, L.c->ws.p, lv_bytes, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return MK_OK;
 }

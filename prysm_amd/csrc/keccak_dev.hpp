@@ -130,7 +130,7 @@ __device__ __forceinline__ void round_fn(State& s, uint32_t rclo, uint32_t rchi)
 }
 
 #ifndef MK_ROUND_UNROLL
-#define MK_ROUND_UNROLL 4
+#define MK_ROUND_UNROLL 2
 #endif
 constexpr int kRoundUnroll = MK_ROUND_UNROLL;
 

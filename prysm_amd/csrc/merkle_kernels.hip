@@ -126,7 +126,7 @@ __device__ __forceinline__ void hash_final(uint4 r0, uint4 r1, uint64_t n, uint4
 // Fast 256-B window (two Keccak blocks).  The block loop is rolled so the
 // kernel keeps one keccak_f copy in its hot loop (I-cache).
 #ifndef MK_LOAD_ALL
-#define MK_LOAD_ALL 0
+#define MK_LOAD_ALL 1
 #endif
 #ifndef MK_MIN_WAVES
 #define MK_MIN_WAVES 1
@@ -366,6 +366,80 @@ template __global__ void k_reduce<false, true>(ReduceArgs);
 template __global__ void k_reduce<false, false>(ReduceArgs);
 
 // ----------------------------------------------------------------------------
+// Latency-oriented pass for the narrow top of the tree: one wave per
+// workgroup, one first-level node per lane, then up to 6 more levels inside
+// the wave (LDS hand-off, no cross-wave barrier).  Every level costs one
+// permutation latency, instead of the 2-4 serial permutations per level the
+// throughput kernel spends when few workgroups exist.
+template <bool LEAF>
+__global__ __launch_bounds__(kWaveThreads) void k_wave(ReduceArgs a) {
+    __shared__ uint4 lds[2 * kWaveThreads];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t wg = a.wg_base + blockIdx.x;
+    const uint64_t lo1 = wg * kWaveThreads;
+    const uint64_t c1 = a.c1;
+    const uint64_t m1 = (c1 - lo1) < kWaveThreads ? (c1 - lo1) : kWaveThreads;
+    if (tid < m1) {
+        const uint64_t j = lo1 + tid;
+        uint4 d0, d1;
+        if (LEAF && j < a.c1_full) {
+            hash_window256(reinterpret_cast<const uint4*>(a.items) + j * 16, d0, d1);
+        } else {
+            first_level_generic<LEAF>(a, j, d0, d1);
+        }
+        lds[2 * tid] = d0;
+        lds[2 * tid + 1] = d1;
+    }
+    __syncthreads();
+    uint64_t c = c1, m = m1;
+    int left = a.finalize ? 64 : (int)a.levels - 1;
+    int done = 0;
+    while (left > 0 && (c > 1 || a.pad_at_one)) {
+        const uint64_t mn = (m + 1) / 2;
+        const bool act = tid < mn;
+        uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+        bool padded = false;
+        if (act) {
+            l0 = lds[4 * tid];
+            l1 = lds[4 * tid + 1];
+            padded = !(2 * (uint64_t)tid + 1 < m);
+            if (!padded) {
+                r0 = lds[4 * tid + 2];
+                r1 = lds[4 * tid + 3];
+            }
+        }
+        __syncthreads();
+        if (act) {
+            uint4 d0, d1;
+            hash_pair(l0, l1, r0, r1, padded, d0, d1);
+            lds[2 * tid] = d0;
+            lds[2 * tid + 1] = d1;
+        }
+        __syncthreads();
+        c = (c + 1) / 2;
+        m = mn;
+        --left;
+        ++done;
+    }
+    uint4* out = reinterpret_cast<uint4*>(a.out);
+    if (a.finalize) {
+        if (tid == 0) {
+            uint4 d0, d1;
+            hash_final(lds[0], lds[1], a.n_items, d0, d1);
+            out[0] = d0;
+            out[1] = d1;
+        }
+    } else if (tid < m) {
+        const uint64_t lo_out = lo1 >> done;
+        out[2 * (lo_out + tid)] = lds[2 * tid];
+        out[2 * (lo_out + tid) + 1] = lds[2 * tid + 1];
+    }
+}
+
+template __global__ void k_wave<true>(ReduceArgs);
+template __global__ void k_wave<false>(ReduceArgs);
+
+// ----------------------------------------------------------------------------
 // Final hash for trees with <= 1 chunk: K(bytes[0,total) || [0^128 if n==0] || lenc)
 __global__ void k_final_small(const uint8_t* __restrict__ items, uint64_t total, uint64_t n, uint8_t* out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -454,6 +528,74 @@ __global__ __launch_bounds__(256) void k_keccak_var(const uint8_t* __restrict__ 
     sponge_generic(in + a, b - a, 0, false, 0, d0, d1);
     out[2 * i] = d0;
     out[2 * i + 1] = d1;
+}
+
+// ----------------------------------------------------------------------------
+// Struct hashing (hash.go:141-159) for flat fixed-layout records: every
+// record's message is the concatenation, in declaration order, of
+//   MK_FIELD_BYTES: Keccak(le32(len) || bytes)   (hashedEncoding, hash.go:100-107)
+//   MK_FIELD_RAW:   the raw little-endian bytes  (getEncoding of bool/uintN)
+// k_struct_fields writes those messages; k_keccak_fixed hashes them.
+
+// Keccak(le32(L) || A[0, L)) with 32-bit loads (A 4-byte aligned).
+__device__ __noinline__ void sponge_prefix4(const uint8_t* __restrict__ A, uint32_t L, uint4& d0, uint4& d1) {
+    const uint32_t* A32 = reinterpret_cast<const uint32_t*>(A);
+    const uint32_t len = L + 4;
+    const uint32_t nb = len / 136 + 1;
+    State s;
+    zero(s);
+    for (uint32_t b = 0; b < nb; ++b) {
+#pragma unroll
+        for (int w = 0; w < 17; ++w) {
+            const uint32_t m0 = b * 136 + 8u * w;  // message byte of this word
+            uint32_t half[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t m = m0 + 4u * h;  // 4-byte group [m, m+4) of the message
+                uint32_t v = 0;
+                if (m == 0) {
+                    v = L;
+                } else if (m + 4 <= len) {
+                    v = A32[(m - 4) / 4];
+                } else if (m < len) {
+                    for (uint32_t k = 0; k < len - m; ++k) v |= (uint32_t)A[m - 4 + k] << (8 * k);
+                }
+                if (m <= len && len < m + 4) v ^= 1u << (8 * (len - m));  // pad 0x01
+                half[h] = v;
+            }
+            if (b == nb - 1 && w == 16) half[1] ^= 0x80000000u;
+            s.lo[w] ^= half[0];
+            s.hi[w] ^= half[1];
+        }
+        keccak_f(s);
+    }
+    digest(s, d0, d1);
+}
+
+__global__ __launch_bounds__(256) void k_struct_fields(const uint8_t* __restrict__ rec, uint64_t n, StructSpec sp,
+                                                       uint8_t* __restrict__ msg) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* r = rec + i * sp.rec_len;
+    uint8_t* m = msg + i * sp.msg_len;
+    for (uint32_t f = 0; f < sp.nfields; ++f) {
+        const uint32_t off = sp.off[f], len = sp.len[f], out = sp.out_off[f];
+        if (sp.kind[f] == 1) {  // MK_FIELD_BYTES
+            uint4 d0, d1;
+            sponge_prefix4(r + off, len, d0, d1);
+            const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+            if ((out & 3u) == 0 && (((uintptr_t)m) & 3u) == 0) {
+                uint32_t* o = reinterpret_cast<uint32_t*>(m + out);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) o[k] = dw[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 32; ++k) m[out + k] = (uint8_t)(dw[k / 4] >> (8 * (k % 4)));
+            }
+        } else {  // MK_FIELD_RAW
+            for (uint32_t k = 0; k < len; ++k) m[out + k] = r[off + k];
+        }
+    }
 }
 
 // ----------------------------------------------------------------------------

@@ -9,6 +9,9 @@ constexpr uint32_t kReduceThreads = 256;             // 4 waves
 constexpr uint64_t kReduceSpan1 = 4 * kReduceThreads;  // first-level nodes per workgroup
 constexpr uint64_t kReduceSpan2 = kReduceSpan1 / 2;    // level-2 nodes per workgroup (LDS)
 constexpr uint32_t kMaxPassLevels = 5;               // levels per non-final pass (1024 -> 64)
+constexpr uint32_t kWaveThreads = 64;                // latency pass: one wave per workgroup
+constexpr uint32_t kWaveLevels = 7;                  // first level + 6 in-wave levels (64 -> 1)
+constexpr uint64_t kWaveMaxC1 = 1ull << 16;          // use the latency pass at or below this width
 
 struct ReduceArgs {
     const uint8_t* items;  // LEAF: item bytes; NODE: 32-B input nodes
@@ -26,8 +29,20 @@ struct ReduceArgs {
     uint64_t wg_base;      // workgroup index offset of this launch
 };
 
+constexpr uint32_t kMaxStructFields = 32;
+struct StructSpec {                 // flat fixed-layout record (hash.go:141-159)
+    uint32_t kind[kMaxStructFields];   // 1 = bytes (hashed with le32 prefix), 2 = raw scalar
+    uint32_t off[kMaxStructFields];    // byte offset inside the record
+    uint32_t len[kMaxStructFields];    // field length in bytes
+    uint32_t out_off[kMaxStructFields];  // byte offset inside the struct message
+    uint32_t nfields, rec_len, msg_len;
+};
+
 template <bool LEAF, bool FAST>
 __global__ void k_reduce(ReduceArgs a);
+__global__ void k_struct_fields(const uint8_t* rec, uint64_t n, StructSpec sp, uint8_t* msg);
+template <bool LEAF>
+__global__ void k_wave(ReduceArgs a);
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
 __global__ void k_finish_roots(const uint4* roots, uint64_t nroots, uint64_t n_items, uint4* out);
 __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);

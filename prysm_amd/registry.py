@@ -1,0 +1,148 @@
+"""Typed validator-registry path (BASELINE configs 1/3).
+
+The reference tree-hashes a registry reflectively, one Keccak call per field
+(shared/ssz/hash.go:118-159).  Its own plugin hook, ``ssz.Hashable``
+(hash.go:18-20, checked first at :57-58), lets a typed registry hash itself:
+``ValidatorRegistry.tree_hash_ssz()`` keeps the validators as one flat
+fixed-layout array and hands it to the engine (``mk_*ssz_struct*``): one
+launch hashes every bytes field (Keccak(le32(len)||bytes)), one hashes every
+144-byte struct message, then the fused merkleHash kernels reduce the list.
+
+Record layout (160 B, 4-byte aligned): the field order of ``pb.Validator``
+(proto/beacon/p2p/v1/types.pb.go:661-671) with ``StatusFlags`` widened from
+int32 to uint64 so SSZ accepts it (``makeEncoder`` rejects int32,
+ssz/encode.go:107-108; recorded deviation).
+"""
+from __future__ import annotations
+
+import ctypes
+import struct as _st
+
+import numpy as np
+
+from . import _lib
+from . import ssz as S
+from .hashutil import _ptr
+
+VALIDATOR_DTYPE = np.dtype([
+    ("pubkey", "u1", 48),
+    ("withdrawal_credentials_hash32", "u1", 32),
+    ("randao_commitment_hash32", "u1", 32),
+    ("randao_layers", "<u8"),
+    ("activation_epoch", "<u8"),
+    ("exit_epoch", "<u8"),
+    ("withdrawal_epoch", "<u8"),
+    ("penalized_epoch", "<u8"),
+    ("status_flags", "<u8"),
+])
+assert VALIDATOR_DTYPE.itemsize == 160
+
+# (kind, offset, len) in declaration order
+VALIDATOR_FIELDS = [(_lib.MK_FIELD_BYTES, 0, 48), (_lib.MK_FIELD_BYTES, 48, 32), (_lib.MK_FIELD_BYTES, 80, 32)] + \
+                   [(_lib.MK_FIELD_RAW, 112 + 8 * k, 8) for k in range(6)]
+
+# The same type for the reflective mirror (prysm_amd.ssz), for cross-checks.
+VALIDATOR_SSZ = S.Struct("ssz.ValidatorRecord", [
+    ("Pubkey", S.Bytes()), ("WithdrawalCredentialsHash32", S.Bytes()), ("RandaoCommitmentHash32", S.Bytes()),
+    ("RandaoLayers", S.Uint(64)), ("ActivationEpoch", S.Uint(64)), ("ExitEpoch", S.Uint(64)),
+    ("WithdrawalEpoch", S.Uint(64)), ("PenalizedEpoch", S.Uint(64)), ("StatusFlags", S.Uint(64))])
+
+
+def _fields(spec):
+    arr = (_lib.Field * len(spec))()
+    for i, (k, o, n) in enumerate(spec):
+        arr[i].kind, arr[i].offset, arr[i].len = k, o, n
+    return arr
+
+
+def struct_roots(records: np.ndarray, spec=VALIDATOR_FIELDS) -> np.ndarray:
+    """Struct hash of every record -> (n, 32) uint8."""
+    rec = np.ascontiguousarray(records)
+    n = len(rec)
+    raw = rec.view(np.uint8).reshape(-1)
+    out = np.empty((n, 32), dtype=np.uint8)
+    f = _fields(spec)
+    _lib.check(_lib.load().mk_ssz_struct_roots(_ptr(raw), n, rec.dtype.itemsize, f, len(spec), _ptr(out)),
+               "mk_ssz_struct_roots")
+    return out
+
+
+def struct_list_root(records: np.ndarray, spec=VALIDATOR_FIELDS) -> bytes:
+    """TreeHash of a list of such structs (makeSliceHasher -> merkleHash)."""
+    rec = np.ascontiguousarray(records)
+    raw = rec.view(np.uint8).reshape(-1)
+    out = ctypes.create_string_buffer(32)
+    f = _fields(spec)
+    _lib.check(_lib.load().mk_ssz_struct_list_root(_ptr(raw) if raw.size else None, len(rec), rec.dtype.itemsize,
+                                                   f, len(spec), out), "mk_ssz_struct_list_root")
+    return out.raw
+
+
+class ValidatorRegistry:
+    """[]*ValidatorRecord as one flat array; implements ssz.Hashable."""
+
+    def __init__(self, records: np.ndarray):
+        assert records.dtype == VALIDATOR_DTYPE
+        self.records = records
+
+    def __len__(self):
+        return len(self.records)
+
+    def tree_hash_ssz(self) -> bytes:
+        return struct_list_root(self.records)
+
+    TreeHashSSZ = tree_hash_ssz
+
+    def as_dicts(self):
+        """The same values in the reflective mirror's representation."""
+        out = []
+        for r in self.records:
+            out.append({"Pubkey": bytes(r["pubkey"]),
+                        "WithdrawalCredentialsHash32": bytes(r["withdrawal_credentials_hash32"]),
+                        "RandaoCommitmentHash32": bytes(r["randao_commitment_hash32"]),
+                        "RandaoLayers": int(r["randao_layers"]), "ActivationEpoch": int(r["activation_epoch"]),
+                        "ExitEpoch": int(r["exit_epoch"]), "WithdrawalEpoch": int(r["withdrawal_epoch"]),
+                        "PenalizedEpoch": int(r["penalized_epoch"]), "StatusFlags": int(r["status_flags"])})
+        return out
+
+
+# As a descriptor for prysm_amd.ssz.tree_hash (the Hashable hook is checked first).
+REGISTRY_HASHABLE = S.Hashable("ssz.ValidatorRegistry", lambda reg: reg.tree_hash_ssz())
+
+
+def state_root(registry: ValidatorRegistry, balances: np.ndarray) -> bytes:
+    """TreeHash of the synthetic State{ValidatorRegistry []*ValidatorRecord;
+    ValidatorBalances []uint64} (BASELINE config 3): Keccak(reg_root || bal_root)."""
+    reg = registry.tree_hash_ssz()
+    bal = np.ascontiguousarray(balances, dtype="<u8")
+    bal_root = S.merkle_hash_flat(bal.view(np.uint8), len(bal), 8)
+    from .hashutil import hash_batch_var
+
+    return hash_batch_var([reg + bal_root])[0]
+
+
+FAR_FUTURE_EPOCH = (1 << 64) - 1  # shared/params/config.go:118
+
+
+def synthetic_registry(n: int, seed: int) -> ValidatorRegistry:
+    """SURVEY.md §8d synthetic registry: PRNG bytes fields; epochs PRNG or
+    FarFutureEpoch; StatusFlags 0..3."""
+    rng = np.random.default_rng(seed & ((1 << 63) - 1))
+    rec = np.zeros(n, dtype=VALIDATOR_DTYPE)
+    rec["pubkey"] = rng.integers(0, 256, (n, 48), dtype=np.uint8)
+    rec["withdrawal_credentials_hash32"] = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    rec["randao_commitment_hash32"] = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    rec["randao_layers"] = rng.integers(0, 1 << 20, n, dtype=np.uint64)
+    rec["activation_epoch"] = rng.integers(0, 1 << 30, n, dtype=np.uint64)
+    far = np.uint64(FAR_FUTURE_EPOCH)
+    rec["exit_epoch"] = np.where(np.arange(n) % 3 == 0, rng.integers(0, 1 << 30, n, dtype=np.uint64), far)
+    rec["withdrawal_epoch"] = far
+    rec["penalized_epoch"] = np.where(np.arange(n) % 5 == 0, np.uint64(7), far)
+    rec["status_flags"] = np.arange(n, dtype=np.uint64) % 4
+    return ValidatorRegistry(rec)
+
+
+def synthetic_balances(n: int, seed: int) -> np.ndarray:
+    """32e9 Gwei +- PRNG."""
+    rng = np.random.default_rng((seed + 1) & ((1 << 63) - 1))
+    return (np.uint64(32 * 10**9) + rng.integers(0, 10**9, n, dtype=np.uint64) - np.uint64(5 * 10**8)).astype("<u8")

@@ -308,3 +308,50 @@ def test_verify_branches_batch(gpu):
     bad[3] += 1
     res = T.verify_merkle_branches(leaves, branches, 32, bad, roots)
     assert res[3] is False and sum(res) == len(idx) - 1
+
+
+# ------------------------------------------------------------------ typed registry (Hashable plugin)
+@pytest.mark.parametrize("n", [1, 2, 5, 300, 4099, 70_001])
+def test_registry_struct_roots_and_list_root(gpu, n):
+    from oracle import oracle as O
+    from prysm_amd import registry as R
+
+    reg = R.synthetic_registry(n, SEED + 91)
+    raw = reg.records.view(np.uint8).reshape(-1)
+    spec = [(k, o, l) for k, o, l in R.VALIDATOR_FIELDS]
+    want_roots = O.struct_roots(raw, n, 160, spec, nthreads=16)
+    assert np.array_equal(R.struct_roots(reg.records), want_roots)
+    assert reg.tree_hash_ssz() == O.merkle_hash_flat(want_roots.reshape(-1), n, 32, nthreads=16)
+
+
+def test_registry_equals_reflective_tree_hash(gpu):
+    """The Hashable fast path equals the reference's reflective TreeHash of
+    []*ValidatorRecord (oracle restatement and the host mirror)."""
+    from oracle import ssz_ref as OS
+    from prysm_amd import registry as R
+    from prysm_amd import ssz
+
+    reg = R.synthetic_registry(333, SEED + 92)
+    dicts = reg.as_dicts()
+    t_ref = ("slice", ("ptr", ("struct", "ssz.ValidatorRecord",
+                               [("Pubkey", ("bytes",)), ("WithdrawalCredentialsHash32", ("bytes",)),
+                                ("RandaoCommitmentHash32", ("bytes",))] +
+                               [(f, ("uint", 64)) for f in ("RandaoLayers", "ActivationEpoch", "ExitEpoch",
+                                                            "WithdrawalEpoch", "PenalizedEpoch", "StatusFlags")])))
+    want = OS.tree_hash(t_ref, dicts)
+    assert ssz.tree_hash(reg, R.REGISTRY_HASHABLE) == want
+    assert ssz.tree_hash(dicts, ssz.Slice(ssz.Ptr(R.VALIDATOR_SSZ))) == want
+
+
+def test_state_root(gpu):
+    from oracle import oracle as O
+    from prysm_amd import registry as R
+
+    n = 10_000
+    reg = R.synthetic_registry(n, SEED + 93)
+    bal = R.synthetic_balances(n, SEED + 93)
+    spec = [(k, o, l) for k, o, l in R.VALIDATOR_FIELDS]
+    roots = O.struct_roots(reg.records.view(np.uint8).reshape(-1), n, 160, spec, nthreads=16)
+    want = O.keccak256(O.merkle_hash_flat(roots.reshape(-1), n, 32) +
+                       O.merkle_hash_flat(bal.view(np.uint8), n, 8))
+    assert R.state_root(reg, bal) == want

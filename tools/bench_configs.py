@@ -1,0 +1,164 @@
+"""Single-GPU side benchmarks for the other BASELINE.json configs
+(bench.py --config c2|c3|c5).  Same JSON shape as the headline line; inputs
+resident in HBM before timing; hipEvent-free wall timing bracketed by
+torch.cuda.synchronize(); the dominant kernel is timed with the library's
+own hipEvents where the library exposes them (merkle passes).
+
+  c2: hashutil.Hash over 2^24 x 64-B messages (one Keccak-f each)
+  c3: TreeHash of a synthetic 1,000,000-validator State{registry, balances}
+      via the typed Hashable path (struct kernels + merkleHash)
+  c5: depth-32 deposit trie from 2^20 x 280-B synthetic deposits
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PEAK_INT_OPS = 256 * 4 * 32 * 2.4e9
+OPS_PER_PERM = 4320
+
+
+def _timeit(fn, steps, warmup):
+    import torch
+
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def _line(metric, value, unit, args, sec, perms, config, cpu=None, extra=None):
+    achieved = perms * OPS_PER_PERM / sec
+    out = {"metric": metric, "value": value, "unit": unit, "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": sec * 1e3, "higher_is_better": True, "scaling": "none",
+           "vs_baseline": None, "dtype": "u64 (Keccak lanes as u32 pairs)", "data": "synthetic",
+           "config": config,
+           "roofline": {"bound": "valu-int", "achieved": achieved / 1e12, "peak": PEAK_INT_OPS / 1e12,
+                        "unit": "Tops/s (int32 VALU, whole step)", "frac": achieved / PEAK_INT_OPS,
+                        "perms_per_step": perms}}
+    if extra:
+        out["roofline"].update(extra)
+    if cpu:
+        out["cpu_baseline"] = cpu
+    print(json.dumps(out), flush=True)
+
+
+def run_config(args):
+    import torch
+
+    sys.path.insert(0, ROOT)
+    from prysm_amd import _lib
+    from prysm_amd import device as D
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    _lib.init(0)
+    L = _lib.load()
+    st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    seed = 0x5EED000000000000
+
+    if args.config == "c2":
+        n = 1 << 24
+        msgs = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+        D.synth_fill(msgs, seed + 2)
+        out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        sec = _timeit(lambda: _lib.check(L.mk_dev_hash_batch(P(msgs), n, 64, P(out), st()), "c2"),
+                      args.steps, args.warmup)
+        cpu = None
+        if not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            m = 1 << 21
+            host = O.splitmix_bytes(m * 64, seed + 2)
+            t0 = time.perf_counter()
+            O.keccak256_batch(host, 64, nthreads=1)
+            dt = time.perf_counter() - t0
+            cpu = {"value": m / dt, "unit": "hashes/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle keccak256_batch, 2^21 x 64-B messages, 1 thread, {dt:.1f} s"}
+        _line("hashutil.Hash throughput, 2^24 x 64-B messages", n / sec, "hashes/s", args, sec, n,
+              {"workload": "C2: batched Keccak-256 of 2^24 x 64-B messages (1 GiB)", "n": n, "msg_len": 64},
+              cpu, {"hbm_GBps_algorithmic": n * 96 / sec / 1e9})
+        return
+
+    if args.config == "c3":
+        from prysm_amd import registry as R
+
+        n = 1_000_000
+        reg = R.synthetic_registry(n, seed + 3)
+        bal = R.synthetic_balances(n, seed + 3)
+        rec = torch.from_numpy(reg.records.view(np.uint8).reshape(-1).copy()).to(dev)
+        dbal = torch.from_numpy(bal.view(np.uint8).copy()).to(dev)
+        spec = R._fields(R.VALIDATOR_FIELDS)
+        nf = len(R.VALIDATOR_FIELDS)
+        ws = torch.empty(L.mk_ssz_struct_list_workspace_bytes(n, spec, nf) + 4096, dtype=torch.uint8, device=dev)
+        bws = D.merkle_workspace(n, 8, dev)
+        roots = torch.empty(64, dtype=torch.uint8, device=dev)
+        out = torch.empty(32, dtype=torch.uint8, device=dev)
+
+        def step():
+            _lib.check(L.mk_dev_ssz_struct_list_root(P(rec), n, 160, spec, nf, P(roots), P(ws), ws.numel(), st()),
+                       "registry")
+            D.merkle_hash(dbal, n, 8, out=roots[32:], ws=bws)
+            _lib.check(L.mk_dev_hash_batch(P(roots), 1, 64, P(out), st()), "state")
+
+        sec = _timeit(step, args.steps, args.warmup)
+        got = bytes(out.cpu().numpy())
+        assert got == R.state_root(reg, bal), "c3 root mismatch vs host-buffer path"
+        # perms: 3 field hashes + 2 struct blocks per validator, registry + balances merkle, final
+        perms = 5 * n + (n / 4 / 2) * 2 + n / 8 + (n / 16 / 2) * 2 + n / 32 + 1
+        cpu = None
+        if not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            m = 1 << 17
+            raw = reg.records[:m].view(np.uint8).reshape(-1)
+            t0 = time.perf_counter()
+            rr = O.struct_roots(raw, m, 160, R.VALIDATOR_FIELDS, nthreads=1)
+            O.merkle_hash_flat(rr.reshape(-1), m, 32)
+            O.merkle_hash_flat(bal[:m].view(np.uint8), m, 8)
+            dt = time.perf_counter() - t0
+            cpu = {"value": m / dt, "unit": "validators/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle struct_roots + merkleHash, 2^17 validators + balances, 1 thread, {dt:.1f} s"}
+        _line("TreeHash of a 1M-validator State (registry + balances)", n / sec, "validators/s", args, sec, perms,
+              {"workload": "C3: synthetic State{[]*ValidatorRecord, []uint64}, 1,000,000 validators",
+               "n": n, "root": got.hex()}, cpu)
+        return
+
+    if args.config == "c5":
+        n, dl, depth = 1 << 20, 280, 32
+        data = torch.empty(n * dl, dtype=torch.uint8, device=dev)
+        D.synth_fill(data, seed + 5)
+        offs = torch.arange(0, (n + 1) * dl, dl, dtype=torch.int64, device=dev)
+        lv = torch.empty(L.mk_deposit_trie_levels_bytes(n, depth), dtype=torch.uint8, device=dev)
+        root = torch.empty(32, dtype=torch.uint8, device=dev)
+        sec = _timeit(lambda: _lib.check(L.mk_dev_deposit_trie_build(P(data), P(offs), n, depth, P(lv), P(root),
+                                                                     st()), "c5"), args.steps, args.warmup)
+        perms = 3 * n + (n - 1) + (depth - 20)
+        cpu = None
+        if not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            m = 1 << 17
+            host = O.splitmix_bytes(m * dl, seed + 5)
+            deps = [bytes(host[i * dl:(i + 1) * dl]) for i in range(m)]
+            t0 = time.perf_counter()
+            O.deposit_trie_levels(deps)
+            dt = time.perf_counter() - t0
+            cpu = {"value": m / dt, "unit": "deposits/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle batch deposit trie, 2^17 x 280-B deposits, 1 thread, {dt:.1f} s "
+                             "(the reference's incremental UpdateDepositTrie does 35 perms/deposit, "
+                             "this batch form 4)"}
+        _line("deposit trie build, 2^20 x 280-B deposits, depth 32", n / sec, "deposits/s", args, sec, perms,
+              {"workload": "C5: trieutil deposit trie, 2^20 synthetic 280-B deposits", "n": n,
+               "root": bytes(root.cpu().numpy()).hex()}, cpu)
+        return
+
+
+import numpy as np  # noqa: E402
