@@ -20,6 +20,11 @@ using mk::ReduceArgs;
 using mk::kReduceSpan1;
 using mk::kReduceThreads;
 
+#ifndef MK_WAVE2
+#define MK_WAVE2 1
+#endif
+constexpr bool kWave2 = MK_WAVE2 != 0;  // two-lanes-per-state latency pass
+
 thread_local std::string t_err;
 thread_local int t_dev = -1;
 
@@ -208,9 +213,9 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         }
         uint64_t c = c1;
         const bool wave = c1 <= mk::kWaveMaxC1;
-        const uint64_t span = wave ? mk::kWaveThreads : kReduceSpan1;
+        const uint64_t span = wave ? (kWave2 ? mk::kWave2Span : mk::kWaveThreads) : kReduceSpan1;
         const bool final_pass = c1 <= span;
-        const uint32_t max_lv = wave ? mk::kWaveLevels : mk::kMaxPassLevels;
+        const uint32_t max_lv = wave ? (kWave2 ? mk::kWave2Levels : mk::kWaveLevels) : mk::kMaxPassLevels;
         uint32_t lv = final_pass ? remaining : std::min<uint32_t>(max_lv, remaining);
         for (uint32_t l = 1; l < lv; ++l) {  // fused levels above the first
             if (c <= 1 && !pad_at_one) break;
@@ -277,10 +282,17 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
         }
         if (ps.wave) {
             a.wg_base = 0;
-            if (ps.leaf)
-                hipLaunchKernelGGL((mk::k_wave<true>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
-            else
-                hipLaunchKernelGGL((mk::k_wave<false>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
+            if (kWave2) {
+                if (ps.leaf)
+                    hipLaunchKernelGGL((mk::k_wave2<true>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
+                else
+                    hipLaunchKernelGGL((mk::k_wave2<false>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
+            } else {
+                if (ps.leaf)
+                    hipLaunchKernelGGL((mk::k_wave<true>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
+                else
+                    hipLaunchKernelGGL((mk::k_wave<false>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
+            }
             HIPCHK(hipGetLastError());
         } else if (ps.nfast) {
             a.wg_base = 0;

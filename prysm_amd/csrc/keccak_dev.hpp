@@ -180,3 +180,84 @@ __device__ __forceinline__ void digest(const State& s, uint4& d0, uint4& d1) {
 }
 
 }  // namespace mk
+
+// ============================================================================
+// Two lanes per state (latency form).  Lane pair (2k, 2k+1) holds one state:
+// the even lane the low 32-bit halves of all 25 lanes, the odd lane the high
+// halves.  Every 64-bit rotation needs the partner's half (one DPP
+// quad_perm [1,0,3,2] move) and ONE v_alignbit_b32 per lane instead of two,
+// so a lane issues 120 instructions per round instead of 180: for the
+// narrow top of a tree, where one permutation's latency on a lone wave is
+// the cost of a whole level, that is ~1.6x less time per level.
+namespace mk {
+namespace pair {
+
+__device__ __forceinline__ uint32_t partner(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1 /* quad_perm [1,0,3,2] */, 0xF, 0xF, false);
+}
+
+// own half of rotl64 by N, given own and partner halves (same formula for
+// the low and the high lane).
+template <int N>
+__device__ __forceinline__ uint32_t rot(uint32_t own, uint32_t par) {
+    if constexpr (N == 0)
+        return own;
+    else if constexpr (N == 32)
+        return par;
+    else if constexpr (N < 32)
+        return funnel(own, par, 32 - N);
+    else
+        return funnel(par, own, 64 - N);
+}
+
+struct Half {
+    uint32_t v[25];
+};
+
+template <int I>
+__device__ __forceinline__ void rho_pi_one(const Half& a, uint32_t (&b)[25]) {
+    constexpr int x = I % 5, y = I / 5;
+    constexpr int dst = y + 5 * ((2 * x + 3 * y) % 5);
+    constexpr int r = MK_RHO(I);
+    if constexpr (r == 0)
+        b[dst] = a.v[I];
+    else
+        b[dst] = rot<r>(a.v[I], partner(a.v[I]));
+}
+
+template <int... Is>
+__device__ __forceinline__ void rho_pi_all(const Half& a, uint32_t (&b)[25], std::integer_sequence<int, Is...>) {
+    (rho_pi_one<Is>(a, b), ...);
+}
+
+__device__ __forceinline__ void round_fn(Half& s, uint32_t rc_own) {
+    uint32_t c[5], r[5];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) c[x] = xor3(xor3(s.v[x], s.v[x + 5], s.v[x + 10]), s.v[x + 15], s.v[x + 20]);
+#pragma unroll
+    for (int x = 0; x < 5; ++x) r[x] = rot<1>(c[x], partner(c[x]));
+#pragma unroll
+    for (int i = 0; i < 25; ++i) s.v[i] = xor3(s.v[i], c[(i % 5 + 4) % 5], r[(i % 5 + 1) % 5]);
+    uint32_t b[25];
+    rho_pi_all(s, b, std::make_integer_sequence<int, 25>{});
+#pragma unroll
+    for (int y = 0; y < 5; ++y)
+#pragma unroll
+        for (int x = 0; x < 5; ++x)
+            s.v[x + 5 * y] = chi3(b[x + 5 * y], b[(x + 1) % 5 + 5 * y], b[(x + 2) % 5 + 5 * y]);
+    s.v[0] ^= rc_own;
+}
+
+// odd = this lane holds the high halves
+__device__ __forceinline__ void keccak_f(Half& s, bool odd) {
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < 24; ++r) round_fn(s, odd ? kRcHi[r] : kRcLo[r]);
+}
+
+__device__ __forceinline__ void zero(Half& s) {
+#pragma unroll
+    for (int i = 0; i < 25; ++i) s.v[i] = 0u;
+}
+
+}  // namespace pair
+}  // namespace mk

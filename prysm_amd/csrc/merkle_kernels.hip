@@ -440,6 +440,171 @@ template __global__ void k_wave<true>(ReduceArgs);
 template __global__ void k_wave<false>(ReduceArgs);
 
 // ----------------------------------------------------------------------------
+// Latency pass with two lanes per state (keccak_dev.hpp, mk::pair): lane pair
+// (2k, 2k+1) owns node k; the even lane carries the low 32-bit halves of the
+// Keccak lanes, the odd lane the high halves.  Nodes live in LDS as 8 dwords;
+// a lane touches dwords 2w + odd (w = 0..3) of every node.
+namespace {
+
+// K(L || R) or K(L || 0^128) on own halves (pair-uniform `padded`).
+__device__ __forceinline__ void hash_pair2(const uint32_t (&l)[4], const uint32_t (&r)[4], bool padded, bool odd,
+                                           uint32_t (&d)[4]) {
+    pair::Half s;
+    pair::zero(s);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s.v[w] = l[w];
+    if (!padded) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) s.v[4 + w] = r[w];
+    }
+    const int nperm = padded ? 2 : 1;
+#pragma unroll 1
+    for (int k = 0; k < nperm; ++k) {
+        if (k == nperm - 1) {
+            if (!odd) {
+                if (padded)
+                    s.v[3] ^= 1u;
+                else
+                    s.v[8] ^= 1u;
+            } else {
+                s.v[16] ^= 0x80000000u;
+            }
+        }
+        pair::keccak_f(s, odd);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) d[w] = s.v[w];
+}
+
+// full 256-B window on own halves (two blocks, one keccak_f copy)
+__device__ __forceinline__ void hash_window2(const uint32_t* __restrict__ w32, bool odd, uint32_t (&d)[4]) {
+    pair::Half s;
+    pair::zero(s);
+    const uint32_t p = odd ? 1u : 0u;
+#pragma unroll 1
+    for (int b = 0; b < 2; ++b) {
+        if (b == 0) {
+#pragma unroll
+            for (int w = 0; w < 17; ++w) s.v[w] ^= w32[2 * w + p];
+        } else {
+#pragma unroll
+            for (int w = 0; w < 15; ++w) s.v[w] ^= w32[2 * (17 + w) + p];
+            if (!odd)
+                s.v[15] ^= 1u;
+            else
+                s.v[16] ^= 0x80000000u;
+        }
+        pair::keccak_f(s, odd);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) d[w] = s.v[w];
+}
+
+}  // namespace
+
+template <bool LEAF>
+__global__ __launch_bounds__(kWaveThreads) void k_wave2(ReduceArgs a) {
+    __shared__ uint32_t lds[8 * kWave2Span];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t k = tid >> 1;          // node slot of this lane pair
+    const bool odd = (tid & 1u) != 0;
+    const uint32_t p = odd ? 1u : 0u;
+    const uint64_t wg = a.wg_base + blockIdx.x;
+    const uint64_t lo1 = wg * kWave2Span;
+    const uint64_t c1 = a.c1;
+    const uint64_t m1 = (c1 - lo1) < kWave2Span ? (c1 - lo1) : kWave2Span;
+    if (k < m1) {
+        const uint64_t j = lo1 + k;
+        uint32_t d[4];
+        if constexpr (LEAF) {
+            if (j < a.c1_full) {
+                hash_window2(reinterpret_cast<const uint32_t*>(a.items) + j * 64, odd, d);
+            } else {  // ragged window: both lanes run the full-state sponge
+                uint4 d0, d1;
+                first_level_generic<true>(a, j, d0, d1);
+                d[0] = odd ? d0.y : d0.x;
+                d[1] = odd ? d0.w : d0.z;
+                d[2] = odd ? d1.y : d1.x;
+                d[3] = odd ? d1.w : d1.z;
+            }
+        } else {
+            const uint32_t* in = reinterpret_cast<const uint32_t*>(a.items);
+            uint32_t l[4], r[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int w = 0; w < 4; ++w) l[w] = in[16 * j + 2 * w + p];
+            if (a.cin == 1 && !a.pad_at_one) {  // single node: it is the root
+#pragma unroll
+                for (int w = 0; w < 4; ++w) d[w] = l[w];
+            } else {
+                const bool padded = !(2 * j + 1 < a.cin);
+                if (!padded) {
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) r[w] = in[16 * j + 8 + 2 * w + p];
+                }
+                hash_pair2(l, r, padded, odd, d);
+            }
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) lds[8 * k + 2 * w + p] = d[w];
+    }
+    __syncthreads();
+    uint64_t c = c1, m = m1;
+    int left = a.finalize ? 64 : (int)a.levels - 1;
+    int done = 0;
+    while (left > 0 && (c > 1 || a.pad_at_one)) {
+        const uint64_t mn = (m + 1) / 2;
+        const bool act = k < mn;
+        uint32_t l[4], r[4] = {0, 0, 0, 0};
+        bool padded = false;
+        if (act) {
+            padded = !(2 * (uint64_t)k + 1 < m);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) l[w] = lds[16 * k + 2 * w + p];
+            if (!padded) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) r[w] = lds[16 * k + 8 + 2 * w + p];
+            }
+        }
+        __syncthreads();
+        if (act) {
+            uint32_t d[4];
+            hash_pair2(l, r, padded, odd, d);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) lds[8 * k + 2 * w + p] = d[w];
+        }
+        __syncthreads();
+        c = (c + 1) / 2;
+        m = mn;
+        --left;
+        ++done;
+    }
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
+    if (a.finalize) {
+        if (k == 0) {  // K(root || le64(n) || 0^24) on lanes 0/1
+            pair::Half s;
+            pair::zero(s);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) s.v[w] = lds[2 * w + p];
+            s.v[4] = odd ? (uint32_t)(a.n_items >> 32) : (uint32_t)a.n_items;
+            if (!odd)
+                s.v[8] ^= 1u;
+            else
+                s.v[16] ^= 0x80000000u;
+            pair::keccak_f(s, odd);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) out[2 * w + p] = s.v[w];
+        }
+    } else if (k < m) {
+        const uint64_t lo_out = lo1 >> done;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) out[8 * (lo_out + k) + 2 * w + p] = lds[8 * k + 2 * w + p];
+    }
+}
+
+template __global__ void k_wave2<true>(ReduceArgs);
+template __global__ void k_wave2<false>(ReduceArgs);
+
+// ----------------------------------------------------------------------------
 // Final hash for trees with <= 1 chunk: K(bytes[0,total) || [0^128 if n==0] || lenc)
 __global__ void k_final_small(const uint8_t* __restrict__ items, uint64_t total, uint64_t n, uint8_t* out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;

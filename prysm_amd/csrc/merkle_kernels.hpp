@@ -12,6 +12,8 @@ constexpr uint32_t kMaxPassLevels = 5;               // levels per non-final pas
 constexpr uint32_t kWaveThreads = 64;                // latency pass: one wave per workgroup
 constexpr uint32_t kWaveLevels = 7;                  // first level + 6 in-wave levels (64 -> 1)
 constexpr uint64_t kWaveMaxC1 = 1ull << 16;          // use the latency pass at or below this width
+constexpr uint32_t kWave2Span = kWaveThreads / 2;    // two lanes per state: 32 nodes per wave
+constexpr uint32_t kWave2Levels = 6;                 // first level + 5 in-wave levels (32 -> 1)
 
 struct ReduceArgs {
     const uint8_t* items;  // LEAF: item bytes; NODE: 32-B input nodes
@@ -43,6 +45,8 @@ __global__ void k_reduce(ReduceArgs a);
 __global__ void k_struct_fields(const uint8_t* rec, uint64_t n, StructSpec sp, uint8_t* msg);
 template <bool LEAF>
 __global__ void k_wave(ReduceArgs a);
+template <bool LEAF>
+__global__ void k_wave2(ReduceArgs a);
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
 __global__ void k_finish_roots(const uint4* roots, uint64_t nroots, uint64_t n_items, uint4* out);
 __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);
