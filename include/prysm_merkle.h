@@ -136,10 +136,13 @@ int mk_ssz_struct_list_root(const uint8_t* records, uint64_t n, uint32_t record_
 uint64_t mk_deposit_trie_levels_bytes(uint64_t n, uint32_t depth);
 int mk_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
                           uint8_t* levels_out, uint8_t root[32]);
-/* Device-resident build: d_offs (n+1 u64) and d_levels
- * (mk_deposit_trie_levels_bytes) in device memory; root to d_root32. */
-int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t depth,
-                              void* d_levels, void* d_root32, void* stream);
+/* Device-resident build: d_levels (mk_deposit_trie_levels_bytes) and the
+ * deposits in device memory; root to d_root32.  Deposit i is
+ * d_data[d_offs[i], d_offs[i+1]) or, with d_offs == NULL, the fixed-length
+ * record d_data[i*fixed_len, (i+1)*fixed_len) (the 280-B deposit-data layout
+ * of core/blocks/block.go:103-130). */
+int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len,
+                              uint32_t depth, void* d_levels, void* d_root32, void* stream);
 /* Batched VerifyMerkleBranch: ok[i] = fold(leaves[i], branches[i*depth..],
  * indices[i] + 2^tree_depth) == roots[i]. */
 int mk_verify_merkle_branches(const uint8_t* leaves, const uint8_t* branches, const uint64_t* indices,

@@ -60,7 +60,7 @@ _SIGS = {
     "mk_ssz_struct_list_root": (_int, [_vp, _u64, _u32, _vp, _u32, _vp]),
     "mk_deposit_trie_levels_bytes": (_u64, [_u64, _u32]),
     "mk_deposit_trie_build": (_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
-    "mk_dev_deposit_trie_build": (_int, [_vp, _vp, _u64, _u32, _vp, _vp, _vp]),
+    "mk_dev_deposit_trie_build": (_int, [_vp, _vp, _u64, _u32, _u32, _vp, _vp, _vp]),
     "mk_verify_merkle_branches": (_int, [_vp, _vp, _vp, _u64, _u32, _u32, _vp, _vp]),
     "mk_dev_synth_fill": (_int, [_vp, _u64, _u64, _u64, _vp]),
     "mk_prof_enable": (_int, [_int]),

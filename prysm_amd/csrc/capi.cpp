@@ -707,10 +707,10 @@ uint64_t mk_deposit_trie_levels_bytes(uint64_t n, uint32_t depth) {
     return 32 * nodes;
 }
 
-int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t depth,
-                              void* d_levels, void* d_root32, void* stream) {
+int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len,
+                              uint32_t depth, void* d_levels, void* d_root32, void* stream) {
     TRY(bind(-1));
-    if (!d_root32 || (n && (!d_offs || !d_levels))) return fail(MK_EINVAL, "null pointer");
+    if (!d_root32 || (n && !d_levels) || (n && !d_offs && !d_data && fixed_len)) return fail(MK_EINVAL, "null pointer");
     if (depth > 63) return fail(MK_EINVAL, "depth %u > 63", depth);
     hipStream_t st = (hipStream_t)stream;
     if (n == 0) {
@@ -718,13 +718,24 @@ int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64
         return MK_OK;
     }
     uint4* lv = (uint4*)d_levels;
-    hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, d_offs, n,
-                       lv);
+    if (d_offs) {
+        hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, d_offs,
+                           n, lv);
+    } else if (fixed_len % 8 == 0 && ((uintptr_t)d_data % 8) == 0) {
+        hipLaunchKernelGGL(mk::k_keccak_words, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint2*)d_data, n,
+                           fixed_len / 8, lv);
+    } else {
+        hipLaunchKernelGGL(mk::k_keccak_fixed, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, n,
+                           fixed_len, lv);
+    }
     HIPCHK(hipGetLastError());
+    // level d lives at lv + 2 * sum_{i<d} count_i (uint4 units).  Wide levels:
+    // one launch per level (every lane busy); narrow top (<= 2^15 nodes) plus
+    // the zero-sibling tail: k_trie_top2, 6 levels per workgroup of 64 inputs.
     uint64_t c = n;
     uint4* cur = lv;
     uint32_t d = 0;
-    while (d < depth && c > 1) {
+    while (d < depth && c > (1ull << 15)) {
         uint4* nxt = cur + 2 * c;
         const uint64_t cn = (c + 1) / 2;
         hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(cn, 256)), dim3(256), 0, st, cur, c, nxt);
@@ -733,13 +744,30 @@ int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64
         c = cn;
         ++d;
     }
-    uint4* root_node = cur;
-    if (d < depth) {  // single node left: (node || 0^32) up to the top
-        uint4* tail = cur + 2;
-        hipLaunchKernelGGL(mk::k_trie_tail, dim3(1), dim3(64), 0, st, cur, depth - d, tail);
+    while (d < depth) {
+        const uint64_t nwg = ceil_div(c, 2 * mk::kWave2Span);
+        // levels this launch: up to 6 while several workgroups remain; the last
+        // (single-workgroup) launch runs to the top of the trie
+        uint32_t k = 0;
+        uint64_t cc = c;
+        if (nwg == 1) {
+            k = depth - d;
+        } else {
+            while (k < mk::kWave2Levels && cc > 1) {
+                cc = (cc + 1) / 2;
+                ++k;
+            }
+        }
+        hipLaunchKernelGGL(mk::k_trie_top2, dim3(nwg), dim3(mk::kWaveThreads), 0, st, (const uint32_t*)cur, c,
+                           (uint32_t*)(cur + 2 * c), k);
         HIPCHK(hipGetLastError());
-        root_node = tail + 2 * (depth - d - 1);
+        for (uint32_t i = 0; i < k; ++i) {
+            cur += 2 * c;
+            c = (c + 1) / 2;
+        }
+        d += k;
     }
+    uint4* root_node = cur;
     HIPCHK(hipMemcpyAsync(d_root32, root_node, 32, hipMemcpyDeviceToDevice, st));
     return MK_OK;
 }
@@ -761,9 +789,14 @@ int mk_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n,
     TRY(grow(L.c->aux, 8 * (n + 1)));
     TRY(grow(L.c->ws, lv_bytes));
     TRY(grow(L.c->out, 32));
+    bool uniform = offs[0] == 0;
+    const uint64_t len0 = offs[1] - offs[0];
+    for (uint64_t i = 1; uniform && i < n; ++i) uniform = (offs[i + 1] - offs[i]) == len0;
+    uniform = uniform && len0 <= UINT32_MAX;
     if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, data, inb, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(L.c->aux.p, offs, 8 * (n + 1), hipMemcpyHostToDevice, st));
-    TRY(mk_dev_deposit_trie_build(L.c->in.p, (const uint64_t*)L.c->aux.p, n, depth, L.c->ws.p, L.c->out.p, st));
+    if (!uniform) HIPCHK(hipMemcpyAsync(L.c->aux.p, offs, 8 * (n + 1), hipMemcpyHostToDevice, st));
+    TRY(mk_dev_deposit_trie_build(L.c->in.p, uniform ? nullptr : (const uint64_t*)L.c->aux.p, n,
+                                  uniform ? (uint32_t)len0 : 0, depth, L.c->ws.p, L.c->out.p, st));
     HIPCHK(hipMemcpyAsync(root, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
     if (levels_out) HIPCHK(hipMemcpyAsync(levels_out, L.c->ws.p, lv_bytes, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));

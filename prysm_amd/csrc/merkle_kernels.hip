@@ -604,6 +604,63 @@ __global__ __launch_bounds__(kWaveThreads) void k_wave2(ReduceArgs a) {
 template __global__ void k_wave2<true>(ReduceArgs);
 template __global__ void k_wave2<false>(ReduceArgs);
 
+// Narrow top of the deposit trie, two lanes per state: the workgroup owns 64
+// input nodes of level d and writes up to `levels` levels to the level array;
+// once the count is 1 it continues with node = K(node || 0^32) (the levels
+// above the last populated one, deposit_trie.go:33-38), so the top of the
+// trie and its zero-sibling tail are one launch.
+__global__ __launch_bounds__(kWaveThreads) void k_trie_top2(const uint32_t* __restrict__ in, uint64_t cin,
+                                                            uint32_t* __restrict__ lv_out, uint32_t levels) {
+    __shared__ uint32_t lds[8 * kWave2Span];
+    const uint32_t tid = threadIdx.x, k = tid >> 1;
+    const bool odd = (tid & 1u) != 0;
+    const uint32_t p = odd ? 1u : 0u;
+    uint64_t c = cin;
+    uint64_t lo = (uint64_t)blockIdx.x * 2 * kWave2Span;  // first input node of this workgroup
+    uint64_t m = (c - lo) < 2 * kWave2Span ? (c - lo) : 2 * kWave2Span;
+    uint32_t* dst = lv_out;
+    for (uint32_t l = 0; l < levels; ++l) {
+        const uint64_t cn = (c + 1) / 2, mn = (m + 1) / 2;
+        const bool act = k < mn;
+        uint32_t a[4], b[4] = {0, 0, 0, 0};
+        if (act) {
+            const bool right = 2 * (uint64_t)k + 1 < m;
+            if (l == 0) {
+                const uint64_t base = 8 * (lo + 2 * (uint64_t)k);
+#pragma unroll
+                for (int w = 0; w < 4; ++w) a[w] = in[base + 2 * w + p];
+                if (right) {
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) b[w] = in[base + 8 + 2 * w + p];
+                }
+            } else {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) a[w] = lds[16 * k + 2 * w + p];
+                if (right) {
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) b[w] = lds[16 * k + 8 + 2 * w + p];
+                }
+            }
+        }
+        __syncthreads();
+        if (act) {
+            uint32_t d[4];
+            hash_pair2(a, b, false, odd, d);
+            const uint64_t g = lo / 2 + k;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                lds[8 * k + 2 * w + p] = d[w];
+                dst[8 * g + 2 * w + p] = d[w];
+            }
+        }
+        __syncthreads();
+        dst += 8 * cn;
+        c = cn;
+        m = mn;
+        lo /= 2;
+    }
+}
+
 // ----------------------------------------------------------------------------
 // Final hash for trees with <= 1 chunk: K(bytes[0,total) || [0^128 if n==0] || lenc)
 __global__ void k_final_small(const uint8_t* __restrict__ items, uint64_t total, uint64_t n, uint8_t* out) {
@@ -760,6 +817,128 @@ __global__ __launch_bounds__(256) void k_struct_fields(const uint8_t* __restrict
         } else {  // MK_FIELD_RAW
             for (uint32_t k = 0; k < len; ++k) m[out + k] = r[off + k];
         }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// n messages of msg_len bytes, msg_len % 8 == 0, 8-byte aligned: whole-word
+// loads only (deposit leaves: 280 B = 35 words = 3 blocks).
+__global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ in, uint64_t n, uint32_t nwords,
+                                                      uint4* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint2* p = in + i * nwords;
+    const uint32_t nb = nwords / 17 + 1;
+    State s;
+    zero(s);
+    if ((((uintptr_t)p) & 7u) == 0) {
+        // 16-B loads: a message starts 16-B aligned or 8 bytes past it; each
+        // block reads the 9 aligned 16-B units that cover its 17 words and
+        // selects per lane (deposit leaves: 35 words, 3 blocks)
+        const uint32_t so = (((uintptr_t)p) & 15u) ? 1u : 0u;
+        const uint4* q = reinterpret_cast<const uint4*>(p - so);
+        const uint32_t nq = (nwords + so + 1) / 2;
+#pragma unroll 1
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t first = 17 * b + so;  // aligned word index of block word 0
+            const uint32_t pb = first >> 1, odd = first & 1u;
+            uint2 e[18];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const uint4 t = (pb + k) < nq ? ld_nt(q + pb + k) : make_uint4(0, 0, 0, 0);
+                e[2 * k] = make_uint2(t.x, t.y);
+                e[2 * k + 1] = make_uint2(t.z, t.w);
+            }
+#pragma unroll
+            for (int w = 0; w < 17; ++w) {
+                const uint32_t idx = 17 * b + w;
+                // static-index select (a conditional index would spill e[] to scratch)
+                const uint32_t msk = 0u - odd;
+                uint2 v = make_uint2(__builtin_amdgcn_bitop3_b32(e[w].x, e[w + 1].x, msk, 0xD8),
+                                     __builtin_amdgcn_bitop3_b32(e[w].y, e[w + 1].y, msk, 0xD8));
+                if (idx >= nwords) v = make_uint2(idx == nwords ? 1u : 0u, 0u);  // zero / domain pad
+                s.lo[w] ^= v.x;
+                s.hi[w] ^= v.y;
+            }
+            if (b == nb - 1) s.hi[16] ^= 0x80000000u;
+            keccak_f(s);
+        }
+    } else {
+#pragma unroll 1
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t base = b * 17;
+#pragma unroll
+            for (int w = 0; w < 17; ++w) {
+                const uint32_t idx = base + w;
+                if (idx < nwords) {
+                    const uint2 v = ld_nt(p + idx);
+                    s.lo[w] ^= v.x;
+                    s.hi[w] ^= v.y;
+                } else if (idx == nwords) {
+                    s.lo[w] ^= 1u;  // domain pad byte right after the message
+                }
+            }
+            if (b == nb - 1) s.hi[16] ^= 0x80000000u;
+            keccak_f(s);
+        }
+    }
+    uint4 d0, d1;
+    digest(s, d0, d1);
+    out[2 * i] = d0;
+    out[2 * i + 1] = d1;
+}
+
+// Deposit-trie levels, fused: the workgroup owns input nodes
+// [512*wg, 512*wg + 512) of level d (count cin) and writes `levels` levels
+// d+1 .. d+levels to their slots of the level array (every level is kept:
+// GenerateMerkleBranch reads them).  Missing right child = 0^32
+// (deposit_trie.go:35-37).  One node per thread per level.
+__global__ __launch_bounds__(256) void k_trie_reduce(const uint4* __restrict__ in, uint64_t cin,
+                                                     uint4* __restrict__ lv_out, uint32_t levels) {
+    __shared__ uint4 lds[2 * 256];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t wg = blockIdx.x;
+    uint64_t c = cin;                          // global count of the input level
+    uint64_t lo = wg * 512;                    // first input node of this workgroup
+    uint64_t m = (c - lo) < 512 ? (c - lo) : 512;
+    uint4* dst = lv_out;                       // start of level d+1
+    for (uint32_t l = 0; l < levels && c > 1; ++l) {
+        const uint64_t cn = (c + 1) / 2, mn = (m + 1) / 2;
+        const bool act = tid < mn;
+        uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+        if (act) {
+            if (l == 0) {
+                const uint64_t a = 2 * (lo + 2 * (uint64_t)tid);  // uint4 index of input node lo + 2*tid
+                l0 = in[a];
+                l1 = in[a + 1];
+                if (2 * (uint64_t)tid + 1 < m) {
+                    r0 = in[a + 2];
+                    r1 = in[a + 3];
+                }
+            } else {
+                l0 = lds[4 * tid];
+                l1 = lds[4 * tid + 1];
+                if (2 * (uint64_t)tid + 1 < m) {
+                    r0 = lds[4 * tid + 2];
+                    r1 = lds[4 * tid + 3];
+                }
+            }
+        }
+        __syncthreads();
+        if (act) {
+            uint4 d0, d1;
+            hash_pair(l0, l1, r0, r1, false, d0, d1);
+            lds[2 * tid] = d0;
+            lds[2 * tid + 1] = d1;
+            const uint64_t g = lo / 2 + tid;  // global index at level d+l+1
+            dst[2 * g] = d0;
+            dst[2 * g + 1] = d1;
+        }
+        __syncthreads();
+        dst += 2 * cn;
+        c = cn;
+        m = mn;
+        lo /= 2;
     }
 }
 

@@ -53,6 +53,9 @@ __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);
 __global__ void k_keccak_fixed(const uint8_t* in, uint64_t n, uint32_t msg_len, uint4* out);
 __global__ void k_keccak_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint4* out);
 __global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
+__global__ void k_keccak_words(const uint2* in, uint64_t n, uint32_t nwords, uint4* out);
+__global__ void k_trie_reduce(const uint4* in, uint64_t cin, uint4* lv_out, uint32_t levels);
+__global__ void k_trie_top2(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels);
 __global__ void k_trie_tail(uint4* node, uint32_t count, uint4* levels);
 __global__ void k_verify_branches(const uint4* leaves, const uint4* branches, const uint64_t* indices,
                                   uint32_t depth, uint32_t tree_depth, const uint4* roots, uint64_t n,

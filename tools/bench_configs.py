@@ -135,10 +135,9 @@ def run_config(args):
         n, dl, depth = 1 << 20, 280, 32
         data = torch.empty(n * dl, dtype=torch.uint8, device=dev)
         D.synth_fill(data, seed + 5)
-        offs = torch.arange(0, (n + 1) * dl, dl, dtype=torch.int64, device=dev)
         lv = torch.empty(L.mk_deposit_trie_levels_bytes(n, depth), dtype=torch.uint8, device=dev)
         root = torch.empty(32, dtype=torch.uint8, device=dev)
-        sec = _timeit(lambda: _lib.check(L.mk_dev_deposit_trie_build(P(data), P(offs), n, depth, P(lv), P(root),
+        sec = _timeit(lambda: _lib.check(L.mk_dev_deposit_trie_build(P(data), None, n, dl, depth, P(lv), P(root),
                                                                      st()), "c5"), args.steps, args.warmup)
         perms = 3 * n + (n - 1) + (depth - 20)
         cpu = None
