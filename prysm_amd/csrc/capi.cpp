@@ -54,6 +54,11 @@ struct DevCtx {
     std::mutex mu;
     hipStream_t stream = nullptr;
     DevBuf in, out, ws, aux, aux2;
+    // side stream + events: the ragged last workgroup of a pass runs
+    // concurrently with the pass's full workgroups (fork/join on events)
+    std::mutex side_mu;
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 
 std::mutex g_mu;
@@ -86,9 +91,12 @@ int bind(int dev) {
         std::lock_guard<std::mutex> lk(g_mu);
         if (!g_ctx[dev]) {
             auto* c = new DevCtx();
-            if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+            if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) {
                 delete c;
-                return fail(MK_EHIP, "hipStreamCreate failed on device %d", dev);
+                return fail(MK_EHIP, "stream/event creation failed on device %d", dev);
             }
             g_ctx[dev] = c;
         }
@@ -294,23 +302,41 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                     hipLaunchKernelGGL((mk::k_wave<false>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
             }
             HIPCHK(hipGetLastError());
-        } else if (ps.nfast) {
-            a.wg_base = 0;
-            if (ps.leaf)
-                hipLaunchKernelGGL((mk::k_reduce<true, true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
-            else
-                hipLaunchKernelGGL((mk::k_reduce<false, true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
-            HIPCHK(hipGetLastError());
-        }
-        if (!ps.wave && ps.nwg > ps.nfast) {
-            a.wg_base = ps.nfast;
-            if (ps.leaf)
-                hipLaunchKernelGGL((mk::k_reduce<true, false>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads), 0,
-                                   st, a);
-            else
-                hipLaunchKernelGGL((mk::k_reduce<false, false>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads), 0,
-                                   st, a);
-            HIPCHK(hipGetLastError());
+        } else {
+            // The ragged workgroup(s) of a pass are latency-bound; when the pass
+            // also has full workgroups they go first, on the side stream, so
+            // they overlap the full ones (fork/join through events on `st`).
+            const bool ragged = ps.nwg > ps.nfast;
+            DevCtx* c = (ragged && ps.nfast) ? g_ctx[t_dev] : nullptr;
+            std::unique_lock<std::mutex> lk;
+            if (ragged) {
+                hipStream_t gs = st;
+                if (c) {
+                    lk = std::unique_lock<std::mutex>(c->side_mu);
+                    HIPCHK(hipEventRecord(c->fork, st));
+                    HIPCHK(hipStreamWaitEvent(c->side, c->fork, 0));
+                    gs = c->side;
+                }
+                ReduceArgs g = a;
+                g.wg_base = ps.nfast;
+                if (ps.leaf)
+                    hipLaunchKernelGGL((mk::k_reduce<true, false>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads), 0,
+                                       gs, g);
+                else
+                    hipLaunchKernelGGL((mk::k_reduce<false, false>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads), 0,
+                                       gs, g);
+                HIPCHK(hipGetLastError());
+                if (c) HIPCHK(hipEventRecord(c->join, c->side));
+            }
+            if (ps.nfast) {
+                a.wg_base = 0;
+                if (ps.leaf)
+                    hipLaunchKernelGGL((mk::k_reduce<true, true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+                else
+                    hipLaunchKernelGGL((mk::k_reduce<false, true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+                HIPCHK(hipGetLastError());
+            }
+            if (c) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
         }
         if (rec_this) {
             HIPCHK(hipEventRecord(rec.b, st));
@@ -394,6 +420,9 @@ int mk_dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_ou
     const uint64_t grid = ceil_div(n, 256);
     if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0)
         hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
+    else if (msg_len % 8 == 0 && msg_len > 0 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0)
+        hipLaunchKernelGGL(mk::k_keccak_words, dim3(grid), dim3(256), 0, st, (const uint2*)d_in, n, msg_len / 8,
+                           (uint4*)d_out);
     else
         hipLaunchKernelGGL(mk::k_keccak_fixed, dim3(grid), dim3(256), 0, st, (const uint8_t*)d_in, n, msg_len,
                            (uint4*)d_out);
@@ -619,11 +648,22 @@ static int make_spec(const mk_field* fields, uint32_t nfields, uint32_t record_l
 static int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp, void* d_msg, void* d_roots,
                                hipStream_t st) {
     if (n == 0) return MK_OK;
-    hipLaunchKernelGGL(mk::k_struct_fields, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_rec, n, sp,
-                       (uint8_t*)d_msg);
+    bool fast = true;  // every bytes field hashes as one dword-granular block
+    for (uint32_t f = 0; f < sp.nfields; ++f)
+        if (sp.kind[f] == MK_FIELD_BYTES && ((sp.len[f] % 4) != 0 || sp.len[f] + 4 >= 136)) fast = false;
+    if (fast)
+        hipLaunchKernelGGL((mk::k_struct_fields<true>), dim3(ceil_div(n * sp.nfields, 256)), dim3(256), 0, st,
+                           (const uint8_t*)d_rec, n, sp, (uint8_t*)d_msg);
+    else
+        hipLaunchKernelGGL((mk::k_struct_fields<false>), dim3(ceil_div(n * sp.nfields, 256)), dim3(256), 0, st,
+                           (const uint8_t*)d_rec, n, sp, (uint8_t*)d_msg);
     HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(mk::k_keccak_fixed, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_msg, n,
-                       sp.msg_len, (uint4*)d_roots);
+    if (sp.msg_len % 8 == 0)
+        hipLaunchKernelGGL(mk::k_keccak_words, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint2*)d_msg, n,
+                           sp.msg_len / 8, (uint4*)d_roots);
+    else
+        hipLaunchKernelGGL(mk::k_keccak_fixed, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_msg, n,
+                           sp.msg_len, (uint4*)d_roots);
     HIPCHK(hipGetLastError());
     return MK_OK;
 }

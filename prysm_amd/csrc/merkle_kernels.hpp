@@ -42,6 +42,7 @@ struct StructSpec {                 // flat fixed-layout record (hash.go:141-159
 
 template <bool LEAF, bool FAST>
 __global__ void k_reduce(ReduceArgs a);
+template <bool FAST>
 __global__ void k_struct_fields(const uint8_t* rec, uint64_t n, StructSpec sp, uint8_t* msg);
 template <bool LEAF>
 __global__ void k_wave(ReduceArgs a);
