@@ -536,10 +536,20 @@ int mk_dev_ssz_merkle_subtree(const void* d_shard_items, uint64_t shard_n, uint3
 
 int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32, void* stream) {
     TRY(bind(-1));
-    if (nroots == 0 || nroots > mk::kReduceSpan2) return fail(MK_EINVAL, "nroots %llu out of range",
-                                                                  (unsigned long long)nroots);
-    hipLaunchKernelGGL(mk::k_finish_roots, dim3(1), dim3(kReduceThreads), 0, (hipStream_t)stream,
-                       (const uint4*)d_roots, nroots, n_total, (uint4*)d_out32);
+    if (nroots == 0 || nroots > 2 * mk::kWave2Span)
+        return fail(MK_EINVAL, "nroots %llu out of range (1..%u)", (unsigned long long)nroots, 2 * mk::kWave2Span);
+    // the reference level loop over the shard roots (odd -> 0^128) plus the
+    // length mix-in is one finalizing node pass of the two-lane latency kernel
+    ReduceArgs a{};
+    a.items = (const uint8_t*)d_roots;
+    a.cin = nroots;
+    a.c1 = nroots > 1 ? (nroots + 1) / 2 : 1;
+    a.c1_full = nroots / 2;
+    a.out = (uint8_t*)d_out32;
+    a.n_items = n_total;
+    a.levels = 64;
+    a.finalize = 1;
+    hipLaunchKernelGGL((mk::k_wave2<false>), dim3(1), dim3(mk::kWaveThreads), 0, (hipStream_t)stream, a);
     HIPCHK(hipGetLastError());
     return MK_OK;
 }
