@@ -24,6 +24,29 @@ using mk::kReduceThreads;
 #define MK_WAVE2 1
 #endif
 constexpr bool kWave2 = MK_WAVE2 != 0;  // two-lanes-per-state latency pass
+#ifndef MK_WAVE3
+#define MK_WAVE3 1
+#endif
+constexpr bool kWave3 = kWave2 && MK_WAVE3 != 0;  // node latency passes bit-interleaved (k_wave3)
+#ifndef MK_NODE_WAVE_MAX_LOG2
+#define MK_NODE_WAVE_MAX_LOG2 17
+#endif
+// node passes switch to the latency form at or below this width: the first
+// level is throughput-bound either way, but the throughput kernel spends ~9
+// serial permutations on its 5 levels where the wave pass spends 6
+constexpr uint64_t kNodeWaveMaxC1 = 1ull << MK_NODE_WAVE_MAX_LOG2;
+#ifndef MK_NODE_WAVE_WGS
+#define MK_NODE_WAVE_WGS 256
+#endif
+constexpr uint64_t kNodeWaveWgs = MK_NODE_WAVE_WGS;
+uint32_t ilog2(uint64_t v) {
+    uint32_t l = 0;
+    while (v > 1) {
+        v >>= 1;
+        ++l;
+    }
+    return l;
+}
 
 thread_local std::string t_err;
 thread_local int t_dev = -1;
@@ -142,6 +165,7 @@ struct Pass {
     bool leaf;
     bool wave;  // latency pass (k_wave) instead of the throughput pass (k_reduce)
     uint64_t nwg, nfast;
+    uint32_t nt;  // threads per workgroup
     ReduceArgs a;
     int in_ws;   // -1 = user input, else ping-pong slot
     int out_ws;  // -1 = user output, else ping-pong slot
@@ -220,10 +244,17 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
             perms += (double)(cin / 2) + (cin % 2 ? 2.0 : 0.0);
         }
         uint64_t c = c1;
-        const bool wave = c1 <= mk::kWaveMaxC1;
-        const uint64_t span = wave ? (kWave2 ? mk::kWave2Span : mk::kWaveThreads) : kReduceSpan1;
+        const bool wave = c1 <= (leaf || !kWave3 ? mk::kWaveMaxC1 : kNodeWaveMaxC1);
+        const bool w3 = kWave3 && wave && !leaf;
+        // k_wave3: the smallest workgroup (64..1024 threads, 2 per pair) that
+        // keeps the pass within ~256 workgroups, one per CU
+        uint32_t nt = w3 ? mk::kWaveThreads : (wave ? mk::kWaveThreads : kReduceThreads);
+        if (w3)
+            while (nt < mk::kMidThreads && ceil_div(c1, nt / 2) > kNodeWaveWgs) nt *= 2;
+        const uint64_t span = w3 ? nt / 2 : wave ? (kWave2 ? mk::kWave2Span : mk::kWaveThreads) : kReduceSpan1;
         const bool final_pass = c1 <= span;
-        const uint32_t max_lv = wave ? (kWave2 ? mk::kWave2Levels : mk::kWaveLevels) : mk::kMaxPassLevels;
+        const uint32_t max_lv = w3 ? 1 + ilog2(nt / 2)
+                              : wave ? (kWave2 ? mk::kWave2Levels : mk::kWaveLevels) : mk::kMaxPassLevels;
         uint32_t lv = final_pass ? remaining : std::min<uint32_t>(max_lv, remaining);
         for (uint32_t l = 1; l < lv; ++l) {  // fused levels above the first
             if (c <= 1 && !pad_at_one) break;
@@ -232,6 +263,9 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         }
         ps.perms = perms;
         ps.wave = wave;
+        ps.nt = nt;
+        a.in_ilv = (w3 && !p.passes.empty() && p.passes.back().wave && !p.passes.back().leaf) ? 1 : 0;
+        a.out_ilv = w3 ? 1 : 0;  // cleared below for the final pass
         a.levels = lv;
         ps.nwg = ceil_div(c1, span);
         ps.nfast = wave ? 0 : std::min<uint64_t>(ps.nwg, a.c1_full / kReduceSpan1);
@@ -244,6 +278,7 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
                 return fail(MK_EINVAL, "planner: unsupported single-level pass");
             }
             ps.out_ws = -1;
+            ps.a.out_ilv = 0;
             p.passes.push_back(ps);
             break;
         }
@@ -290,7 +325,15 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
         }
         if (ps.wave) {
             a.wg_base = 0;
-            if (kWave2) {
+            if (kWave3 && !ps.leaf) {
+                switch (ps.nt) {
+                    case 64: hipLaunchKernelGGL(mk::k_wave3<64>, dim3(ps.nwg), dim3(64), 0, st, a); break;
+                    case 128: hipLaunchKernelGGL(mk::k_wave3<128>, dim3(ps.nwg), dim3(128), 0, st, a); break;
+                    case 256: hipLaunchKernelGGL(mk::k_wave3<256>, dim3(ps.nwg), dim3(256), 0, st, a); break;
+                    case 512: hipLaunchKernelGGL(mk::k_wave3<512>, dim3(ps.nwg), dim3(512), 0, st, a); break;
+                    default: hipLaunchKernelGGL(mk::k_wave3<1024>, dim3(ps.nwg), dim3(1024), 0, st, a); break;
+                }
+            } else if (kWave2) {
                 if (ps.leaf)
                     hipLaunchKernelGGL((mk::k_wave2<true>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
                 else
@@ -540,6 +583,7 @@ int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_to
         return fail(MK_EINVAL, "nroots %llu out of range (1..%u)", (unsigned long long)nroots, 2 * mk::kWave2Span);
     // the reference level loop over the shard roots (odd -> 0^128) plus the
     // length mix-in is one finalizing node pass of the two-lane latency kernel
+    // (plain 32-B roots in, plain digest out)
     ReduceArgs a{};
     a.items = (const uint8_t*)d_roots;
     a.cin = nroots;
@@ -549,7 +593,7 @@ int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_to
     a.n_items = n_total;
     a.levels = 64;
     a.finalize = 1;
-    hipLaunchKernelGGL((mk::k_wave2<false>), dim3(1), dim3(mk::kWaveThreads), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(mk::k_wave3<mk::kWaveThreads>, dim3(1), dim3(mk::kWaveThreads), 0, (hipStream_t)stream, a);
     HIPCHK(hipGetLastError());
     return MK_OK;
 }

@@ -97,6 +97,20 @@ __device__ __forceinline__ void rho_pi_all(const State& a, uint32_t (&blo)[25], 
     (rho_pi_one<Is>(a, blo, bhi), ...);
 }
 
+// MK_SCHED=1 fences the round's phases (sched_barrier) so the half-rate
+// alignbit work (theta D, rho) issues in long runs instead of being
+// interleaved with the full-rate bitop3 work (tools/isa_rates: a wave stream
+// alternating full- and half-rate ops issues at ~4.4 cycles per instruction,
+// segmented streams cost less).
+#ifndef MK_SCHED
+#define MK_SCHED 0
+#endif
+#if MK_SCHED
+#define MK_SB() __builtin_amdgcn_sched_barrier(0)
+#else
+#define MK_SB()
+#endif
+
 __device__ __forceinline__ void round_fn(State& s, uint32_t rclo, uint32_t rchi) {
     uint32_t clo[5], chi_[5];
 #pragma unroll
@@ -104,17 +118,21 @@ __device__ __forceinline__ void round_fn(State& s, uint32_t rclo, uint32_t rchi)
         clo[x] = xor3(xor3(s.lo[x], s.lo[x + 5], s.lo[x + 10]), s.lo[x + 15], s.lo[x + 20]);
         chi_[x] = xor3(xor3(s.hi[x], s.hi[x + 5], s.hi[x + 10]), s.hi[x + 15], s.hi[x + 20]);
     }
+    MK_SB();
     uint32_t rlo[5], rhi[5];  // rotl(C[x], 1)
 #pragma unroll
     for (int x = 0; x < 5; ++x) rotl64<1>(clo[x], chi_[x], rlo[x], rhi[x]);
+    MK_SB();
 #pragma unroll
     for (int i = 0; i < 25; ++i) {
         const int x = i % 5;
         s.lo[i] = xor3(s.lo[i], clo[(x + 4) % 5], rlo[(x + 1) % 5]);
         s.hi[i] = xor3(s.hi[i], chi_[(x + 4) % 5], rhi[(x + 1) % 5]);
     }
+    MK_SB();
     uint32_t blo[25], bhi[25];
     rho_pi_all(s, blo, bhi, std::make_integer_sequence<int, 25>{});
+    MK_SB();
 #pragma unroll
     for (int y = 0; y < 5; ++y) {
 #pragma unroll
@@ -127,6 +145,7 @@ __device__ __forceinline__ void round_fn(State& s, uint32_t rclo, uint32_t rchi)
     }
     s.lo[0] ^= rclo;
     s.hi[0] ^= rchi;
+    MK_SB();
 }
 
 #ifndef MK_ROUND_UNROLL
@@ -260,4 +279,129 @@ __device__ __forceinline__ void zero(Half& s) {
 }
 
 }  // namespace pair
+}  // namespace mk
+
+// ============================================================================
+// Two lanes per state, BIT-INTERLEAVED (latency form, v2).  Lane pair
+// (2k, 2k+1) holds one state; lane p (= lane & 1) holds, for each of the 25
+// Keccak lanes, the 32 bits of parity p: bit j of word v[i] = bit 2j+p of
+// Keccak lane i.  A 64-bit rotation by an even r is then a 32-bit rotation of
+// the lane's OWN word by r/2 (one v_alignbit, no exchange); an odd r swaps the
+// parities: the lane rotates its own word by the amount its partner needs
+// (m + p for r = 2m+1) and takes the partner's result (one DPP move).  Per
+// round and lane: 60 bitop3 + 25 xor + 29 alignbit + 17 DPP (vs 120 bitop3 +
+// 58 alignbit for a whole state in one lane, 119 in the lo/hi pair form).
+namespace mk {
+namespace ilv {
+
+// round constants split into even / odd bits (computed from kRcLo/kRcHi)
+__constant__ uint32_t kRcE[24] = {
+    0x00000001u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000001u, 0x00000001u,
+    0x00000001u, 0x00000001u, 0x00000000u, 0x00000000u, 0x00000001u, 0x00000000u,
+    0x00000001u, 0x00000001u, 0x00000001u, 0x00000001u, 0x00000000u, 0x00000000u,
+    0x00000000u, 0x00000000u, 0x00000001u, 0x00000000u, 0x00000001u, 0x00000000u};
+__constant__ uint32_t kRcO[24] = {
+    0x00000000u, 0x00000089u, 0x8000008bu, 0x80008080u, 0x0000008bu, 0x00008000u,
+    0x80008088u, 0x80000082u, 0x0000000bu, 0x0000000au, 0x00008082u, 0x00008003u,
+    0x0000808bu, 0x8000000bu, 0x8000008au, 0x80000081u, 0x80000081u, 0x80000008u,
+    0x00000083u, 0x80008003u, 0x80008088u, 0x80000088u, 0x00008000u, 0x80008082u};
+
+__device__ __forceinline__ uint32_t partner(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1 /* quad_perm [1,0,3,2] */, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t rot32(uint32_t x, uint32_t sh /* = 32 - amount, mod 32 */) {
+    return __builtin_amdgcn_alignbit(x, x, sh);
+}
+
+struct Half {
+    uint32_t v[25];
+};
+
+// own word of rotl64 by R; p = lane parity (0/1)
+template <int R>
+__device__ __forceinline__ uint32_t rot(uint32_t own, uint32_t p) {
+    if constexpr (R == 0) {
+        return own;
+    } else if constexpr (R % 2 == 0) {
+        return rot32(own, 32 - R / 2);
+    } else {
+        constexpr uint32_t m = (R - 1) / 2;
+        return partner(rot32(own, (32 - m - p) & 31u));  // partner needs own rotated by m + p
+    }
+}
+
+template <int I>
+__device__ __forceinline__ void rho_pi_one(const Half& a, uint32_t (&b)[25], uint32_t p) {
+    constexpr int x = I % 5, y = I / 5;
+    constexpr int dst = y + 5 * ((2 * x + 3 * y) % 5);
+    b[dst] = rot<MK_RHO(I)>(a.v[I], p);
+}
+
+template <int... Is>
+__device__ __forceinline__ void rho_pi_all(const Half& a, uint32_t (&b)[25], uint32_t p,
+                                           std::integer_sequence<int, Is...>) {
+    (rho_pi_one<Is>(a, b, p), ...);
+}
+
+__device__ __forceinline__ void round_fn(Half& s, uint32_t rc_own, uint32_t p) {
+    uint32_t c[5], d[5];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) c[x] = xor3(xor3(s.v[x], s.v[x + 5], s.v[x + 10]), s.v[x + 15], s.v[x + 20]);
+#pragma unroll
+    for (int x = 0; x < 5; ++x) d[x] = c[(x + 4) % 5] ^ rot<1>(c[(x + 1) % 5], p);
+#pragma unroll
+    for (int i = 0; i < 25; ++i) s.v[i] ^= d[i % 5];
+    uint32_t b[25];
+    rho_pi_all(s, b, p, std::make_integer_sequence<int, 25>{});
+#pragma unroll
+    for (int y = 0; y < 5; ++y)
+#pragma unroll
+        for (int x = 0; x < 5; ++x)
+            s.v[x + 5 * y] = chi3(b[x + 5 * y], b[(x + 1) % 5 + 5 * y], b[(x + 2) % 5 + 5 * y]);
+    s.v[0] ^= rc_own;
+}
+
+__device__ __forceinline__ void keccak_f(Half& s, uint32_t p) {
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < 24; ++r) round_fn(s, p ? kRcO[r] : kRcE[r], p);
+}
+
+__device__ __forceinline__ void zero(Half& s) {
+#pragma unroll
+    for (int i = 0; i < 25; ++i) s.v[i] = 0u;
+}
+
+// ---- conversion between (lo, hi) 32-bit halves and the parity-p word -------
+// even bits of x gathered into the low 16 bits
+__device__ __forceinline__ uint32_t pack_even16(uint32_t x) {
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    x = (x | (x >> 8)) & 0x0000FFFFu;
+    return x;
+}
+// low 16 bits of x spread to the even bit positions
+__device__ __forceinline__ uint32_t spread16(uint32_t x) {
+    x &= 0x0000FFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+// parity-p word of the 64-bit lane (hi:lo)
+__device__ __forceinline__ uint32_t to_ilv(uint32_t lo, uint32_t hi, uint32_t p) {
+    return pack_even16(lo >> p) | (pack_even16(hi >> p) << 16);
+}
+// this lane's half (p = 0: lo, p = 1: hi) of the 64-bit lane whose parity
+// words are `own` (this lane's) and the partner lane's
+__device__ __forceinline__ uint32_t from_ilv(uint32_t own, uint32_t p) {
+    const uint32_t par = partner(own);
+    const uint32_t e = p ? par : own, o = p ? own : par;
+    const uint32_t sh = p ? 16u : 0u;
+    return spread16(e >> sh) | (spread16(o >> sh) << 1);
+}
+
+}  // namespace ilv
 }  // namespace mk

@@ -604,6 +604,163 @@ __global__ __launch_bounds__(kWaveThreads) void k_wave2(ReduceArgs a) {
 template __global__ void k_wave2<true>(ReduceArgs);
 template __global__ void k_wave2<false>(ReduceArgs);
 
+// ----------------------------------------------------------------------------
+// Node pass of the latency form with BIT-INTERLEAVED lane pairs
+// (keccak_dev.hpp, mk::ilv): lane p of pair k owns the parity-p words of node
+// k.  Nodes in LDS and, between consecutive wave3 passes, in HBM stay in
+// that form ("ilv nodes": dword 2w + p = parity-p word of digest lane w);
+// a.in_ilv / a.out_ilv select conversion from / to plain 32-B digests at the
+// pass boundary, so a chain of passes converts once at each end.
+// NT = 64..1024 threads own NT/2 lane pairs and reduce them through
+// log2(NT/2) more levels in LDS.  The host picks NT so the first level's
+// workgroups spread over all 256 CUs (NT = 1024 for 2^17 pairs): the first,
+// throughput-bound level fills the chip, and each later level halves the
+// number of waves that still issue (waves with no active lane skip the
+// permutation and wait at the barrier), so one launch covers up to 10 levels
+// at close to one permutation latency each.
+namespace {
+
+__device__ __forceinline__ void hash_pair3(const uint32_t (&l)[4], const uint32_t (&r)[4], bool padded, uint32_t p,
+                                           uint32_t (&d)[4]) {
+    ilv::Half s;
+    ilv::zero(s);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) s.v[w] = l[w];
+    if (!padded) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) s.v[4 + w] = r[w];
+    }
+    const int nperm = padded ? 2 : 1;
+#pragma unroll 1
+    for (int k = 0; k < nperm; ++k) {
+        if (k == nperm - 1) {  // bit 0 of a lane is even (p = 0), bit 63 odd (p = 1)
+            if (p == 0)
+                s.v[padded ? 3 : 8] ^= 1u;
+            else
+                s.v[16] ^= 0x80000000u;
+        }
+        ilv::keccak_f(s, p);
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) d[w] = s.v[w];
+}
+
+// node j of a plain or ilv node array -> this lane's parity words
+__device__ __forceinline__ void load_node3(const uint32_t* __restrict__ in, uint64_t j, bool is_ilv, uint32_t p,
+                                           uint32_t (&w4)[4]) {
+    if (is_ilv) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) w4[w] = in[8 * j + 2 * w + p];
+    } else {
+        const uint4 a = reinterpret_cast<const uint4*>(in)[2 * j];
+        const uint4 b = reinterpret_cast<const uint4*>(in)[2 * j + 1];
+        w4[0] = ilv::to_ilv(a.x, a.y, p);
+        w4[1] = ilv::to_ilv(a.z, a.w, p);
+        w4[2] = ilv::to_ilv(b.x, b.y, p);
+        w4[3] = ilv::to_ilv(b.z, b.w, p);
+    }
+}
+
+// this lane's dwords (2w + p) of a node, plain or ilv
+__device__ __forceinline__ void store_node3(uint32_t* __restrict__ out, uint64_t j, bool is_ilv, uint32_t p,
+                                            const uint32_t (&w4)[4]) {
+#pragma unroll
+    for (int w = 0; w < 4; ++w) out[8 * j + 2 * w + p] = is_ilv ? w4[w] : ilv::from_ilv(w4[w], p);
+}
+
+}  // namespace
+
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void k_wave3(ReduceArgs a) {
+    constexpr uint32_t kSpan = NT / 2;  // first-level nodes (lane pairs) per workgroup
+    __shared__ uint32_t lds[8 * kSpan];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t k = tid >> 1;
+    const uint32_t p = tid & 1u;
+    const uint64_t wg = a.wg_base + blockIdx.x;
+    const uint64_t lo1 = wg * kSpan;
+    const uint64_t c1 = a.c1;
+    const uint64_t m1 = (c1 - lo1) < kSpan ? (c1 - lo1) : kSpan;
+    const uint32_t* in = reinterpret_cast<const uint32_t*>(a.items);
+    if (k < m1) {
+        const uint64_t j = lo1 + k;
+        uint32_t l[4], r[4] = {0, 0, 0, 0}, d[4];
+        load_node3(in, 2 * j, a.in_ilv, p, l);
+        if (a.cin == 1 && !a.pad_at_one) {  // single node: it is the root
+#pragma unroll
+            for (int w = 0; w < 4; ++w) d[w] = l[w];
+        } else {
+            const bool padded = !(2 * j + 1 < a.cin);
+            if (!padded) load_node3(in, 2 * j + 1, a.in_ilv, p, r);
+            hash_pair3(l, r, padded, p, d);
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) lds[8 * k + 2 * w + p] = d[w];
+    }
+    __syncthreads();
+    uint64_t c = c1, m = m1;
+    int left = a.finalize ? 64 : (int)a.levels - 1;
+    int done = 0;
+    while (left > 0 && (c > 1 || a.pad_at_one)) {
+        const uint64_t mn = (m + 1) / 2;
+        const bool act = k < mn;
+        uint32_t l[4], r[4] = {0, 0, 0, 0};
+        bool padded = false;
+        if (act) {
+            padded = !(2 * (uint64_t)k + 1 < m);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) l[w] = lds[16 * k + 2 * w + p];
+            if (!padded) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) r[w] = lds[16 * k + 8 + 2 * w + p];
+            }
+        }
+        __syncthreads();
+        if (act) {
+            uint32_t d[4];
+            hash_pair3(l, r, padded, p, d);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) lds[8 * k + 2 * w + p] = d[w];
+        }
+        __syncthreads();
+        c = (c + 1) / 2;
+        m = mn;
+        --left;
+        ++done;
+    }
+    uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
+    if (a.finalize) {
+        if (k == 0) {  // K(root || le64(n) || 0^24) on lanes 0/1
+            ilv::Half s;
+            ilv::zero(s);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) s.v[w] = lds[2 * w + p];
+            s.v[4] = ilv::to_ilv((uint32_t)a.n_items, (uint32_t)(a.n_items >> 32), p);
+            if (p == 0)
+                s.v[8] ^= 1u;
+            else
+                s.v[16] ^= 0x80000000u;
+            ilv::keccak_f(s, p);
+            uint32_t d[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) d[w] = s.v[w];
+            store_node3(out, 0, false, p, d);
+        }
+    } else if (k < m) {
+        const uint64_t lo_out = lo1 >> done;
+        uint32_t d[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) d[w] = lds[8 * k + 2 * w + p];
+        store_node3(out, lo_out + k, a.out_ilv, p, d);
+    }
+}
+
+template __global__ void k_wave3<64>(ReduceArgs);
+template __global__ void k_wave3<128>(ReduceArgs);
+template __global__ void k_wave3<256>(ReduceArgs);
+template __global__ void k_wave3<512>(ReduceArgs);
+template __global__ void k_wave3<1024>(ReduceArgs);
+
 // Narrow top of the deposit trie, two lanes per state: the workgroup owns 64
 // input nodes of level d and writes up to `levels` levels to the level array;
 // once the count is 1 it continues with node = K(node || 0^32) (the levels

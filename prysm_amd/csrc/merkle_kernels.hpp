@@ -14,6 +14,7 @@ constexpr uint32_t kWaveLevels = 7;                  // first level + 6 in-wave 
 constexpr uint64_t kWaveMaxC1 = 1ull << 16;          // use the latency pass at or below this width (A/B: 2^19 is slower)
 constexpr uint32_t kWave2Span = kWaveThreads / 2;    // two lanes per state: 32 nodes per wave
 constexpr uint32_t kWave2Levels = 6;                 // first level + 5 in-wave levels (32 -> 1)
+constexpr uint32_t kMidThreads = 1024;               // largest k_wave3: 16 waves, 512 lane pairs, 10 levels
 
 struct ReduceArgs {
     const uint8_t* items;  // LEAF: item bytes; NODE: 32-B input nodes
@@ -29,6 +30,8 @@ struct ReduceArgs {
     uint32_t finalize;     // reduce to the root and mix in the length
     uint32_t pad_at_one;   // subtree mode: keep hashing (x || 0^128) at count 1
     uint64_t wg_base;      // workgroup index offset of this launch
+    uint32_t in_ilv;       // k_wave3: input nodes are bit-interleaved lane pairs
+    uint32_t out_ilv;      // k_wave3: write bit-interleaved output nodes
 };
 
 constexpr uint32_t kMaxStructFields = 32;
@@ -48,6 +51,8 @@ template <bool LEAF>
 __global__ void k_wave(ReduceArgs a);
 template <bool LEAF>
 __global__ void k_wave2(ReduceArgs a);
+template <uint32_t NT>
+__global__ void k_wave3(ReduceArgs a);
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
 __global__ void k_finish_roots(const uint4* roots, uint64_t nroots, uint64_t n_items, uint4* out);
 __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);

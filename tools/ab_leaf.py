@@ -48,7 +48,7 @@ def main():
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     first = libs[a.variants[0]]
     assert first.mk_dev_synth_fill(ctypes.c_void_p(items.data_ptr()), n * il, 0x5EED000000000004, 0, st) == 0
-    ws = torch.empty(first.mk_ssz_merkle_workspace_bytes(n, il) + 4096, dtype=torch.uint8, device=dev)
+    ws = torch.empty(max(L.mk_ssz_merkle_workspace_bytes(n, il) for L in libs.values()) + 4096, dtype=torch.uint8, device=dev)
     outs = {v: torch.empty(32, dtype=torch.uint8, device=dev) for v in a.variants}
     times = {v: [] for v in a.variants}
     leaf = {v: [] for v in a.variants}
