@@ -108,6 +108,9 @@ def main():
     ws = D.subtree_workspace(local_n, item_len, dev) if sp.nonempty > 1 else D.merkle_workspace(n, item_len, dev)
     root_buf = torch.empty(32, dtype=torch.uint8, device=dev)
     gather_buf = torch.empty(world * 32, dtype=torch.uint8, device=dev)
+    finish_out = torch.empty(32, dtype=torch.uint8, device=dev)
+    # rank 0 finishes the top levels on a side stream, overlapping its next step
+    finish_stream = torch.cuda.Stream(device=dev) if world > 1 and rank == 0 else None
     torch.cuda.synchronize()
     log(f"rank {rank}/{world}: {local_n} items ({nbytes / 2**30:.2f} GiB), shard height {sp.height}, "
         f"nonempty {sp.nonempty}")
@@ -117,8 +120,8 @@ def main():
             items, n, item_len, sp, rank, world,
             subtree_fn=lambda it, sn, il, h, pad: D.merkle_subtree(it, sn, il, h, pad, out=root_buf, ws=ws),
             full_fn=lambda it, nn, il: D.merkle_hash(it, nn, il, out=root_buf, ws=ws),
-            finish_fn=lambda g, nr, nt: D.merkle_finish(g, nr, nt),
-            gather_buf=gather_buf)
+            finish_fn=lambda g, nr, nt: D.merkle_finish(g, nr, nt, out=finish_out),
+            gather_buf=gather_buf, finish_stream=finish_stream)
 
     for i in range(args.warmup):
         step()

@@ -17,7 +17,6 @@
 namespace {
 
 using mk::ReduceArgs;
-using mk::kReduceSpan1;
 using mk::kReduceThreads;
 
 #ifndef MK_WAVE2
@@ -39,6 +38,22 @@ constexpr uint64_t kNodeWaveMaxC1 = 1ull << MK_NODE_WAVE_MAX_LOG2;
 #define MK_NODE_WAVE_WGS 256
 #endif
 constexpr uint64_t kNodeWaveWgs = MK_NODE_WAVE_WGS;
+#ifndef MK_LEAF_WAVE3
+#define MK_LEAF_WAVE3 1
+#endif
+constexpr bool kLeafWave3 = MK_LEAF_WAVE3 != 0;  // narrow leaf passes bit-interleaved too
+#ifndef MK_LEAF_WAVE_MAX_LOG2
+#define MK_LEAF_WAVE_MAX_LOG2 17
+#endif
+constexpr uint64_t kLeafWaveMaxC1 = 1ull << MK_LEAF_WAVE_MAX_LOG2;  // leaf passes at or below: latency form
+#ifndef MK_REDUCE_NI2_MIN_LOG2
+#define MK_REDUCE_NI2_MIN_LOG2 18
+#endif
+constexpr uint64_t kReduceNi2MinC1 = 1ull << MK_REDUCE_NI2_MIN_LOG2;  // leaf passes narrower than this use NI = 1
+#ifndef MK_STRUCT_FUSED
+#define MK_STRUCT_FUSED 1
+#endif
+constexpr bool kStructFused = MK_STRUCT_FUSED != 0;  // k_struct_fused instead of fields + message kernels
 uint32_t ilog2(uint64_t v) {
     uint32_t l = 0;
     while (v > 1) {
@@ -165,7 +180,9 @@ struct Pass {
     bool leaf;
     bool wave;  // latency pass (k_wave) instead of the throughput pass (k_reduce)
     uint64_t nwg, nfast;
+    bool w3;      // k_wave3 (bit-interleaved latency form)
     uint32_t nt;  // threads per workgroup
+    uint32_t ni;  // k_reduce: window pairs per thread (span 512 * ni)
     ReduceArgs a;
     int in_ws;   // -1 = user input, else ping-pong slot
     int out_ws;  // -1 = user output, else ping-pong slot
@@ -244,14 +261,18 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
             perms += (double)(cin / 2) + (cin % 2 ? 2.0 : 0.0);
         }
         uint64_t c = c1;
-        const bool wave = c1 <= (leaf || !kWave3 ? mk::kWaveMaxC1 : kNodeWaveMaxC1);
-        const bool w3 = kWave3 && wave && !leaf;
+        const bool wave = c1 <= (leaf || !kWave3 ? kLeafWaveMaxC1 : kNodeWaveMaxC1);
+        const bool w3 = kWave3 && wave && (!leaf || kLeafWave3);
         // k_wave3: the smallest workgroup (64..1024 threads, 2 per pair) that
         // keeps the pass within ~256 workgroups, one per CU
         uint32_t nt = w3 ? mk::kWaveThreads : (wave ? mk::kWaveThreads : kReduceThreads);
         if (w3)
             while (nt < mk::kMidThreads && ceil_div(c1, nt / 2) > kNodeWaveWgs) nt *= 2;
-        const uint64_t span = w3 ? nt / 2 : wave ? (kWave2 ? mk::kWave2Span : mk::kWaveThreads) : kReduceSpan1;
+        // throughput pass: 2 window pairs per thread on wide passes, 1 on mid-size
+        // leaf passes so they still spread over the CUs
+        const uint32_t ni = (!wave && leaf && c1 < kReduceNi2MinC1) ? 1 : 2;
+        const uint64_t span = w3 ? nt / 2 : wave ? (kWave2 ? mk::kWave2Span : mk::kWaveThreads)
+                                                 : (uint64_t)2 * ni * kReduceThreads;
         const bool final_pass = c1 <= span;
         const uint32_t max_lv = w3 ? 1 + ilog2(nt / 2)
                               : wave ? (kWave2 ? mk::kWave2Levels : mk::kWaveLevels) : mk::kMaxPassLevels;
@@ -264,17 +285,19 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         ps.perms = perms;
         ps.wave = wave;
         ps.nt = nt;
-        a.in_ilv = (w3 && !p.passes.empty() && p.passes.back().wave && !p.passes.back().leaf) ? 1 : 0;
+        a.in_ilv = (w3 && !leaf && !p.passes.empty() && p.passes.back().w3) ? 1 : 0;
+        ps.w3 = w3;
         a.out_ilv = w3 ? 1 : 0;  // cleared below for the final pass
         a.levels = lv;
         ps.nwg = ceil_div(c1, span);
-        ps.nfast = wave ? 0 : std::min<uint64_t>(ps.nwg, a.c1_full / kReduceSpan1);
+        ps.nfast = wave ? 0 : std::min<uint64_t>(ps.nwg, a.c1_full / span);
+        ps.ni = ni;
         ps.in_ws = in_slot;
         if (final_pass) {
             if (!subtree) {
                 a.finalize = 1;
                 a.levels = 64;
-            } else if (!wave && c1 > kReduceSpan1 / 2 && lv < 2) {
+            } else if (!wave && c1 > span / 2 && lv < 2) {
                 return fail(MK_EINVAL, "planner: unsupported single-level pass");
             }
             ps.out_ws = -1;
@@ -293,6 +316,17 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         if (remaining == 0) return fail(MK_EINVAL, "planner: ran out of levels");
     }
     return MK_OK;
+}
+
+template <bool LEAF>
+void launch_wave3(uint32_t nt, uint64_t nwg, const ReduceArgs& a, hipStream_t st) {
+    switch (nt) {
+        case 64: hipLaunchKernelGGL((mk::k_wave3<64, LEAF>), dim3(nwg), dim3(64), 0, st, a); break;
+        case 128: hipLaunchKernelGGL((mk::k_wave3<128, LEAF>), dim3(nwg), dim3(128), 0, st, a); break;
+        case 256: hipLaunchKernelGGL((mk::k_wave3<256, LEAF>), dim3(nwg), dim3(256), 0, st, a); break;
+        case 512: hipLaunchKernelGGL((mk::k_wave3<512, LEAF>), dim3(nwg), dim3(512), 0, st, a); break;
+        default: hipLaunchKernelGGL((mk::k_wave3<1024, LEAF>), dim3(nwg), dim3(1024), 0, st, a); break;
+    }
 }
 
 uint64_t plan_ws_bytes(const Plan& p) { return 32 * (p.slot_nodes[0] + p.slot_nodes[1]) + 256; }
@@ -325,14 +359,11 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
         }
         if (ps.wave) {
             a.wg_base = 0;
-            if (kWave3 && !ps.leaf) {
-                switch (ps.nt) {
-                    case 64: hipLaunchKernelGGL(mk::k_wave3<64>, dim3(ps.nwg), dim3(64), 0, st, a); break;
-                    case 128: hipLaunchKernelGGL(mk::k_wave3<128>, dim3(ps.nwg), dim3(128), 0, st, a); break;
-                    case 256: hipLaunchKernelGGL(mk::k_wave3<256>, dim3(ps.nwg), dim3(256), 0, st, a); break;
-                    case 512: hipLaunchKernelGGL(mk::k_wave3<512>, dim3(ps.nwg), dim3(512), 0, st, a); break;
-                    default: hipLaunchKernelGGL(mk::k_wave3<1024>, dim3(ps.nwg), dim3(1024), 0, st, a); break;
-                }
+            if (ps.w3) {
+                if (ps.leaf)
+                    launch_wave3<true>(ps.nt, ps.nwg, a, st);
+                else
+                    launch_wave3<false>(ps.nt, ps.nwg, a, st);
             } else if (kWave2) {
                 if (ps.leaf)
                     hipLaunchKernelGGL((mk::k_wave2<true>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
@@ -362,21 +393,26 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                 }
                 ReduceArgs g = a;
                 g.wg_base = ps.nfast;
-                if (ps.leaf)
-                    hipLaunchKernelGGL((mk::k_reduce<true, false>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads), 0,
-                                       gs, g);
+                if (ps.leaf && ps.ni == 1)
+                    hipLaunchKernelGGL((mk::k_reduce<true, false, 1>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads),
+                                       0, gs, g);
+                else if (ps.leaf)
+                    hipLaunchKernelGGL((mk::k_reduce<true, false, 2>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads),
+                                       0, gs, g);
                 else
-                    hipLaunchKernelGGL((mk::k_reduce<false, false>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads), 0,
-                                       gs, g);
+                    hipLaunchKernelGGL((mk::k_reduce<false, false, 2>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads),
+                                       0, gs, g);
                 HIPCHK(hipGetLastError());
                 if (c) HIPCHK(hipEventRecord(c->join, c->side));
             }
             if (ps.nfast) {
                 a.wg_base = 0;
-                if (ps.leaf)
-                    hipLaunchKernelGGL((mk::k_reduce<true, true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+                if (ps.leaf && ps.ni == 1)
+                    hipLaunchKernelGGL((mk::k_reduce<true, true, 1>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+                else if (ps.leaf)
+                    hipLaunchKernelGGL((mk::k_reduce<true, true, 2>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
                 else
-                    hipLaunchKernelGGL((mk::k_reduce<false, true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+                    hipLaunchKernelGGL((mk::k_reduce<false, true, 2>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
                 HIPCHK(hipGetLastError());
             }
             if (c) HIPCHK(hipStreamWaitEvent(st, c->join, 0));
@@ -593,7 +629,7 @@ int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_to
     a.n_items = n_total;
     a.levels = 64;
     a.finalize = 1;
-    hipLaunchKernelGGL(mk::k_wave3<mk::kWaveThreads>, dim3(1), dim3(mk::kWaveThreads), 0, (hipStream_t)stream, a);
+    launch_wave3<false>(mk::kWaveThreads, 1, a, (hipStream_t)stream);
     HIPCHK(hipGetLastError());
     return MK_OK;
 }
@@ -702,6 +738,26 @@ static int make_spec(const mk_field* fields, uint32_t nfields, uint32_t record_l
 static int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp, void* d_msg, void* d_roots,
                                hipStream_t st) {
     if (n == 0) return MK_OK;
+    // fused path: dword-granular single-block fields, dword-aligned message
+    bool fused = kStructFused && sp.msg_len % 4 == 0 && sp.msg_len <= mk::kStructFusedMaxMsg &&
+                 ((uintptr_t)d_rec % 4) == 0;
+    bool vec16 = ((uintptr_t)d_rec % 16) == 0 && sp.rec_len % 16 == 0;
+    for (uint32_t f = 0; f < sp.nfields; ++f) {
+        if (sp.out_off[f] % 4) fused = false;
+        if (sp.kind[f] == MK_FIELD_BYTES) {
+            if ((sp.len[f] % 4) != 0 || sp.len[f] > mk::kStructFusedMaxField) fused = false;
+            if (sp.off[f] % 16 || sp.off[f] + ((sp.len[f] + 15) & ~15u) > sp.rec_len) vec16 = false;
+        } else if (sp.len[f] % 4 || sp.off[f] % 4) {
+            fused = false;
+        }
+    }
+    if (fused) {
+        hipLaunchKernelGGL(mk::k_struct_fused, dim3(ceil_div(n, mk::kStructThreads)), dim3(mk::kStructThreads),
+                           mk::kStructThreads * sp.msg_len, st, (const uint8_t*)d_rec, n, sp, vec16 ? 1u : 0u,
+                           (uint4*)d_roots);
+        HIPCHK(hipGetLastError());
+        return MK_OK;
+    }
     bool fast = true;  // every bytes field hashes as one dword-granular block
     for (uint32_t f = 0; f < sp.nfields; ++f)
         if (sp.kind[f] == MK_FIELD_BYTES && ((sp.len[f] % 4) != 0 || sp.len[f] + 4 >= 136)) fast = false;

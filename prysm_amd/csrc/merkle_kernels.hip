@@ -210,6 +210,10 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
 template <bool LEAF>
 __device__ __forceinline__ void first_level_generic(const ReduceArgs& a, uint64_t j, uint4& d0, uint4& d1) {
     if constexpr (LEAF) {
+        if (j < a.c1_full) {  // full 256-B window (item_len | 128, 16-B aligned)
+            hash_window256(reinterpret_cast<const uint4*>(a.items) + j * 16, d0, d1);
+            return;
+        }
         const uint64_t lo = j * 2 * a.cb;
         uint64_t la;
         uint32_t lz;
@@ -240,19 +244,22 @@ __device__ __forceinline__ void first_level_generic(const ReduceArgs& a, uint64_
 }
 
 // One fused reduce pass.  256 threads; the workgroup owns first-level nodes
-// [1024*wg, 1024*wg+1024), folds them pairwise in registers into 512
-// level-2 nodes in LDS, then reduces further levels in LDS (one node per
+// [S*wg, S*wg+S) with S = 512*NI (NI = 2 for wide passes; NI = 1 halves the
+// serial work per thread so mid-size trees still spread over all CUs),
+// folds them pairwise in registers into S/2 level-2 nodes in LDS, then reduces further levels in LDS (one node per
 // thread per level, read -> barrier -> permute -> write -> barrier).
 // Non-final passes write 512 >> (levels-2) nodes per workgroup; the final
 // pass (one workgroup) reduces to the root and applies the length mix-in.
-template <bool LEAF, bool FAST>
+template <bool LEAF, bool FAST, int NI>
 __global__ __launch_bounds__(kReduceThreads, MK_MIN_WAVES) void k_reduce(ReduceArgs a) {
-    __shared__ uint4 lds[2 * kReduceSpan2];
+    constexpr uint64_t kSpan1 = 2 * NI * kReduceThreads;  // first-level nodes per workgroup
+    constexpr uint64_t kSpan2 = kSpan1 / 2;
+    __shared__ uint4 lds[2 * kSpan2];
     const uint32_t tid = threadIdx.x;
     const uint64_t wg = a.wg_base + blockIdx.x;
-    const uint64_t lo1 = wg * kReduceSpan1;
+    const uint64_t lo1 = wg * kSpan1;
     const uint64_t c1 = a.c1;
-    const uint64_t m1 = (c1 - lo1) < kReduceSpan1 ? (c1 - lo1) : kReduceSpan1;
+    const uint64_t m1 = (c1 - lo1) < kSpan1 ? (c1 - lo1) : kSpan1;
     const bool pair = a.levels >= 2 && (c1 > 1 || a.pad_at_one);
     const uint64_t c2 = pair ? (c1 + 1) / 2 : c1;
     const uint64_t m2 = pair ? (m1 + 1) / 2 : m1;
@@ -262,7 +269,7 @@ __global__ __launch_bounds__(kReduceThreads, MK_MIN_WAVES) void k_reduce(ReduceA
         // Full workgroup of full windows / complete node pairs (host-checked):
         // no bounds checks, no odd padding, one keccak_f copy per call site.
 #pragma unroll 1
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NI; ++i) {
             const uint32_t q = i * kReduceThreads + tid;
             const uint64_t j0 = lo1 + 2 * (uint64_t)q;
             uint4 l0, l1, r0, r1, d0, d1;
@@ -281,7 +288,7 @@ __global__ __launch_bounds__(kReduceThreads, MK_MIN_WAVES) void k_reduce(ReduceA
         }
     } else if (pair) {
 #pragma unroll 1
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NI; ++i) {
             const uint32_t q = i * kReduceThreads + tid;
             if (q < m2) {
                 const uint64_t j0 = lo1 + 2 * (uint64_t)q;
@@ -296,9 +303,9 @@ __global__ __launch_bounds__(kReduceThreads, MK_MIN_WAVES) void k_reduce(ReduceA
         }
     } else {
         // no pair level (levels == 1, or a single first-level node); the host
-        // guarantees m1 <= kReduceSpan2 here.
+        // guarantees m1 <= kSpan2 here.
 #pragma unroll 1
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < NI; ++i) {
             const uint32_t q = i * kReduceThreads + tid;
             if (q < m1) {
                 uint4 d0, d1;
@@ -352,7 +359,7 @@ __global__ __launch_bounds__(kReduceThreads, MK_MIN_WAVES) void k_reduce(ReduceA
             out[1] = d1;
         }
     } else {
-        const uint64_t lo_out = ((pair ? wg * kReduceSpan2 : wg * kReduceSpan1)) >> done;
+        const uint64_t lo_out = ((pair ? wg * kSpan2 : wg * kSpan1)) >> done;
         for (uint32_t k = tid; k < m; k += kReduceThreads) {
             out[2 * (lo_out + k)] = lds[2 * k];
             out[2 * (lo_out + k) + 1] = lds[2 * k + 1];
@@ -360,10 +367,12 @@ __global__ __launch_bounds__(kReduceThreads, MK_MIN_WAVES) void k_reduce(ReduceA
     }
 }
 
-template __global__ void k_reduce<true, true>(ReduceArgs);
-template __global__ void k_reduce<true, false>(ReduceArgs);
-template __global__ void k_reduce<false, true>(ReduceArgs);
-template __global__ void k_reduce<false, false>(ReduceArgs);
+template __global__ void k_reduce<true, true, 2>(ReduceArgs);
+template __global__ void k_reduce<true, false, 2>(ReduceArgs);
+template __global__ void k_reduce<false, true, 2>(ReduceArgs);
+template __global__ void k_reduce<false, false, 2>(ReduceArgs);
+template __global__ void k_reduce<true, true, 1>(ReduceArgs);
+template __global__ void k_reduce<true, false, 1>(ReduceArgs);
 
 // ----------------------------------------------------------------------------
 // Latency-oriented pass for the narrow top of the tree: one wave per
@@ -645,6 +654,39 @@ __device__ __forceinline__ void hash_pair3(const uint32_t (&l)[4], const uint32_
     for (int w = 0; w < 4; ++w) d[w] = s.v[w];
 }
 
+// full 256-B window (two blocks) on this lane's parity words; each 64-bit
+// message lane is split into its even / odd bits on the way in
+__device__ __forceinline__ void hash_window3(const uint4* __restrict__ w, uint32_t p, uint32_t (&d)[4]) {
+    uint4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = ld_nt(w + k);
+    uint32_t m[32];  // message lanes 0..31 as parity-p words
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        m[2 * k] = ilv::to_ilv(v[k].x, v[k].y, p);
+        m[2 * k + 1] = ilv::to_ilv(v[k].z, v[k].w, p);
+    }
+    ilv::Half s;
+    ilv::zero(s);
+#pragma unroll 1
+    for (int b = 0; b < 2; ++b) {
+        if (b == 0) {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) s.v[i] ^= m[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 15; ++i) s.v[i] ^= m[17 + i];
+            if (p == 0)
+                s.v[15] ^= 1u;  // byte 256 = byte 120 of block 1: bit 0 of lane 15
+            else
+                s.v[16] ^= 0x80000000u;
+        }
+        ilv::keccak_f(s, p);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = s.v[k];
+}
+
 // node j of a plain or ilv node array -> this lane's parity words
 __device__ __forceinline__ void load_node3(const uint32_t* __restrict__ in, uint64_t j, bool is_ilv, uint32_t p,
                                            uint32_t (&w4)[4]) {
@@ -670,7 +712,7 @@ __device__ __forceinline__ void store_node3(uint32_t* __restrict__ out, uint64_t
 
 }  // namespace
 
-template <uint32_t NT>
+template <uint32_t NT, bool LEAF>
 __global__ __launch_bounds__(NT) void k_wave3(ReduceArgs a) {
     constexpr uint32_t kSpan = NT / 2;  // first-level nodes (lane pairs) per workgroup
     __shared__ uint32_t lds[8 * kSpan];
@@ -682,7 +724,22 @@ __global__ __launch_bounds__(NT) void k_wave3(ReduceArgs a) {
     const uint64_t c1 = a.c1;
     const uint64_t m1 = (c1 - lo1) < kSpan ? (c1 - lo1) : kSpan;
     const uint32_t* in = reinterpret_cast<const uint32_t*>(a.items);
-    if (k < m1) {
+    if (LEAF && k < m1) {  // window j of the item bytes
+        const uint64_t j = lo1 + k;
+        uint32_t d[4];
+        if (j < a.c1_full) {
+            hash_window3(reinterpret_cast<const uint4*>(a.items) + j * 16, p, d);
+        } else {  // ragged window: both lanes run the full-state sponge
+            uint4 d0, d1;
+            first_level_generic<true>(a, j, d0, d1);
+            d[0] = ilv::to_ilv(d0.x, d0.y, p);
+            d[1] = ilv::to_ilv(d0.z, d0.w, p);
+            d[2] = ilv::to_ilv(d1.x, d1.y, p);
+            d[3] = ilv::to_ilv(d1.z, d1.w, p);
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) lds[8 * k + 2 * w + p] = d[w];
+    } else if (!LEAF && k < m1) {
         const uint64_t j = lo1 + k;
         uint32_t l[4], r[4] = {0, 0, 0, 0}, d[4];
         load_node3(in, 2 * j, a.in_ilv, p, l);
@@ -755,11 +812,16 @@ __global__ __launch_bounds__(NT) void k_wave3(ReduceArgs a) {
     }
 }
 
-template __global__ void k_wave3<64>(ReduceArgs);
-template __global__ void k_wave3<128>(ReduceArgs);
-template __global__ void k_wave3<256>(ReduceArgs);
-template __global__ void k_wave3<512>(ReduceArgs);
-template __global__ void k_wave3<1024>(ReduceArgs);
+template __global__ void k_wave3<64, false>(ReduceArgs);
+template __global__ void k_wave3<128, false>(ReduceArgs);
+template __global__ void k_wave3<256, false>(ReduceArgs);
+template __global__ void k_wave3<512, false>(ReduceArgs);
+template __global__ void k_wave3<1024, false>(ReduceArgs);
+template __global__ void k_wave3<64, true>(ReduceArgs);
+template __global__ void k_wave3<128, true>(ReduceArgs);
+template __global__ void k_wave3<256, true>(ReduceArgs);
+template __global__ void k_wave3<512, true>(ReduceArgs);
+template __global__ void k_wave3<1024, true>(ReduceArgs);
 
 // Narrow top of the deposit trie, two lanes per state: the workgroup owns 64
 // input nodes of level d and writes up to `levels` levels to the level array;
@@ -1004,6 +1066,113 @@ __global__ __launch_bounds__(256) void k_struct_fields(const uint8_t* __restrict
 
 template __global__ void k_struct_fields<true>(const uint8_t*, uint64_t, StructSpec, uint8_t*);
 template __global__ void k_struct_fields<false>(const uint8_t*, uint64_t, StructSpec, uint8_t*);
+
+// Fused struct roots: one thread per record hashes every bytes field
+// (Keccak(le32(len) || bytes), one block), assembles the struct message in
+// LDS (dword-major: dword q of thread t at msg[q * 256 + t], conflict-free)
+// and absorbs it -- no message round trip through HBM and one launch instead
+// of two.  The next bytes field's loads are issued before the current
+// field's permutation, so their latency hides behind it.  Host-checked
+// layout: every bytes field dword-granular and at most 64 B, every output
+// offset and raw length a multiple of 4, records 4-byte aligned (16-B
+// aligned records and field offsets use 16-B loads).
+// Dynamic LDS: kStructThreads * msg_len bytes.
+namespace {
+__device__ __forceinline__ void load_field16(const uint8_t* __restrict__ p, uint32_t len, uint32_t vec16,
+                                             uint32_t (&a)[16]) {
+    if (vec16) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = (4u * k < len / 4) ? *reinterpret_cast<const uint4*>(p + 16 * k) : make_uint4(0, 0, 0, 0);
+            a[4 * k] = v.x;
+            a[4 * k + 1] = v.y;
+            a[4 * k + 2] = v.z;
+            a[4 * k + 3] = v.w;
+        }
+    } else {
+        const uint32_t* A32 = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) a[k] = (uint32_t)k < len / 4 ? A32[k] : 0u;
+    }
+}
+}  // namespace
+
+__global__ __launch_bounds__(kStructThreads) void k_struct_fused(const uint8_t* __restrict__ rec, uint64_t n,
+                                                                 StructSpec sp, uint32_t vec16,
+                                                                 uint4* __restrict__ roots) {
+    extern __shared__ uint32_t msg[];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * kStructThreads + tid;
+    const bool live = i < n;
+    const uint8_t* r = rec + (live ? i : 0) * sp.rec_len;
+    // first bytes field: loads in flight while the raw scalars are copied
+    uint32_t f = 0;
+    while (f < sp.nfields && sp.kind[f] != 1) ++f;
+    uint32_t nxt[16];
+    if (f < sp.nfields) load_field16(r + sp.off[f], sp.len[f], vec16, nxt);
+#pragma unroll 1
+    for (uint32_t g = 0; g < sp.nfields; ++g) {  // MK_FIELD_RAW, len 4 or 8
+        if (sp.kind[g] == 1) continue;
+        const uint32_t* A32 = reinterpret_cast<const uint32_t*>(r + sp.off[g]);
+        const uint32_t q0 = sp.out_off[g] / 4;
+        msg[q0 * kStructThreads + tid] = A32[0];
+        if (sp.len[g] == 8) msg[(q0 + 1) * kStructThreads + tid] = A32[1];
+    }
+#pragma unroll 1
+    while (f < sp.nfields) {  // MK_FIELD_BYTES: Keccak(le32(len) || bytes), one block
+        const uint32_t len = sp.len[f], q0 = sp.out_off[f] / 4;
+        uint32_t a[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) a[k] = nxt[k];
+        ++f;
+        while (f < sp.nfields && sp.kind[f] != 1) ++f;
+        if (f < sp.nfields) load_field16(r + sp.off[f], sp.len[f], vec16, nxt);
+        const uint32_t nd = len / 4 + 1;  // message dwords (<= 17)
+        State s;
+        zero(s);
+#pragma unroll
+        for (int q = 0; q < 18; ++q) {
+            uint32_t v = q == 0 ? len : ((uint32_t)q < nd ? a[q - 1] : 0u);
+            if ((uint32_t)q == nd) v ^= 1u;  // domain pad byte
+            if (q & 1)
+                s.hi[q / 2] ^= v;
+            else
+                s.lo[q / 2] ^= v;
+        }
+        s.hi[16] ^= 0x80000000u;
+        keccak_f(s);
+        uint4 d0, d1;
+        digest(s, d0, d1);
+        const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int w = 0; w < 8; ++w) msg[(q0 + w) * kStructThreads + tid] = dw[w];
+    }
+    // struct hash over the msg_len-byte message (msg_len % 4 == 0)
+    const uint32_t mw = sp.msg_len / 4, nb = sp.msg_len / 136 + 1;
+    State s;
+    zero(s);
+#pragma unroll 1
+    for (uint32_t b = 0; b < nb; ++b) {
+#pragma unroll
+        for (int w = 0; w < 34; ++w) {
+            const uint32_t q = 34 * b + w;
+            uint32_t v = q < mw ? msg[q * kStructThreads + tid] : 0u;
+            if (q == mw) v ^= 1u;
+            if (b == nb - 1 && w == 33) v ^= 0x80000000u;
+            if (w & 1)
+                s.hi[w / 2] ^= v;
+            else
+                s.lo[w / 2] ^= v;
+        }
+        keccak_f(s);
+    }
+    if (live) {
+        uint4 d0, d1;
+        digest(s, d0, d1);
+        roots[2 * i] = d0;
+        roots[2 * i + 1] = d1;
+    }
+}
 
 // ----------------------------------------------------------------------------
 // n messages of msg_len bytes, msg_len % 8 == 0, 8-byte aligned: whole-word

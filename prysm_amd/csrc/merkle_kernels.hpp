@@ -35,6 +35,9 @@ struct ReduceArgs {
 };
 
 constexpr uint32_t kMaxStructFields = 32;
+constexpr uint32_t kStructThreads = 256;              // k_struct_fused: one record per thread
+constexpr uint32_t kStructFusedMaxMsg = 160;          // LDS: kStructThreads * msg_len bytes
+constexpr uint32_t kStructFusedMaxField = 64;         // bytes fields held in 16 registers
 struct StructSpec {                 // flat fixed-layout record (hash.go:141-159)
     uint32_t kind[kMaxStructFields];   // 1 = bytes (hashed with le32 prefix), 2 = raw scalar
     uint32_t off[kMaxStructFields];    // byte offset inside the record
@@ -43,15 +46,16 @@ struct StructSpec {                 // flat fixed-layout record (hash.go:141-159
     uint32_t nfields, rec_len, msg_len;
 };
 
-template <bool LEAF, bool FAST>
+template <bool LEAF, bool FAST, int NI>
 __global__ void k_reduce(ReduceArgs a);
 template <bool FAST>
 __global__ void k_struct_fields(const uint8_t* rec, uint64_t n, StructSpec sp, uint8_t* msg);
+__global__ void k_struct_fused(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
 template <bool LEAF>
 __global__ void k_wave(ReduceArgs a);
 template <bool LEAF>
 __global__ void k_wave2(ReduceArgs a);
-template <uint32_t NT>
+template <uint32_t NT, bool LEAF>
 __global__ void k_wave3(ReduceArgs a);
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
 __global__ void k_finish_roots(const uint4* roots, uint64_t nroots, uint64_t n_items, uint4* out);

@@ -41,12 +41,18 @@ def sharded_merkle_hash(local_items: torch.Tensor, n_total: int, item_len: int, 
                         subtree_fn: Optional[Callable] = None,
                         full_fn: Optional[Callable] = None,
                         finish_fn: Optional[Callable] = None,
-                        gather_buf: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+                        gather_buf: Optional[torch.Tensor] = None,
+                        finish_stream=None) -> Optional[torch.Tensor]:
     """Returns the 32-byte merkleHash root on rank 0 (None elsewhere).
 
     ``local_items`` holds this rank's items [begin[rank], begin[rank+1]).
     When the tree is too small to shard (sp.nonempty == 1) rank 0 hashes
-    everything and the others contribute nothing."""
+    everything and the others contribute nothing.
+
+    ``finish_stream`` (a torch.cuda.Stream, rank 0): run the finisher there so
+    it overlaps the caller's next Merkleization instead of delaying it; the
+    returned root is then produced on that stream (synchronize before use).
+    The next call's all-gather waits for it before reusing ``gather_buf``."""
     if subtree_fn is None or full_fn is None or finish_fn is None:
         from . import device as D
         subtree_fn = subtree_fn or D.merkle_subtree
@@ -64,7 +70,13 @@ def sharded_merkle_hash(local_items: torch.Tensor, n_total: int, item_len: int, 
         root = torch.zeros(32, dtype=torch.uint8, device=dev)
     if gather_buf is None:
         gather_buf = torch.empty(world * 32, dtype=torch.uint8, device=dev)
+    if finish_stream is not None:  # the previous finish still reads gather_buf
+        torch.cuda.current_stream(dev).wait_stream(finish_stream)
     dist.all_gather_into_tensor(gather_buf, root, group=group)
     if rank == 0:
+        if finish_stream is not None:
+            finish_stream.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(finish_stream):
+                return finish_fn(gather_buf, sp.nonempty, n_total)
         return finish_fn(gather_buf, sp.nonempty, n_total)
     return None

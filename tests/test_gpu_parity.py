@@ -355,3 +355,29 @@ def test_state_root(gpu):
     want = O.keccak256(O.merkle_hash_flat(roots.reshape(-1), n, 32) +
                        O.merkle_hash_flat(bal.view(np.uint8), n, 8))
     assert R.state_root(reg, bal) == want
+
+
+# Struct layouts that take the fused one-kernel path (dword-granular fields,
+# with and without 16-B loads, one- and two-block messages) and the two-kernel
+# fallback (2-byte scalar, >160-B message, non-dword bytes field).
+_STRUCT_LAYOUTS = {
+    "fused_dword_loads": (100, [(1, 4, 36), (2, 40, 8), (1, 48, 20), (2, 68, 4), (2, 72, 8)]),
+    "fused_vec16_two_blocks": (208, [(1, 0, 16), (1, 16, 32), (1, 48, 48), (1, 96, 64), (1, 160, 48)]),
+    "fused_tail_field": (96, [(2, 0, 8), (1, 8, 4), (1, 16, 80)]),
+    "fallback_u16": (52, [(1, 0, 32), (2, 32, 2), (2, 36, 8)]),
+    "fallback_long_msg": (192, [(1, 32 * k, 32) for k in range(6)]),
+    "fallback_odd_bytes": (48, [(1, 0, 33), (2, 36, 4)]),
+}
+
+
+@pytest.mark.parametrize("layout", sorted(_STRUCT_LAYOUTS))
+@pytest.mark.parametrize("n", [1, 257, 3000])
+def test_struct_roots_layouts(gpu, layout, n):
+    from oracle import oracle as O
+    from prysm_amd import registry as R
+
+    rec_len, spec = _STRUCT_LAYOUTS[layout]
+    raw = O.splitmix_bytes(n * rec_len, SEED + 97 + rec_len)
+    recs = raw.view(np.dtype((np.void, rec_len)))
+    want = O.struct_roots(raw, n, rec_len, spec, nthreads=8)
+    assert np.array_equal(R.struct_roots(recs, spec), want)
