@@ -50,6 +50,10 @@ constexpr uint64_t kLeafWaveMaxC1 = 1ull << MK_LEAF_WAVE_MAX_LOG2;  // leaf pass
 #define MK_REDUCE_NI2_MIN_LOG2 18
 #endif
 constexpr uint64_t kReduceNi2MinC1 = 1ull << MK_REDUCE_NI2_MIN_LOG2;  // leaf passes narrower than this use NI = 1
+#ifndef MK_TOP_ONE_WG
+#define MK_TOP_ONE_WG 1
+#endif
+constexpr bool kTopOneWg = MK_TOP_ONE_WG != 0;
 #ifndef MK_STRUCT_FUSED
 #define MK_STRUCT_FUSED 1
 #endif
@@ -266,8 +270,11 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         // k_wave3: the smallest workgroup (64..1024 threads, 2 per pair) that
         // keeps the pass within ~256 workgroups, one per CU
         uint32_t nt = w3 ? mk::kWaveThreads : (wave ? mk::kWaveThreads : kReduceThreads);
-        if (w3)
+        if (w3) {
             while (nt < mk::kMidThreads && ceil_div(c1, nt / 2) > kNodeWaveWgs) nt *= 2;
+            if (kTopOneWg)  // the last <= 512 pairs in one workgroup: one launch to the root
+                while (nt < mk::kMidThreads && c1 <= mk::kMidThreads / 2 && c1 > nt / 2) nt *= 2;
+        }
         // throughput pass: 2 window pairs per thread on wide passes, 1 on mid-size
         // leaf passes so they still spread over the CUs
         const uint32_t ni = (!wave && leaf && c1 < kReduceNi2MinC1) ? 1 : 2;
@@ -880,12 +887,14 @@ int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64
     }
     HIPCHK(hipGetLastError());
     // level d lives at lv + 2 * sum_{i<d} count_i (uint4 units).  Wide levels:
-    // one launch per level (every lane busy); narrow top (<= 2^15 nodes) plus
-    // the zero-sibling tail: k_trie_top2, 6 levels per workgroup of 64 inputs.
+    // one launch per level (every lane busy); the narrow top (<= 2^17 nodes)
+    // plus the zero-sibling tail: k_trie_top3 (bit-interleaved lane pairs),
+    // log2(NT) levels per workgroup of NT inputs, the last launch to the top.
     uint64_t c = n;
     uint4* cur = lv;
     uint32_t d = 0;
-    while (d < depth && c > (1ull << 15)) {
+    const uint64_t top_max = kWave3 ? kNodeWaveMaxC1 : (1ull << 15);
+    while (d < depth && c > top_max) {
         uint4* nxt = cur + 2 * c;
         const uint64_t cn = (c + 1) / 2;
         hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(cn, 256)), dim3(256), 0, st, cur, c, nxt);
@@ -895,21 +904,37 @@ int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64
         ++d;
     }
     while (d < depth) {
-        const uint64_t nwg = ceil_div(c, 2 * mk::kWave2Span);
-        // levels this launch: up to 6 while several workgroups remain; the last
-        // (single-workgroup) launch runs to the top of the trie
-        uint32_t k = 0;
-        uint64_t cc = c;
-        if (nwg == 1) {
-            k = depth - d;
+        uint32_t k = 0, nt = 0;
+        uint64_t nwg = 0;
+        if (kWave3) {
+            nt = mk::kWaveThreads;
+            while (nt < mk::kMidThreads && ceil_div(c, nt) > kNodeWaveWgs) nt *= 2;
+            if (kTopOneWg)  // the last <= 1024 nodes in one workgroup
+                while (nt < mk::kMidThreads && c <= mk::kMidThreads && c > nt) nt *= 2;
+            nwg = ceil_div(c, nt);
+            k = nwg == 1 ? depth - d : std::min<uint32_t>(ilog2(nt), depth - d);
         } else {
-            while (k < mk::kWave2Levels && cc > 1) {
-                cc = (cc + 1) / 2;
-                ++k;
+            nwg = ceil_div(c, 2 * mk::kWave2Span);
+            uint64_t cc = c;
+            if (nwg == 1) {
+                k = depth - d;
+            } else {
+                while (k < mk::kWave2Levels && cc > 1) {
+                    cc = (cc + 1) / 2;
+                    ++k;
+                }
             }
         }
-        hipLaunchKernelGGL(mk::k_trie_top2, dim3(nwg), dim3(mk::kWaveThreads), 0, st, (const uint32_t*)cur, c,
-                           (uint32_t*)(cur + 2 * c), k);
+        const uint32_t* src = (const uint32_t*)cur;
+        uint32_t* dst = (uint32_t*)(cur + 2 * c);
+        switch (nt) {
+            case 0: hipLaunchKernelGGL(mk::k_trie_top2, dim3(nwg), dim3(mk::kWaveThreads), 0, st, src, c, dst, k); break;
+            case 64: hipLaunchKernelGGL(mk::k_trie_top3<64>, dim3(nwg), dim3(64), 0, st, src, c, dst, k); break;
+            case 128: hipLaunchKernelGGL(mk::k_trie_top3<128>, dim3(nwg), dim3(128), 0, st, src, c, dst, k); break;
+            case 256: hipLaunchKernelGGL(mk::k_trie_top3<256>, dim3(nwg), dim3(256), 0, st, src, c, dst, k); break;
+            case 512: hipLaunchKernelGGL(mk::k_trie_top3<512>, dim3(nwg), dim3(512), 0, st, src, c, dst, k); break;
+            default: hipLaunchKernelGGL(mk::k_trie_top3<1024>, dim3(nwg), dim3(1024), 0, st, src, c, dst, k); break;
+        }
         HIPCHK(hipGetLastError());
         for (uint32_t i = 0; i < k; ++i) {
             cur += 2 * c;

@@ -880,6 +880,62 @@ __global__ __launch_bounds__(kWaveThreads) void k_trie_top2(const uint32_t* __re
     }
 }
 
+// Narrow top of the deposit trie, bit-interleaved lane pairs (mk::ilv): the
+// workgroup owns NT input nodes of level d (NT/2 lane pairs) and writes
+// `levels` levels to the (plain) level array; once the count is 1 it goes on
+// with node = K(node || 0^32), the zero-sibling levels of
+// deposit_trie.go:33-38.  The host picks NT so a launch has <= ~256
+// workgroups; the last launch (one workgroup) runs to the top of the trie.
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void k_trie_top3(const uint32_t* __restrict__ in, uint64_t cin,
+                                                  uint32_t* __restrict__ lv_out, uint32_t levels) {
+    constexpr uint32_t kPairs = NT / 2;
+    __shared__ uint32_t lds[8 * kPairs];
+    const uint32_t tid = threadIdx.x, k = tid >> 1, p = tid & 1u;
+    uint64_t c = cin;
+    uint64_t lo = (uint64_t)blockIdx.x * NT;  // first input node of this workgroup
+    uint64_t m = (c - lo) < NT ? (c - lo) : NT;
+    uint32_t* dst = lv_out;
+    for (uint32_t l = 0; l < levels; ++l) {
+        const uint64_t cn = (c + 1) / 2, mn = (m + 1) / 2;
+        const bool act = k < mn;
+        uint32_t a[4], b[4] = {0, 0, 0, 0};
+        if (act) {
+            const bool right = 2 * (uint64_t)k + 1 < m;
+            if (l == 0) {
+                load_node3(in, lo + 2 * (uint64_t)k, false, p, a);
+                if (right) load_node3(in, lo + 2 * (uint64_t)k + 1, false, p, b);
+            } else {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) a[w] = lds[16 * k + 2 * w + p];
+                if (right) {
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) b[w] = lds[16 * k + 8 + 2 * w + p];
+                }
+            }
+        }
+        __syncthreads();
+        if (act) {
+            uint32_t d[4];
+            hash_pair3(a, b, false, p, d);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) lds[8 * k + 2 * w + p] = d[w];
+            store_node3(dst, lo / 2 + k, false, p, d);
+        }
+        __syncthreads();
+        dst += 8 * cn;
+        c = cn;
+        m = mn;
+        lo /= 2;
+    }
+}
+
+template __global__ void k_trie_top3<64>(const uint32_t*, uint64_t, uint32_t*, uint32_t);
+template __global__ void k_trie_top3<128>(const uint32_t*, uint64_t, uint32_t*, uint32_t);
+template __global__ void k_trie_top3<256>(const uint32_t*, uint64_t, uint32_t*, uint32_t);
+template __global__ void k_trie_top3<512>(const uint32_t*, uint64_t, uint32_t*, uint32_t);
+template __global__ void k_trie_top3<1024>(const uint32_t*, uint64_t, uint32_t*, uint32_t);
+
 // ----------------------------------------------------------------------------
 // Final hash for trees with <= 1 chunk: K(bytes[0,total) || [0^128 if n==0] || lenc)
 __global__ void k_final_small(const uint8_t* __restrict__ items, uint64_t total, uint64_t n, uint8_t* out) {

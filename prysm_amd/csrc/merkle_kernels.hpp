@@ -66,6 +66,8 @@ __global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
 __global__ void k_keccak_words(const uint2* in, uint64_t n, uint32_t nwords, uint4* out);
 __global__ void k_trie_reduce(const uint4* in, uint64_t cin, uint4* lv_out, uint32_t levels);
 __global__ void k_trie_top2(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels);
+template <uint32_t NT>
+__global__ void k_trie_top3(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels);
 __global__ void k_trie_tail(uint4* node, uint32_t count, uint4* levels);
 __global__ void k_verify_branches(const uint4* leaves, const uint4* branches, const uint64_t* indices,
                                   uint32_t depth, uint32_t tree_depth, const uint4* roots, uint64_t n,

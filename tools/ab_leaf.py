@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--log2n", type=int, default=26)
     ap.add_argument("--item-len", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--trie", action="store_true", help="A/B the depth-32 deposit trie over 2^log2n x 280-B deposits")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -43,6 +44,8 @@ def main():
             os.path.join(ROOT, "prysm_amd", "lib", "variants", f"libprysm_merkle_{v}.so")
         libs[v] = load(p)
         assert libs[v].mk_init(0) == 0
+    if a.trie:
+        return ab_trie(a, libs, dev)
     n, il = 1 << a.log2n, a.item_len
     items = torch.empty(n * il, dtype=torch.uint8, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -78,6 +81,36 @@ def main():
         print(json.dumps({"variant": v, "log2n": a.log2n, "median_ms": statistics.median(times[v]),
                           "min_ms": min(times[v]), "leaf_median_ms": statistics.median(leaf[v]),
                           "leaves_per_s": n / (statistics.median(times[v]) / 1e3)}))
+    print(json.dumps({"root": roots[a.variants[0]]}))
+
+
+def ab_trie(a, libs, dev):
+    import torch
+
+    n, ln, depth = 1 << a.log2n, 280, 32
+    data = torch.empty(n * ln, dtype=torch.uint8, device=dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    first = libs[a.variants[0]]
+    assert first.mk_dev_synth_fill(ctypes.c_void_p(data.data_ptr()), n * ln, 0x5EED000000000005, 0, st) == 0
+    lv = torch.empty(first.mk_deposit_trie_levels_bytes(n, depth), dtype=torch.uint8, device=dev)
+    outs = {v: torch.empty(32, dtype=torch.uint8, device=dev) for v in a.variants}
+    times = {v: [] for v in a.variants}
+    for r in range(a.rounds + 1):
+        for v, L in libs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = L.mk_dev_deposit_trie_build(ctypes.c_void_p(data.data_ptr()), None, n, ln, depth,
+                                             ctypes.c_void_p(lv.data_ptr()), ctypes.c_void_p(outs[v].data_ptr()), st)
+            e1.record()
+            torch.cuda.synchronize()
+            assert rc == 0, (v, rc)
+            if r:
+                times[v].append(e0.elapsed_time(e1))
+    roots = {v: bytes(o.cpu().numpy()).hex() for v, o in outs.items()}
+    assert len(set(roots.values())) == 1, roots
+    for v in a.variants:
+        print(json.dumps({"variant": v, "trie_log2n": a.log2n, "median_ms": statistics.median(times[v]),
+                          "min_ms": min(times[v])}))
     print(json.dumps({"root": roots[a.variants[0]]}))
 
 

@@ -10,3 +10,7 @@ for n in ${AB_SIZES:-25 28}; do
   timeout -k 10 300 python tools/ab_leaf.py --log2n $n --rounds ${AB_ROUNDS:-7} ${AB_VARIANTS:-main} > gpurun_out/ab_$n.json 2>&1 || { cat gpurun_out/ab_$n.json; exit 1; }
   cat gpurun_out/ab_$n.json
 done
+for n in ${AB_TRIE_SIZES:-}; do
+  timeout -k 10 300 python tools/ab_leaf.py --trie --log2n $n --rounds ${AB_ROUNDS:-7} ${AB_VARIANTS:-main} > gpurun_out/ab_trie_$n.json 2>&1 || { cat gpurun_out/ab_trie_$n.json; exit 1; }
+  cat gpurun_out/ab_trie_$n.json
+done
