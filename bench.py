@@ -181,7 +181,7 @@ def main():
                        "shard_height": sp.height, "root": root_hex},
             "roofline": {
                 "bound": "valu-int",
-                "kernel": "k_reduce<LEAF> (leaf pass: 256-B windows + 4 fused levels)",
+                "kernel": "k_reduce<LEAF, FAST, 2> (leaf pass: 256-B windows + 4 fused levels)",
                 "achieved": achieved / 1e12,
                 "peak": PEAK_INT_OPS / 1e12,
                 "unit": "Tops/s (int32 VALU)",

@@ -1,6 +1,6 @@
 """Summarise a tools/profile.sh run: per-kernel average duration from the
 kernel-trace stats, and per-dispatch PMC counters of the leaf kernel
-(k_reduce<true, true>), with the gfx950 FETCH_SIZE x2 correction
+(k_reduce<true, true, 2>), with the gfx950 FETCH_SIZE x2 correction
 (MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes of a wide
 coalesced stream; FETCH_SIZE/WRITE_SIZE are in KiB)."""
 import csv
@@ -10,7 +10,7 @@ import os
 import sys
 from collections import defaultdict
 
-LEAF = "k_reduce<true, true>"
+LEAF = "k_reduce<true, true, 2>"
 
 
 def counters(d):
