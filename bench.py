@@ -72,6 +72,10 @@ def main():
     ap.add_argument("--item-len", type=int, default=32)
     ap.add_argument("--cpu-sample-log2n", type=int, default=24)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N ranks on one GPU)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="all ranks on cuda:0 (rehearsal of the N-rank path on a one-GPU box, with --backend gloo)")
     ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5"],
                     help="BASELINE.json config: c4 = headline (default); c2/c3/c5 = single-GPU side benches")
     args = ap.parse_args()
@@ -91,10 +95,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if args.share_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     n, item_len = 1 << args.log2n, args.item_len
     sp = P.plan(n, item_len, world)
@@ -151,7 +160,7 @@ def main():
     if rank == 0 and r is not None:
         root_hex = bytes(r.cpu().numpy()).hex()
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = t.item()

@@ -72,7 +72,14 @@ def sharded_merkle_hash(local_items: torch.Tensor, n_total: int, item_len: int, 
         gather_buf = torch.empty(world * 32, dtype=torch.uint8, device=dev)
     if finish_stream is not None:  # the previous finish still reads gather_buf
         torch.cuda.current_stream(dev).wait_stream(finish_stream)
-    dist.all_gather_into_tensor(gather_buf, root, group=group)
+    if root.is_cuda and dist.get_backend(group) == "gloo":
+        # rehearsal of the N-rank path on one GPU (bench.py --backend gloo):
+        # gloo gathers host tensors
+        host = torch.empty(gather_buf.numel(), dtype=torch.uint8)
+        dist.all_gather_into_tensor(host, root.cpu(), group=group)
+        gather_buf.copy_(host)
+    else:
+        dist.all_gather_into_tensor(gather_buf, root, group=group)
     if rank == 0:
         if finish_stream is not None:
             finish_stream.wait_stream(torch.cuda.current_stream(dev))
