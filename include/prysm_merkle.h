@@ -127,6 +127,19 @@ int mk_dev_ssz_struct_list_root(const void* d_records, uint64_t n, uint32_t reco
 int mk_ssz_struct_list_root(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
                             uint32_t nfields, uint8_t out[32]);
 
+/* ---- hashutil.MerkleRoot (merkleRoot.go:12-30) -------------------------- */
+/* Root of the heap o[i] = Hash(o[2i] || o[2i+1]) over leaves
+ * o[n+i] = Hash(values[i]); values i = data[offs[i], offs[i+1]).  leaves_out
+ * (optional, n x 32) receives Hash(values[i]): the reference overwrites its
+ * input slice with them (merkleRoot.go:16-19) and a drop-in keeps that side
+ * effect.  n == 0 is MK_EINVAL (the reference panics: index out of range). */
+int mk_merkle_root(const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_t* leaves_out, uint8_t out[32]);
+uint64_t mk_merkle_root_workspace_bytes(uint64_t n);
+/* Device-resident: d_offs (n+1, device) or fixed_len; d_heap of
+ * mk_merkle_root_workspace_bytes(n); d_leaves32 optional (n x 32). */
+int mk_dev_merkle_root(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len, void* d_heap,
+                       uint64_t heap_bytes, void* d_leaves32, void* d_out32, void* stream);
+
 /* ---- trieutil deposit trie (deposit_trie.go:29-81) ---------------------- */
 /* Batch build of the depth-`depth` sparse trie over n deposits (message i =
  * data[offs[i], offs[i+1])).  Equals n calls of UpdateDepositTrie: empty nodes

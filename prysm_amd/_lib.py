@@ -58,6 +58,9 @@ _SIGS = {
     "mk_ssz_struct_list_workspace_bytes": (_u64, [_u64, _vp, _u32]),
     "mk_dev_ssz_struct_list_root": (_int, [_vp, _u64, _u32, _vp, _u32, _vp, _vp, _u64, _vp]),
     "mk_ssz_struct_list_root": (_int, [_vp, _u64, _u32, _vp, _u32, _vp]),
+    "mk_merkle_root": (_int, [_vp, _vp, _u64, _vp, _vp]),
+    "mk_merkle_root_workspace_bytes": (_u64, [_u64]),
+    "mk_dev_merkle_root": (_int, [_vp, _vp, _u64, _u32, _vp, _u64, _vp, _vp, _vp]),
     "mk_deposit_trie_levels_bytes": (_u64, [_u64, _u32]),
     "mk_deposit_trie_build": (_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
     "mk_dev_deposit_trie_build": (_int, [_vp, _vp, _u64, _u32, _u32, _vp, _vp, _vp]),

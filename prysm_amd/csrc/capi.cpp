@@ -213,14 +213,17 @@ uint32_t levels_to_one(uint64_t count) {
 // Builds the pass sequence.  subtree=false: full merkleHash with the length
 // mix-in; subtree=true: exactly `height` levels above the chunks, output one
 // node (pad_at_one keeps the odd rule alive at count 1).
+// node_input: the input is n 32-B nodes reduced pairwise (a plain binary
+// tree, no chunking; hashutil.MerkleRoot's heap bands), subtree must be set.
 int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool pad_at_one,
-              bool aligned16, Plan& p) {
+              bool aligned16, Plan& p, bool node_input = false) {
     p = Plan();
     p.n = n;
     if (n > 0 && item_len == 0) return fail(MK_EINVAL, "item_len == 0 (reference: integer divide by zero)");
+    if (node_input && (!subtree || item_len != 32)) return fail(MK_EINVAL, "planner: node input needs subtree mode");
     const uint64_t total = n * (uint64_t)item_len;
-    const uint64_t cb = n ? chunk_bytes(item_len) : 128;
-    const uint64_t nchunks = n ? ceil_div(total, cb) : 0;
+    const uint64_t cb = node_input ? 32 : n ? chunk_bytes(item_len) : 128;
+    const uint64_t nchunks = node_input ? n : n ? ceil_div(total, cb) : 0;
     p.total = total;
     if (!subtree && nchunks <= 1) {
         p.small = true;
@@ -230,7 +233,7 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         return fail(MK_EINVAL, "subtree: bad height %u for %llu chunks", height, (unsigned long long)nchunks);
 
     uint32_t remaining = subtree ? height : levels_to_one(nchunks);
-    bool leaf = true;
+    bool leaf = !node_input;
     uint64_t cin = nchunks;  // leaf: chunks; node: input nodes
     int slot = 0;
     int in_slot = -1;
@@ -849,6 +852,102 @@ extern "C" int mk_ssz_struct_list_root(const uint8_t* records, uint64_t n, uint3
     if (n) HIPCHK(hipMemcpyAsync(L.c->in.p, records, n * (size_t)record_len, hipMemcpyHostToDevice, st));
     TRY(mk_dev_ssz_struct_list_root(L.c->in.p, n, record_len, fields, nfields, L.c->out.p, L.c->ws.p, wsb, st));
     HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+// ---- hashutil.MerkleRoot (merkleRoot.go:12-30) ------------------------------------
+// Heap o[1..2n): leaves o[n+i] = Hash(values[i]); o[i] = Hash(o[2i] || o[2i+1])
+// for i = n-1 .. 1; the result is o[1].  The children of a heap band
+// [2^k, 2^(k+1)) are the contiguous range [2^(k+1), 2^(k+2)), so with
+// P = 2^floor(log2 n): when n > P the partial band [P, n) is one pairwise
+// level over o[2P, 2n), and everything above is a power-of-two binary tree
+// over o[P, 2P) -- a node-input merkle plan.  (The reference's spurious
+// newSet[0] = Hash(nil || o[1]) is computed and discarded; it is skipped.)
+static uint64_t pow2_floor(uint64_t n) {
+    uint64_t p = 1;
+    while (p * 2 <= n) p *= 2;
+    return p;
+}
+
+extern "C" uint64_t mk_merkle_root_workspace_bytes(uint64_t n) {
+    if (n == 0) return 0;
+    const uint64_t P = pow2_floor(n);
+    Plan p;
+    uint64_t ws = 0;
+    if (P > 1 && make_plan(P, 32, true, ilog2(P), false, true, p, true) == MK_OK) ws = plan_ws_bytes(p);
+    return 64 * n + align256(ws) + 256;
+}
+
+extern "C" int mk_dev_merkle_root(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len,
+                                  void* d_heap, uint64_t heap_bytes, void* d_leaves32, void* d_out32, void* stream) {
+    TRY(bind(-1));
+    if (n == 0) return fail(MK_EINVAL, "MerkleRoot of an empty list (reference: index out of range)");
+    if (!d_heap || !d_out32 || (!d_offs && !d_data && fixed_len)) return fail(MK_EINVAL, "null pointer");
+    if (heap_bytes < mk_merkle_root_workspace_bytes(n)) return fail(MK_ENOMEM, "heap workspace too small");
+    hipStream_t st = (hipStream_t)stream;
+    uint8_t* heap = (uint8_t*)d_heap;  // node i at heap + 32 i (node 0 unused)
+    uint4* leaves = (uint4*)(heap + 32 * n);
+    if (d_offs) {
+        hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, d_offs,
+                           n, leaves);
+    } else if (fixed_len == 64 && ((uintptr_t)d_data % 16) == 0) {
+        hipLaunchKernelGGL(mk::k_keccak64, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint4*)d_data, n, leaves);
+    } else if (fixed_len % 8 == 0 && ((uintptr_t)d_data % 8) == 0) {
+        hipLaunchKernelGGL(mk::k_keccak_words, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint2*)d_data, n,
+                           fixed_len / 8, leaves);
+    } else {
+        hipLaunchKernelGGL(mk::k_keccak_fixed, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, n,
+                           fixed_len, leaves);
+    }
+    HIPCHK(hipGetLastError());
+    if (d_leaves32 && d_leaves32 != (void*)leaves)
+        HIPCHK(hipMemcpyAsync(d_leaves32, leaves, 32 * n, hipMemcpyDeviceToDevice, st));
+    if (n == 1) {  // the loop body never runs: o[1] is the hashed value
+        HIPCHK(hipMemcpyAsync(d_out32, leaves, 32, hipMemcpyDeviceToDevice, st));
+        return MK_OK;
+    }
+    const uint64_t P = pow2_floor(n);
+    if (P < n)  // partial band [P, n): o[i] = Hash(o[2i] || o[2i+1]) over o[2P, 2n)
+        hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(n - P, 256)), dim3(256), 0, st,
+                           (const uint4*)(heap + 64 * P), 2 * (n - P), (uint4*)(heap + 32 * P));
+    HIPCHK(hipGetLastError());
+    Plan p;
+    TRY(make_plan(P, 32, true, ilog2(P), false, true, p, true));
+    uint8_t* ws = heap + 64 * n;
+    return launch_plan(p, heap + 32 * P, (uint8_t*)d_out32, ws, heap_bytes - 64 * n, st);
+}
+
+extern "C" int mk_merkle_root(const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_t* leaves_out,
+                              uint8_t out[32]) {
+    if (!out || (n && !offs)) return fail(MK_EINVAL, "null pointer");
+    if (n == 0) return fail(MK_EINVAL, "MerkleRoot of an empty list (reference: index out of range)");
+    Locked L;
+    TRY(lock_current(L));
+    hipStream_t st = L.c->stream;
+    const size_t inb = offs[n] - offs[0];
+    bool uniform = true;
+    const uint64_t len0 = offs[1] - offs[0];
+    for (uint64_t i = 1; uniform && i < n; ++i) uniform = (offs[i + 1] - offs[i]) == len0;
+    uniform = uniform && len0 <= UINT32_MAX;
+    const uint64_t wsb = mk_merkle_root_workspace_bytes(n);
+    TRY(grow(L.c->in, inb + 16));
+    TRY(grow(L.c->aux, 8 * (n + 1)));
+    TRY(grow(L.c->ws, wsb));
+    TRY(grow(L.c->out, 32));
+    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, data + offs[0], inb, hipMemcpyHostToDevice, st));
+    if (!uniform) {
+        std::vector<uint64_t> rel(offs, offs + n + 1);
+        for (auto& o : rel) o -= offs[0];
+        HIPCHK(hipMemcpyAsync(L.c->aux.p, rel.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
+        TRY(mk_dev_merkle_root(L.c->in.p, (const uint64_t*)L.c->aux.p, n, 0, L.c->ws.p, wsb, nullptr, L.c->out.p,
+                               st));
+        HIPCHK(hipStreamSynchronize(st));  // rel is a stack vector
+    } else {
+        TRY(mk_dev_merkle_root(L.c->in.p, nullptr, n, (uint32_t)len0, L.c->ws.p, wsb, nullptr, L.c->out.p, st));
+    }
+    HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
+    if (leaves_out) HIPCHK(hipMemcpyAsync(leaves_out, (uint8_t*)L.c->ws.p + 32 * n, 32 * n, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return MK_OK;
 }

@@ -65,24 +65,18 @@ def MerkleRoot(values: List[bytes]) -> bytes:
     """hashutil.MerkleRoot (merkleRoot.go:12-30), including its side effect:
     ``values[i]`` is replaced by ``Hash(values[i])`` (merkleRoot.go:16-19).
 
-    Heap layout o[i] = Hash(o[2i] || o[2i+1]) for i = n-1 .. 1; the nodes of
-    one heap band [2^k, 2^(k+1)) only depend on the band below, so each band
-    is one batched GPU launch.  Like the reference, an empty list is an
-    index-out-of-range panic (IndexError here)."""
+    One library call (``mk_merkle_root``): the leaves are hashed into the
+    upper half of the heap o[1..2n), the partial top heap band is one
+    pairwise level and the rest a power-of-two binary tree on the device.
+    Like the reference, an empty list is an index-out-of-range panic
+    (IndexError here)."""
     n = len(values)
     if n == 0:
         raise IndexError("index out of range [1] with length 0")
-    leaves = hash_batch_var(values)
-    for i, h in enumerate(leaves):
-        values[i] = h
-    o: List[bytes] = [b""] * n + leaves
-    top = n - 1
-    while top >= 1:
-        lo = 1 << (top.bit_length() - 1)  # band [lo, top]
-        idx = range(top, lo - 1, -1)
-        msgs = np.frombuffer(b"".join(o[2 * i] + o[2 * i + 1] for i in idx), dtype=np.uint8)
-        hs = hash_batch(msgs, 64)
-        for k, i in enumerate(idx):
-            o[i] = bytes(hs[k])
-        top = lo - 1
-    return o[1]
+    data, offs = _flatten(values)
+    leaves = np.empty((n, 32), dtype=np.uint8)
+    out = ctypes.create_string_buffer(32)
+    _lib.check(_lib.load().mk_merkle_root(_ptr(data), _ptr(offs), n, _ptr(leaves), out), "mk_merkle_root")
+    for i in range(n):
+        values[i] = bytes(leaves[i])
+    return out.raw

@@ -239,6 +239,22 @@ def test_merkle_root(gpu, n):
     assert mutated == [O.keccak256(v) for v in vals]  # merkleRoot.go:16-19 side effect
 
 
+@pytest.mark.parametrize("n,vlen", [(1, 32), (6, 64), (1000, 32), (1000, 64), (4097, 280), ((1 << 19) + 3, 32)])
+def test_merkle_root_uniform(gpu, n, vlen):
+    """Equal-length values take the fixed-length leaf kernels (64-B, word,
+    byte); 2^19 + 3 values run a partial heap band plus k_reduce node passes."""
+    from oracle import oracle as O
+    from prysm_amd import hashutil as H
+
+    raw = O.splitmix_bytes(n * vlen, SEED + 17 + vlen)
+    vals = [bytes(raw[i * vlen:(i + 1) * vlen]) for i in range(n)]
+    want = O.merkle_root(vals)
+    mutated = list(vals)
+    assert H.MerkleRoot(mutated) == want
+    if n <= 1000:
+        assert mutated == [O.keccak256(v) for v in vals]
+
+
 def test_merkle_root_reference_vector(gpu, ref_vectors):
     from prysm_amd import hashutil as H
 
