@@ -75,13 +75,14 @@ def main():
             if r:  # round 0 is warmup
                 times[v].append(e0.elapsed_time(e1))
                 leaf[v].append(ms.value)
-    roots = {v: bytes(o.cpu().numpy()).hex() for v, o in outs.items()}
-    assert len(set(roots.values())) == 1, roots
+    # "nl_*" variants are compute-only probes (MK_NOLOAD): their roots differ
+    roots = {v: bytes(o.cpu().numpy()).hex() for v, o in outs.items() if not v.startswith("nl_")}
+    assert len(set(roots.values())) <= 1, roots
     for v in a.variants:
         print(json.dumps({"variant": v, "log2n": a.log2n, "median_ms": statistics.median(times[v]),
                           "min_ms": min(times[v]), "leaf_median_ms": statistics.median(leaf[v]),
                           "leaves_per_s": n / (statistics.median(times[v]) / 1e3)}))
-    print(json.dumps({"root": roots[a.variants[0]]}))
+    print(json.dumps({"root": next(iter(roots.values()), None)}))
 
 
 def ab_trie(a, libs, dev):
@@ -111,7 +112,7 @@ def ab_trie(a, libs, dev):
     for v in a.variants:
         print(json.dumps({"variant": v, "trie_log2n": a.log2n, "median_ms": statistics.median(times[v]),
                           "min_ms": min(times[v])}))
-    print(json.dumps({"root": roots[a.variants[0]]}))
+    print(json.dumps({"root": next(iter(roots.values()), None)}))
 
 
 if __name__ == "__main__":

@@ -65,6 +65,25 @@ TESTS = {
 }
 # wave-specialised: even workgroups run SPLIT[0], odd ones SPLIT[1]
 SPLIT = {"split_B_A": ([B3], [AL]), "split_B_B": ([B3], [CH])}
+# phase-aligned: 1024-thread workgroups (4 waves per SIMD, all of one
+# workgroup) so an s_barrier lines up every wave of a SIMD on the same
+# instruction class.  name -> segments; "|" between segments = s_barrier,
+# a trailing barrier closes every iteration when bar_end is set.
+# (segments, bar_end)
+SYNC = {
+    "s_B": ([[B3] * 64], True),
+    "s_A": ([[AL] * 64], True),
+    "s_B32A32_nobar": ([[B3] * 32 + [AL] * 32], False),
+    "s_B32A32_bar1": ([[B3] * 32 + [AL] * 32], True),
+    "s_B32|A32": ([[B3] * 32, [AL] * 32], True),
+    "s_B64|A64": ([[B3] * 64, [AL] * 64], True),
+    "s_B128|A128": ([[B3] * 128, [AL] * 128], True),
+    # Keccak-round shaped: F72 H10 F50 H48 (122 full + 58 half)
+    "s_round_nobar": ([[B3] * 72 + [AL] * 10 + [B3] * 50 + [AL] * 48], False),
+    "s_round_bar1": ([[B3] * 72 + [AL] * 10 + [B3] * 50 + [AL] * 48], True),
+    "s_round_bar4": ([[B3] * 72, [AL] * 10, [B3] * 50, [AL] * 48], True),
+    "s_round_bar2": ([[B3] * 72 + [AL] * 10 + [B3] * 50, [AL] * 48], True),
+}
 
 def regs(c, kind):
     if kind == "pair":  # 64-bit chains v[40+2c : 41+2c] (4 chains reused twice)
@@ -136,6 +155,43 @@ def gen():
         assert len(b0) == len(b1)
         names.append((name, len(b0)))
         emit(name, [b0, b1])
+    def emit_sync(name, segs, bar_end):
+        out.append(f"__global__ __launch_bounds__(1024) void k_{name.replace('|', '_')}(unsigned* out, int iters, unsigned long long* clk) {{")
+        out.append("    unsigned seed = threadIdx.x * 2654435761u + blockIdx.x;")
+        out.append("    asm volatile(\"v_mov_b32 v40, %0\\n\"")
+        for r in list(range(41, 48)) + list(range(48, 64)):
+            out.append(f"        \"v_add_u32 v{r}, {r}, v40\\n\"")
+        out.append(f"        :: \"v\"(seed) : {clob});")
+        out.append("    __syncthreads();")
+        out.append("    unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();")
+        out.append("#pragma unroll 1")
+        out.append("    for (int it = 0; it < iters; ++it) {")
+        lines = []
+        for si, seg in enumerate(segs):
+            lines += [seg[k].format(**regs(k % 8, "diff")) for k in range(len(seg))]
+            if si + 1 < len(segs) or bar_end:
+                lines.append("s_barrier")
+        out.append("        asm volatile(")
+        out.append("\n".join(f'        "{l}\\n"' for l in lines))
+        out.append(f"        ::: {clob});")
+        out.append("    }")
+        out.append("    unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();")
+        out.append("    unsigned x;")
+        out.append("    asm volatile(\"v_xor_b32 %0, v40, v41\\n v_xor_b32 %0, v42, %0\\n\" : \"=v\"(x) :: " + clob + ");")
+        out.append("    out[blockIdx.x * blockDim.x + threadIdx.x] = x;")
+        out.append("    if (threadIdx.x == 0 && blockIdx.x == 0) { clk[0] = t1 - t0; clk[1] = r1 - r0; }")
+        out.append("}")
+        out.append("")
+
+    if ONLY != "sync":
+        pass
+    else:
+        del names[:]
+        out[:] = out[:7]
+    sync_names = []
+    for name, (segs, bar_end) in SYNC.items():
+        emit_sync(name, segs, bar_end)
+        sync_names.append((name, sum(len(x) for x in segs)))
     out.append("""
 typedef void (*kfn)(unsigned*, int, unsigned long long*);
 static void run(const char* name, kfn k, int ninstr, int blocks, int threads, int iters) {
@@ -158,8 +214,11 @@ static void run(const char* name, kfn k, int ninstr, int blocks, int threads, in
     // cycles per wave-instruction per SIMD (throughput: all waves of a SIMD share it)
     const double cpi_simd = blocks == 1 ? cyc_in_kernel / wave_instr
                                         : (ms / 1e3) * ghz * 1e9 / (wave_instr * waves_per_simd);
+    char mode[16];
+    if (blocks == 1) snprintf(mode, sizeof mode, "lone");
+    else snprintf(mode, sizeof mode, "%s%g", threads == 1024 ? "sync_w" : "w", waves_per_simd);
     printf("{\\"test\\": \\"%s\\", \\"mode\\": \\"%s\\", \\"cycles_per_instr\\": %.3f, \\"Tops\\": %.2f, \\"ms\\": %.3f, \\"clock_GHz\\": %.3f}\\n",
-           name, blocks == 1 ? "lone" : (blocks == 512 ? "w2" : blocks == 1024 ? "w4" : "w8"), cpi_simd,
+           name, mode, cpi_simd,
            blocks == 1 ? 0.0 : wave_instr * waves * 64 / (ms / 1e3) / 1e12, ms, ghz);
     CHECK(hipFree(out)); CHECK(hipFree(clk));
 }
@@ -171,11 +230,21 @@ int main() {
         for w in (2, 4, 8):
             out.append(f"    run(\"{name}\", k_{name}, {n}, {256 * w}, 256, {it});")
         out.append(f"    run(\"{name}\", k_{name}, {n}, 1, 64, {it // 4});")
+    for name, n in sync_names:
+        it = max(100, 256000 // n)
+        for w in (4, 8):
+            out.append(f"    run(\"{name}\", k_{name.replace('|', '_')}, {n}, {256 * w // 4}, 1024, {it});")
     out.append("    return 0;\n}")
     return "\n".join(out) + "\n"
 
 
+ONLY = ""
+
+
 def main():
+    global ONLY
+    if len(sys.argv) > 1 and sys.argv[1] == "--only-sync":
+        ONLY = "sync"
     src = os.path.join(HERE, "isa_rates.hip")
     with open(src, "w") as f:
         f.write(gen())
