@@ -5,8 +5,9 @@ BASELINE.json configs[3]) on N MI355X, subtree-sharded.
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 One step = one complete Merkleization of the whole tree (every rank reduces
-its shard, one 32-B-per-rank RCCL all-gather, rank 0 finishes the top levels
-and the length mix-in).  Inputs are generated on the device before timing and
+its shard to the level 10 below its shard root (1024 nodes, the "frontier"),
+one 32-KB-per-rank RCCL all-gather, rank 0 finishes the top levels and the
+length mix-in on a side stream that overlaps its next step).  Inputs are generated on the device before timing and
 stay resident in HBM.  Total work is fixed as N grows ("strong" scaling);
 value = 2^log2n leaves x K / max-over-ranks wall time.  Rank 0 prints one
 JSON line; progress goes to stderr.
@@ -76,6 +77,9 @@ def main():
                     help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N ranks on one GPU)")
     ap.add_argument("--share-device", action="store_true",
                     help="all ranks on cuda:0 (rehearsal of the N-rank path on a one-GPU box, with --backend gloo)")
+    ap.add_argument("--frontier", type=int, default=10,
+                    help="N>1: each rank gathers its tree level this many levels below its shard root "
+                         "(2^k nodes) and rank 0 finishes the top (0 = gather the 32-B shard roots)")
     ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5"],
                     help="BASELINE.json config: c4 = headline (default); c2/c3/c5 = single-GPU side benches")
     args = ap.parse_args()
@@ -116,13 +120,19 @@ def main():
         D.synth_fill(items[:nbytes], SEED, word0=lo * item_len // 8)
     ws = D.subtree_workspace(local_n, item_len, dev) if sp.nonempty > 1 else D.merkle_workspace(n, item_len, dev)
     root_buf = torch.empty(32, dtype=torch.uint8, device=dev)
-    gather_buf = torch.empty(world * 32, dtype=torch.uint8, device=dev)
+    # frontier: the narrowest (latency-bound) k levels of every shard move to
+    # rank 0's finisher, which overlaps its next step (parallel.py)
+    k = args.frontier if sp.nonempty > 1 and 0 < args.frontier < sp.height - 4 else 0
+    block = 32 << k
+    frontier_buf = torch.empty(block, dtype=torch.uint8, device=dev)
+    gather_buf = torch.empty(world * block, dtype=torch.uint8, device=dev)
     finish_out = torch.empty(32, dtype=torch.uint8, device=dev)
+    finish_ws = D.finish_workspace(world << k, dev) if k and rank == 0 else None
     # rank 0 finishes the top levels on a side stream, overlapping its next step
     finish_stream = torch.cuda.Stream(device=dev) if world > 1 and rank == 0 else None
     torch.cuda.synchronize()
     log(f"rank {rank}/{world}: {local_n} items ({nbytes / 2**30:.2f} GiB), shard height {sp.height}, "
-        f"nonempty {sp.nonempty}")
+        f"nonempty {sp.nonempty}, frontier {k}")
 
     def step():
         return P.sharded_merkle_hash(
@@ -130,7 +140,10 @@ def main():
             subtree_fn=lambda it, sn, il, h, pad: D.merkle_subtree(it, sn, il, h, pad, out=root_buf, ws=ws),
             full_fn=lambda it, nn, il: D.merkle_hash(it, nn, il, out=root_buf, ws=ws),
             finish_fn=lambda g, nr, nt: D.merkle_finish(g, nr, nt, out=finish_out),
-            gather_buf=gather_buf, finish_stream=finish_stream)
+            gather_buf=gather_buf, finish_stream=finish_stream, frontier_log2=k,
+            frontier_fn=lambda it, sn, il, h, kk, pad: D.merkle_subtree_frontier(it, sn, il, h, kk, pad,
+                                                                                 out=frontier_buf, ws=ws),
+            finish_nodes_fn=lambda g, c, nt: D.merkle_finish_nodes(g, c, nt, out=finish_out, ws=finish_ws))
 
     for i in range(args.warmup):
         step()
@@ -187,7 +200,7 @@ def main():
             "config": {"workload": f"C4: ssz.merkleHash of 2^{args.log2n} x {item_len}-B items "
                                    f"({n * item_len / 2**30:.0f} GiB), subtree-sharded",
                        "n_items": n, "item_len": item_len, "parallelism": f"subtree{world}",
-                       "shard_height": sp.height, "root": root_hex},
+                       "shard_height": sp.height, "frontier_log2": k, "root": root_hex},
             "roofline": {
                 "bound": "valu-int",
                 "kernel": "k_reduce<LEAF, FAST, 2> (leaf pass: 256-B windows + 4 fused levels)",

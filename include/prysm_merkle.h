@@ -91,6 +91,23 @@ int mk_ssz_merkle_shard_plan(uint64_t n, uint32_t item_len, uint32_t nshards, ui
 int mk_dev_ssz_merkle_subtree(const void* d_shard_items, uint64_t shard_n, uint32_t item_len,
                               uint32_t height, int pad_at_one, void* d_out32, void* d_ws,
                               uint64_t ws_bytes, void* stream);
+/* Frontier variant: stop `frontier_log2` levels below the shard root and
+ * write the shard's nodes at height (height - frontier_log2) to d_out (32 B
+ * each, 2^frontier_log2 of them, fewer for a ragged last shard; *nodes_out
+ * gets the count).  The shards' frontiers, concatenated in shard order, are
+ * that level of the whole tree, so ranks gather a few KB each and the top
+ * levels move to the finisher (mk_dev_ssz_merkle_finish_nodes), which can
+ * overlap the ranks' next Merkleization.  0 < frontier_log2 < height. */
+int mk_dev_ssz_merkle_subtree_frontier(const void* d_shard_items, uint64_t shard_n, uint32_t item_len,
+                                       uint32_t height, uint32_t frontier_log2, int pad_at_one, void* d_out,
+                                       uint64_t* nodes_out, void* d_ws, uint64_t ws_bytes, void* stream);
+/* Finisher over `count` nodes forming one complete tree level in order (the
+ * gathered frontiers): the reference level loop (odd -> 0^128 pad) and
+ * Keccak(root || le64(n_total) || 0^24).  Workspace from
+ * mk_ssz_merkle_finish_workspace_bytes(count). */
+uint64_t mk_ssz_merkle_finish_workspace_bytes(uint64_t count);
+int mk_dev_ssz_merkle_finish_nodes(const void* d_nodes, uint64_t count, uint64_t n_total, void* d_out32,
+                                   void* d_ws, uint64_t ws_bytes, void* stream);
 /* Finisher on one device: the reference level loop over the `nroots`
  * gathered shard roots (odd -> 0^128 pad), then Keccak(root || le64(n) || 0^24). */
 int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32,

@@ -52,6 +52,9 @@ _SIGS = {
     "mk_ssz_merkle_shard_plan": (_int, [_u64, _u32, _u32, _vp, _vp, _vp]),
     "mk_dev_ssz_merkle_subtree": (_int, [_vp, _u64, _u32, _u32, _int, _vp, _vp, _u64, _vp]),
     "mk_dev_ssz_merkle_finish": (_int, [_vp, _u64, _u64, _vp, _vp]),
+    "mk_dev_ssz_merkle_subtree_frontier": (_int, [_vp, _u64, _u32, _u32, _u32, _int, _vp, _vp, _vp, _u64, _vp]),
+    "mk_ssz_merkle_finish_workspace_bytes": (_u64, [_u64]),
+    "mk_dev_ssz_merkle_finish_nodes": (_int, [_vp, _u64, _u64, _vp, _vp, _u64, _vp]),
     "mk_ssz_merkle_hash_multi": (_int, [_vp, _u64, _u32, _int, _vp]),
     "mk_ssz_struct_msg_len": (_u64, [_vp, _u32]),
     "mk_ssz_struct_roots": (_int, [_vp, _u64, _u32, _vp, _u32, _vp]),

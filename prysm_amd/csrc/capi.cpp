@@ -198,6 +198,7 @@ struct Plan {
     std::vector<Pass> passes;
     uint64_t slot_nodes[2] = {0, 0};
     uint64_t total = 0, n = 0;
+    uint64_t out_nodes = 1;  // nodes written to the output (frontier mode: > 1)
 };
 
 // Hashing levels from `count` nodes down to one (reference loop length).
@@ -214,13 +215,19 @@ uint32_t levels_to_one(uint64_t count) {
 // mix-in; subtree=true: exactly `height` levels above the chunks, output one
 // node (pad_at_one keeps the odd rule alive at count 1).
 // node_input: the input is n 32-B nodes reduced pairwise (a plain binary
-// tree, no chunking; hashutil.MerkleRoot's heap bands), subtree must be set.
+// tree, no chunking; hashutil.MerkleRoot's heap bands, or a gathered tree
+// level for the multi-GPU finisher).  Without subtree mode the final pass
+// mixes in `mixin_n` (the item count of the whole tree), n must be >= 2.
+// frontier (subtree mode): stop `frontier` levels below the subtree root and
+// write the level there (2^frontier nodes, fewer for a ragged shard).
 int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool pad_at_one,
-              bool aligned16, Plan& p, bool node_input = false) {
+              bool aligned16, Plan& p, bool node_input = false, uint32_t frontier = 0, uint64_t mixin_n = 0) {
     p = Plan();
     p.n = n;
     if (n > 0 && item_len == 0) return fail(MK_EINVAL, "item_len == 0 (reference: integer divide by zero)");
-    if (node_input && (!subtree || item_len != 32)) return fail(MK_EINVAL, "planner: node input needs subtree mode");
+    if (node_input && item_len != 32) return fail(MK_EINVAL, "planner: node input is 32-B nodes");
+    if (node_input && !subtree && n < 2) return fail(MK_EINVAL, "planner: node finisher needs >= 2 nodes");
+    if (frontier && (!subtree || frontier >= height)) return fail(MK_EINVAL, "planner: bad frontier %u", frontier);
     const uint64_t total = n * (uint64_t)item_len;
     const uint64_t cb = node_input ? 32 : n ? chunk_bytes(item_len) : 128;
     const uint64_t nchunks = node_input ? n : n ? ceil_div(total, cb) : 0;
@@ -232,7 +239,11 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
     if (subtree && (height == 0 || nchunks == 0 || nchunks > (1ull << height)))
         return fail(MK_EINVAL, "subtree: bad height %u for %llu chunks", height, (unsigned long long)nchunks);
 
-    uint32_t remaining = subtree ? height : levels_to_one(nchunks);
+    uint32_t remaining = subtree ? height - frontier : levels_to_one(nchunks);
+    if (frontier) {  // nodes at the frontier level (the odd rule keeps >= 1 with pad_at_one)
+        const uint64_t span = 1ull << (height - frontier);
+        p.out_nodes = std::max<uint64_t>(1, ceil_div(nchunks, span));
+    }
     bool leaf = !node_input;
     uint64_t cin = nchunks;  // leaf: chunks; node: input nodes
     int slot = 0;
@@ -244,7 +255,7 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         const uint64_t c1 = (cin > 1 || pad_at_one) ? ceil_div(cin, 2) : 1;
         a.c1 = c1;
         a.pad_at_one = pad_at_one ? 1 : 0;
-        a.n_items = n;
+        a.n_items = (node_input && !subtree) ? mixin_n : n;
         if (leaf) {
             a.total = total;
             a.cb = cb;
@@ -310,6 +321,12 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
             } else if (!wave && c1 > span / 2 && lv < 2) {
                 return fail(MK_EINVAL, "planner: unsupported single-level pass");
             }
+            ps.out_ws = -1;
+            ps.a.out_ilv = 0;
+            p.passes.push_back(ps);
+            break;
+        }
+        if (frontier && remaining == lv) {  // the frontier level: plain nodes to the output
             ps.out_ws = -1;
             ps.a.out_ilv = 0;
             p.passes.push_back(ps);
@@ -623,6 +640,36 @@ int mk_dev_ssz_merkle_subtree(const void* d_shard_items, uint64_t shard_n, uint3
                        (hipStream_t)stream);
 }
 
+int mk_dev_ssz_merkle_subtree_frontier(const void* d_shard_items, uint64_t shard_n, uint32_t item_len,
+                                       uint32_t height, uint32_t frontier_log2, int pad_at_one, void* d_out,
+                                       uint64_t* nodes_out, void* d_ws, uint64_t ws_bytes, void* stream) {
+    TRY(bind(-1));
+    if (!d_out || (shard_n && !d_shard_items)) return fail(MK_EINVAL, "null pointer");
+    Plan p;
+    TRY(make_plan(shard_n, item_len, true, height, pad_at_one != 0, ((uintptr_t)d_shard_items % 16) == 0, p, false,
+                  frontier_log2));
+    if (nodes_out) *nodes_out = p.out_nodes;
+    return launch_plan(p, (const uint8_t*)d_shard_items, (uint8_t*)d_out, (uint8_t*)d_ws, ws_bytes,
+                       (hipStream_t)stream);
+}
+
+uint64_t mk_ssz_merkle_finish_workspace_bytes(uint64_t count) {
+    Plan p;
+    if (count <= 2 * mk::kWave2Span) return 256;
+    if (make_plan(count, 32, false, 0, false, true, p, true, 0, 1) != MK_OK) return 0;
+    return plan_ws_bytes(p);
+}
+
+int mk_dev_ssz_merkle_finish_nodes(const void* d_nodes, uint64_t count, uint64_t n_total, void* d_out32,
+                                   void* d_ws, uint64_t ws_bytes, void* stream) {
+    if (count <= 2 * mk::kWave2Span) return mk_dev_ssz_merkle_finish(d_nodes, count, n_total, d_out32, stream);
+    TRY(bind(-1));
+    if (!d_nodes || !d_out32) return fail(MK_EINVAL, "null pointer");
+    Plan p;
+    TRY(make_plan(count, 32, false, 0, false, ((uintptr_t)d_nodes % 16) == 0, p, true, 0, n_total));
+    return launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, (hipStream_t)stream);
+}
+
 int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32, void* stream) {
     TRY(bind(-1));
     if (nroots == 0 || nroots > 2 * mk::kWave2Span)
@@ -672,39 +719,51 @@ int mk_ssz_merkle_hash_multi(const uint8_t* items, uint64_t n, uint32_t item_len
         ctx[d] = g_ctx[d];
         locks.emplace_back(ctx[d]->mu);
     }
-    // per device: shard upload + subtree reduce into roots slot `d`
+    // per device: shard upload + reduce to the shard's frontier level (2^k
+    // nodes, k levels below the shard root) into block `d` of the level buffer
+    const uint32_t k = h > 5 ? std::min<uint32_t>(10, h - 5) : 0;
+    const size_t block = (size_t)32 << k;
+    uint64_t last_nodes = 1;
     for (int d = 0; d < ndev; ++d) {
         TRY(bind(d));
         DevCtx* c = ctx[d];
         const uint64_t sn = begin[d + 1] - begin[d];
         const size_t inb = sn * (size_t)item_len;
         TRY(grow(c->in, inb));
-        TRY(grow(c->out, 32 * (size_t)ndev + 32));
-        uint8_t* roots = (uint8_t*)c->out.p;
+        TRY(grow(c->out, block * ndev + 32));
+        uint8_t* lvl = (uint8_t*)c->out.p;
         if (sn) {
             Plan p;
-            TRY(make_plan(sn, item_len, true, h, true, true, p));
+            TRY(make_plan(sn, item_len, true, h, true, true, p, false, k));
+            if (d == (int)ne - 1) last_nodes = p.out_nodes;
             TRY(grow(c->ws, plan_ws_bytes(p)));
             HIPCHK(hipMemcpyAsync(c->in.p, items + begin[d] * item_len, inb, hipMemcpyHostToDevice, c->stream));
-            TRY(launch_plan(p, (const uint8_t*)c->in.p, roots + 32 * d, (uint8_t*)c->ws.p, c->ws.cap, c->stream));
+            TRY(launch_plan(p, (const uint8_t*)c->in.p, lvl + block * d, (uint8_t*)c->ws.p, c->ws.cap, c->stream));
         } else {
-            HIPCHK(hipMemsetAsync(roots + 32 * d, 0, 32, c->stream));
+            HIPCHK(hipMemsetAsync(lvl + block * d, 0, block, c->stream));
         }
     }
-    // gather the 32-B shard roots over RCCL (in place: slot d of every device)
+    // gather the frontier blocks over RCCL (in place: block d of every device)
     if (ncclGroupStart() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupStart");
     for (int d = 0; d < ndev; ++d) {
-        uint8_t* roots = (uint8_t*)ctx[d]->out.p;
-        if (ncclAllGather(roots + 32 * d, roots, 32, ncclUint8, comms[d], ctx[d]->stream) != ncclSuccess) {
+        uint8_t* lvl = (uint8_t*)ctx[d]->out.p;
+        if (ncclAllGather(lvl + block * d, lvl, block, ncclUint8, comms[d], ctx[d]->stream) != ncclSuccess) {
             ncclGroupEnd();
             return fail(MK_ECOMM, "ncclAllGather on device %d", d);
         }
     }
     if (ncclGroupEnd() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupEnd");
     TRY(bind(0));
-    uint8_t* roots0 = (uint8_t*)ctx[0]->out.p;
-    TRY(mk_dev_ssz_merkle_finish(roots0, ne, n, roots0 + 32 * ndev, ctx[0]->stream));
-    HIPCHK(hipMemcpyAsync(out, roots0 + 32 * ndev, 32, hipMemcpyDeviceToHost, ctx[0]->stream));
+    uint8_t* lvl0 = (uint8_t*)ctx[0]->out.p;
+    const uint64_t count = ((uint64_t)(ne - 1) << k) + last_nodes;
+    if (k) {
+        TRY(grow(ctx[0]->ws, mk_ssz_merkle_finish_workspace_bytes(count)));
+        TRY(mk_dev_ssz_merkle_finish_nodes(lvl0, count, n, lvl0 + block * ndev, ctx[0]->ws.p, ctx[0]->ws.cap,
+                                           ctx[0]->stream));
+    } else {
+        TRY(mk_dev_ssz_merkle_finish(lvl0, ne, n, lvl0 + block * ndev, ctx[0]->stream));
+    }
+    HIPCHK(hipMemcpyAsync(out, lvl0 + block * ndev, 32, hipMemcpyDeviceToHost, ctx[0]->stream));
     for (int d = 0; d < ndev; ++d) {
         TRY(bind(d));
         HIPCHK(hipStreamSynchronize(ctx[d]->stream));

@@ -88,6 +88,47 @@ def merkle_subtree(items: torch.Tensor, shard_n: int, item_len: int, height: int
     return out
 
 
+def merkle_subtree_frontier(items: torch.Tensor, shard_n: int, item_len: int, height: int, frontier_log2: int,
+                            pad_at_one: bool, out: torch.Tensor = None, ws: torch.Tensor = None) -> torch.Tensor:
+    """The shard's tree level `frontier_log2` levels below its root: a
+    (nodes*32,) uint8 device tensor (nodes = parallel.frontier_count(...))."""
+    _bind(items)
+    from .parallel import frontier_count
+
+    nodes = frontier_count(shard_n, item_len, height, frontier_log2)
+    if out is None:
+        out = torch.empty(32 << frontier_log2, dtype=torch.uint8, device=items.device)
+    if out.numel() < 32 * nodes:
+        raise ValueError("frontier output buffer too small")
+    if ws is None:
+        ws = subtree_workspace(shard_n, item_len, items.device)
+    got = ctypes.c_uint64()
+    _lib.check(_lib.load().mk_dev_ssz_merkle_subtree_frontier(
+        _p(items), shard_n, item_len, height, frontier_log2, int(pad_at_one), _p(out), ctypes.byref(got), _p(ws),
+        ws.numel(), _stream(items.device)), "mk_dev_ssz_merkle_subtree_frontier")
+    assert got.value == nodes, (got.value, nodes)
+    return out[:32 * nodes]
+
+
+def finish_workspace(count: int, device) -> torch.Tensor:
+    return torch.empty(max(256, _lib.load().mk_ssz_merkle_finish_workspace_bytes(count)), dtype=torch.uint8,
+                       device=device)
+
+
+def merkle_finish_nodes(nodes: torch.Tensor, count: int, n_total: int, out: torch.Tensor = None,
+                        ws: torch.Tensor = None) -> torch.Tensor:
+    """Reference level loop over one gathered tree level of `count` nodes +
+    length mix-in (the finisher of the frontier sharding)."""
+    _bind(nodes)
+    if out is None:
+        out = torch.empty(32, dtype=torch.uint8, device=nodes.device)
+    if ws is None:
+        ws = finish_workspace(count, nodes.device)
+    _lib.check(_lib.load().mk_dev_ssz_merkle_finish_nodes(_p(nodes), count, n_total, _p(out), _p(ws), ws.numel(),
+                                                          _stream(nodes.device)), "mk_dev_ssz_merkle_finish_nodes")
+    return out
+
+
 def merkle_finish(roots: torch.Tensor, nroots: int, n_total: int, out: torch.Tensor = None) -> torch.Tensor:
     """Reference level loop over gathered shard roots + length mix-in."""
     _bind(roots)

@@ -36,7 +36,7 @@ def _plan_cpu(n, item_len, world):
     return h, ne, [min(n, s * (1 << h) * per) for s in range(world + 1)]
 
 
-def _worker(rank, world, port, n, item_len, q):
+def _worker(rank, world, port, n, item_len, q, frontier=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -68,8 +68,18 @@ def _worker(rank, world, port, n, item_len, q):
             lenc = nt.to_bytes(8, "little") + bytes(24)
             return torch.frombuffer(bytearray(O.keccak256(chunks[0] + lenc)), dtype=torch.uint8)
 
+        def frontier_fn(items, sn, il, h, k, pad):
+            # the shard's level k below its root = the roots of its 2^k sub-shards
+            cnt = P.frontier_count(sn, il, h, k)
+            nodes = b"".join(O.merkle_subtree_gen(n, il, SEED, (rank << k) + j, h - k) for j in range(cnt))
+            return torch.frombuffer(bytearray(nodes), dtype=torch.uint8)
+
+        def finish_nodes(g, count, nt):
+            return finish(g, count, nt)
+
         root = P.sharded_merkle_hash(local, n, item_len, sp, rank, world, subtree_fn=subtree, full_fn=full_fn,
-                                     finish_fn=finish)
+                                     finish_fn=finish, frontier_log2=frontier, frontier_fn=frontier_fn,
+                                     finish_nodes_fn=finish_nodes)
         if rank == 0:
             q.put(bytes(root.numpy()))
     finally:
@@ -84,6 +94,26 @@ def test_sharded_root_equals_full_root(world, n):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, n, 32, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    root = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert root == O.merkle_hash_gen(n, 32, SEED)
+
+
+@pytest.mark.parametrize("world,n,k", [(2, 1 << 14, 3), (2, 4 * 1000 + 3, 2), (4, 4 * 1000 + 3, 4), (4, 1 << 12, 5),
+                                       (4, 4 * 37, 1)])
+def test_frontier_sharded_root_equals_full_root(world, n, k):
+    """Frontier mode: ranks gather their 2^k-node level, rank 0 finishes the
+    k + log2(world) top levels (ragged last shards included)."""
+    from oracle import oracle as O
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, 32, q, k)) for r in range(world)]
     for p in procs:
         p.start()
     root = q.get(timeout=120)

@@ -184,6 +184,65 @@ def test_subtree_sharding_equals_full(gpu, n, world):
     assert bytes(full.cpu().numpy()) == want
 
 
+@pytest.mark.parametrize("n,world,k", [(1 << 16, 8, 4), ((1 << 16) + 12, 8, 5), (999_999, 3, 8), (4099, 8, 3),
+                                       (1 << 20, 8, 8), (1 << 22, 4, 10), (41 * 4 + 3, 4, 1)])
+def test_frontier_sharding_equals_full(gpu, n, world, k):
+    """Each shard's level k below its root equals the oracle's sub-shard
+    roots; the concatenated frontiers finish to the full merkleHash root."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+    from prysm_amd import parallel as P
+
+    item_len = 32
+    h, ne, begin = D.shard_plan(n, item_len, world)
+    assert ne > 1 and 0 < k < h
+    items = torch.empty(n * item_len, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 33)
+    level = torch.zeros(world << (k + 5), dtype=torch.uint8, device=gpu)
+    counts = []
+    for s in range(ne):
+        sn = begin[s + 1] - begin[s]
+        nodes = D.merkle_subtree_frontier(items[begin[s] * item_len:begin[s + 1] * item_len], sn, item_len, h, k,
+                                          True, out=level[(s << (k + 5)):((s + 1) << (k + 5))])
+        counts.append(nodes.numel() // 32)
+    count = ((ne - 1) << k) + counts[-1]
+    root = D.merkle_finish_nodes(level, count, n)
+    torch.cuda.synchronize()
+    got = level.cpu().numpy()
+    for s in range(ne):
+        for j in (0, counts[s] - 1):  # first and last node of every frontier
+            want = O.merkle_subtree_gen(n, item_len, SEED + 33, (s << k) + j, h - k, nthreads=16)
+            off = ((s << k) + j) * 32
+            assert bytes(got[off:off + 32]) == want, (s, j)
+    assert bytes(root.cpu().numpy()) == O.merkle_hash_gen(n, item_len, SEED + 33, nthreads=16)
+
+
+@pytest.mark.parametrize("count", [2, 3, 64, 65, 127, 1000, 2048, 2049, 5001])
+def test_finish_nodes_vs_reference_loop(gpu, count):
+    """The finisher over one gathered tree level: reference level loop with
+    the 128-B odd pad, then the length mix-in (hash.go:225-237)."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    nodes = torch.empty(count * 32, dtype=torch.uint8, device=gpu)
+    D.synth_fill(nodes, SEED + 34 + count)
+    n_total = 123_456_789 + count
+    got = D.merkle_finish_nodes(nodes, count, n_total)
+    torch.cuda.synchronize()
+    host = nodes.cpu().numpy()
+    level = [bytes(host[32 * i:32 * i + 32]) for i in range(count)]
+    while len(level) > 1:
+        if len(level) % 2:
+            level.append(bytes(128))
+        level = [O.keccak256(level[i] + level[i + 1]) for i in range(0, len(level), 2)]
+    want = O.keccak256(level[0] + n_total.to_bytes(8, "little") + bytes(24))
+    assert bytes(got.cpu().numpy()) == want
+
+
 def test_multi_device_entry_single_gpu(gpu):
     """mk_ssz_merkle_hash_multi with ndev=1 is the plain path."""
     import ctypes
