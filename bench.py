@@ -80,8 +80,8 @@ def main():
     ap.add_argument("--frontier", type=int, default=10,
                     help="N>1: each rank gathers its tree level this many levels below its shard root "
                          "(2^k nodes) and rank 0 finishes the top (0 = gather the 32-B shard roots)")
-    ap.add_argument("--config", default="c4", choices=["c2", "c3", "c4", "c5"],
-                    help="BASELINE.json config: c4 = headline (default); c2/c3/c5 = single-GPU side benches")
+    ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c5"],
+                    help="BASELINE.json config: c4 = headline (default); c1/c2/c3/c5 = single-GPU side benches")
     args = ap.parse_args()
     if args.config != "c4":
         from tools.bench_configs import run_config

@@ -64,6 +64,9 @@ __global__ void k_keccak_fixed(const uint8_t* in, uint64_t n, uint32_t msg_len, 
 __global__ void k_keccak_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint4* out);
 __global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
 __global__ void k_keccak_words(const uint2* in, uint64_t n, uint32_t nwords, uint4* out);
+template <int NW>
+__global__ void k_keccak_rec(const uint2* in, uint64_t n, uint4* out);
+constexpr uint32_t kRecGridMax = 256 * 4;  // k_keccak_rec: one resident workgroup set, grid-stride
 __global__ void k_trie_reduce(const uint4* in, uint64_t cin, uint4* lv_out, uint32_t levels);
 __global__ void k_trie_top2(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels);
 template <uint32_t NT>

@@ -1,9 +1,11 @@
 """Single-GPU side benchmarks for the other BASELINE.json configs
-(bench.py --config c2|c3|c5).  Same JSON shape as the headline line; inputs
+(bench.py --config c1|c2|c3|c5).  Same JSON shape as the headline line; inputs
 resident in HBM before timing; hipEvent-free wall timing bracketed by
 torch.cuda.synchronize(); the dominant kernel is timed with the library's
 own hipEvents where the library exposes them (merkle passes).
 
+  c1: ssz.TreeHash of 16,384 synthetic ValidatorRecords from host buffers
+      (typed Hashable path; the reflective mirror timed beside it)
   c2: hashutil.Hash over 2^24 x 64-B messages (one Keccak-f each)
   c3: TreeHash of a synthetic 1,000,000-validator State{registry, balances}
       via the typed Hashable path (struct kernels + merkleHash)
@@ -63,6 +65,44 @@ def run_config(args):
     st = lambda: ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)  # noqa: E731
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     seed = 0x5EED000000000000
+
+    if args.config == "c1":
+        # ssz.TreeHash([]*ValidatorRecord) of 16,384 synthetic validators, the
+        # reference's `go test -bench` shape: host records in, 32-B root out.
+        # value: the typed Hashable path (one library call: H2D, struct
+        # kernel, merkleHash, D2H); the reflective mirror (makeSliceHasher ->
+        # makeStructHasher per element, batched digests) is reported beside it.
+        from prysm_amd import registry as R
+        from prysm_amd import ssz as S
+
+        n = 16_384
+        reg = R.synthetic_registry(n, seed + 1)
+        typ = S.Slice(S.Ptr(R.VALIDATOR_SSZ))
+        vals = reg.as_dicts()
+        want = reg.tree_hash_ssz()
+        assert S.tree_hash(vals, typ) == want, "c1: reflective and typed roots differ"
+        sec = _timeit(reg.tree_hash_ssz, args.steps, args.warmup)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            S.tree_hash(vals, typ)
+        refl = (time.perf_counter() - t0) / 3
+        perms = 5 * n + (n / 4 / 2) * 2 + n / 8 + 1
+        cpu = None
+        if not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            raw = reg.records.view(np.uint8).reshape(-1)
+            t0 = time.perf_counter()
+            for _ in range(10):
+                rr = O.struct_roots(raw, n, 160, R.VALIDATOR_FIELDS, nthreads=1)
+                O.merkle_hash_flat(rr.reshape(-1), n, 32)
+            dt = (time.perf_counter() - t0) / 10
+            cpu = {"value": n / dt, "unit": "validators/s", "cores": 1, "kind": "port",
+                   "sample": f"oracle struct_roots + merkleHash, the same 16,384 validators, 1 thread, {dt * 1e3:.1f} ms"}
+        _line("ssz.TreeHash of a 16,384-entry []ValidatorRecord (host buffers)", n / sec, "validators/s", args, sec,
+              perms, {"workload": "C1: TreeHash([]*ValidatorRecord), 16,384 synthetic validators, host records",
+                      "n": n, "root": want.hex(), "reflective_mirror_ms": refl * 1e3}, cpu)
+        return
 
     if args.config == "c2":
         n = 1 << 24

@@ -10,7 +10,7 @@ import os
 import sys
 from collections import defaultdict
 
-LEAF = "k_reduce<true, true, 2>"
+LEAF = os.environ.get("KERNEL", "k_reduce<true, true, 2>")
 
 
 def counters(d):
@@ -38,6 +38,13 @@ def main(d):
                     agg[c] = sum(vals) / len(vals)
                     agg[c + "_dispatches"] = len(vals)
     res["leaf_counters_per_dispatch"] = agg
+    if os.environ.get("ALL"):  # every kernel's counters, averaged per dispatch
+        allk = defaultdict(dict)
+        for sub in ("fetch", "write", "sq", "lds"):
+            for k, cs in counters(os.path.join(d, sub)).items():
+                for c, vals in cs.items():
+                    allk[k[:60]][c] = sum(vals) / len(vals)
+        res["per_kernel"] = allk
     if "FETCH_SIZE" in agg:
         fetch = agg["FETCH_SIZE"] * 1024 * 2  # KiB -> B, x2 gfx950 correction
         write = agg.get("WRITE_SIZE", 0.0) * 1024
