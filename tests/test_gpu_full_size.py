@@ -1,0 +1,109 @@
+"""Device path at the BASELINE.json full sizes against the CPU oracle's
+results (tests/golden/full_size_roots.json, tests/golden/make_full_size.py):
+the same seeded synthetic inputs bench.py measures, checked bit-exactly.
+
+  c2  2^24 x 64-B Hash           (Keccak-256 of the 2^24 digests)
+  c3  1,000,000-validator State  (registry root, balances root, state root)
+  c4  2^28 x 32-B merkleHash     (8 GiB on the device), unsharded and as
+      8 frontier shards finished on one device
+  c5  2^20-deposit trie root
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = json.load(open(os.path.join(HERE, "golden", "full_size_roots.json")))
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+@pytest.mark.gpu
+def test_c4_full_2p28(gpu):
+    import torch
+
+    from prysm_amd import device as D
+    from prysm_amd import parallel as P
+
+    g = GOLD["c4"]
+    n, il = g["n"], g["item_len"]
+    items = torch.empty(n * il, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, g["seed"])
+    root = D.merkle_hash(items, n, il)
+    torch.cuda.synchronize()
+    assert bytes(root.cpu().numpy()).hex() == g["root"]
+    # the 8-GPU decomposition on one device: frontier k=10 per shard, finisher
+    world, k = 8, 10
+    h, ne, begin = D.shard_plan(n, il, world)
+    level = torch.empty(world << (k + 5), dtype=torch.uint8, device=gpu)
+    ws = D.subtree_workspace(begin[1] - begin[0], il, gpu)
+    for s in range(ne):
+        sn = begin[s + 1] - begin[s]
+        D.merkle_subtree_frontier(items[begin[s] * il:begin[s + 1] * il], sn, il, h, k, True,
+                                  out=level[s << (k + 5):(s + 1) << (k + 5)], ws=ws)
+    count = ((ne - 1) << k) + P.frontier_count(begin[ne] - begin[ne - 1], il, h, k)
+    root2 = D.merkle_finish_nodes(level, count, n)
+    torch.cuda.synchronize()
+    assert bytes(root2.cpu().numpy()).hex() == g["root"]
+    del items
+
+
+@pytest.mark.gpu
+def test_c2_full_2p24(gpu):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    g = GOLD["c2"]
+    n, ln = g["n"], g["msg_len"]
+    msgs = torch.empty(n * ln, dtype=torch.uint8, device=gpu)
+    D.synth_fill(msgs, g["seed"])
+    out = D.hash_batch(msgs, n, ln)
+    torch.cuda.synchronize()
+    assert O.keccak256(out.cpu().numpy().tobytes()).hex() == g["digest_of_digests"]
+
+
+@pytest.mark.gpu
+def test_c3_full_1m_validators(gpu):
+    from prysm_amd import registry as R
+    from prysm_amd import ssz as S
+
+    g = GOLD["c3"]
+    reg = R.synthetic_registry(g["n"], g["seed"])
+    bal = R.synthetic_balances(g["n"], g["seed"])
+    assert reg.tree_hash_ssz().hex() == g["registry_root"]
+    assert S.merkle_hash_flat(bal.view(np.uint8), len(bal), 8).hex() == g["balances_root"]
+    assert R.state_root(reg, bal).hex() == g["state_root"]
+
+
+@pytest.mark.gpu
+def test_c5_full_2p20_deposits(gpu):
+    import ctypes
+
+    import torch
+
+    from prysm_amd import _lib
+    from prysm_amd import device as D
+
+    g = GOLD["c5"]
+    n, dl, depth = g["n"], g["deposit_len"], g["depth"]
+    data = torch.empty(n * dl, dtype=torch.uint8, device=gpu)
+    D.synth_fill(data, g["seed"])
+    L = _lib.load()
+    lv = torch.empty(L.mk_deposit_trie_levels_bytes(n, depth), dtype=torch.uint8, device=gpu)
+    root = torch.empty(32, dtype=torch.uint8, device=gpu)
+    st = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
+    _lib.check(L.mk_dev_deposit_trie_build(ctypes.c_void_p(data.data_ptr()), None, n, dl, depth,
+                                           ctypes.c_void_p(lv.data_ptr()), ctypes.c_void_p(root.data_ptr()), st),
+               "mk_dev_deposit_trie_build")
+    torch.cuda.synchronize()
+    assert bytes(root.cpu().numpy()).hex() == g["root"]
