@@ -66,7 +66,10 @@ __global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
 __global__ void k_keccak_words(const uint2* in, uint64_t n, uint32_t nwords, uint4* out);
 template <int NW>
 __global__ void k_keccak_rec(const uint2* in, uint64_t n, uint4* out);
-constexpr uint32_t kRecGridMax = 256 * 4;  // k_keccak_rec: one resident workgroup set, grid-stride
+#ifndef MK_REC_GRID
+#define MK_REC_GRID 4096
+#endif
+constexpr uint32_t kRecGridMax = MK_REC_GRID;  // k_keccak_rec grid cap (A/B at 2^20: 512..4096 WGs, 4096 best)
 __global__ void k_trie_reduce(const uint4* in, uint64_t cin, uint4* lv_out, uint32_t levels);
 __global__ void k_trie_top2(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels);
 template <uint32_t NT>
