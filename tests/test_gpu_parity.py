@@ -44,14 +44,14 @@ def test_hash_batch_fixed(gpu, msg_len):
 
 def test_dev_hash_batch_280_grid_stride(gpu):
     """280-B deposit messages take the grid-stride k_keccak_rec<35>: more
-    records than resident threads (1024 x 256), odd count, so threads hash
-    2-3 records and prefetch across record boundaries."""
+    records than the grid's threads (cap 4096 x 256), odd count, so threads
+    hash 2-3 records and prefetch across record boundaries."""
     import torch
 
     from oracle import oracle as O
     from prysm_amd import device as D
 
-    n, ln = 2 * 1024 * 256 + 12_345, 280
+    n, ln = 2 * 4096 * 256 + 12_345, 280
     msgs = torch.empty(n * ln, dtype=torch.uint8, device=gpu)
     D.synth_fill(msgs, SEED + 281)
     got = D.hash_batch(msgs, n, ln)
