@@ -531,8 +531,9 @@ int mk_dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_ou
     if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0)
         hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
     else if (kRecKernel && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0)
-        hipLaunchKernelGGL((mk::k_keccak_rec<35>), dim3(std::min<uint64_t>(grid, mk::kRecGridMax)), dim3(256), 0, st,
-                           (const uint2*)d_in, n, (uint4*)d_out);
+        hipLaunchKernelGGL((mk::k_keccak_rec<35>),
+                           dim3(std::min<uint64_t>(ceil_div(n, mk::kRecThreads), mk::kRecGridMax)),
+                           dim3(mk::kRecThreads), 0, st, (const uint2*)d_in, n, (uint4*)d_out);
     else if (msg_len % 8 == 0 && msg_len > 0 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0)
         hipLaunchKernelGGL(mk::k_keccak_words, dim3(grid), dim3(256), 0, st, (const uint2*)d_in, n, msg_len / 8,
                            (uint4*)d_out);
@@ -1044,8 +1045,9 @@ int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64
         hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, d_offs,
                            n, lv);
     } else if (kRecKernel && fixed_len == 280 && ((uintptr_t)d_data % 8) == 0) {  // deposit leaves
-        hipLaunchKernelGGL((mk::k_keccak_rec<35>), dim3(std::min<uint64_t>(ceil_div(n, 256), mk::kRecGridMax)),
-                           dim3(256), 0, st, (const uint2*)d_data, n, lv);
+        hipLaunchKernelGGL((mk::k_keccak_rec<35>),
+                           dim3(std::min<uint64_t>(ceil_div(n, mk::kRecThreads), mk::kRecGridMax)),
+                           dim3(mk::kRecThreads), 0, st, (const uint2*)d_data, n, lv);
     } else if (fixed_len % 8 == 0 && ((uintptr_t)d_data % 8) == 0) {
         hipLaunchKernelGGL(mk::k_keccak_words, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint2*)d_data, n,
                            fixed_len / 8, lv);

@@ -1308,10 +1308,11 @@ __global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ 
 #define MK_REC_NT 0
 #endif
 template <int NW>
-__global__ __launch_bounds__(256) void k_keccak_rec(const uint2* __restrict__ in, uint64_t n, uint4* __restrict__ out) {
+__global__ __launch_bounds__(kRecThreads) void k_keccak_rec(const uint2* __restrict__ in, uint64_t n,
+                                                            uint4* __restrict__ out) {
     constexpr int NB = NW / 17 + 1;
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * kRecThreads;
+    uint64_t i = (uint64_t)blockIdx.x * kRecThreads + threadIdx.x;
     if (i >= n) return;
     uint2 buf[17];
     auto load = [&](uint64_t rec, int b) {

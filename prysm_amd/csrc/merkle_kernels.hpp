@@ -35,7 +35,10 @@ struct ReduceArgs {
 };
 
 constexpr uint32_t kMaxStructFields = 32;
-constexpr uint32_t kStructThreads = 256;              // k_struct_fused: one record per thread
+#ifndef MK_STRUCT_THREADS
+#define MK_STRUCT_THREADS 256
+#endif
+constexpr uint32_t kStructThreads = MK_STRUCT_THREADS;  // k_struct_fused: one record per thread
 constexpr uint32_t kStructFusedMaxMsg = 160;          // LDS: kStructThreads * msg_len bytes
 constexpr uint32_t kStructFusedMaxField = 64;         // bytes fields held in 16 registers
 struct StructSpec {                 // flat fixed-layout record (hash.go:141-159)
@@ -66,6 +69,10 @@ __global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
 __global__ void k_keccak_words(const uint2* in, uint64_t n, uint32_t nwords, uint4* out);
 template <int NW>
 __global__ void k_keccak_rec(const uint2* in, uint64_t n, uint4* out);
+#ifndef MK_REC_THREADS
+#define MK_REC_THREADS 256
+#endif
+constexpr uint32_t kRecThreads = MK_REC_THREADS;  // k_keccak_rec workgroup size
 #ifndef MK_REC_GRID
 #define MK_REC_GRID 4096
 #endif

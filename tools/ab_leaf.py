@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--item-len", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--trie", action="store_true", help="A/B the depth-32 deposit trie over 2^log2n x 280-B deposits")
+    ap.add_argument("--struct", action="store_true", help="A/B the typed registry root of 1,000,000 validators")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -46,6 +47,8 @@ def main():
         assert libs[v].mk_init(0) == 0
     if a.trie:
         return ab_trie(a, libs, dev)
+    if a.struct:
+        return ab_struct(a, libs, dev)
     n, il = 1 << a.log2n, a.item_len
     items = torch.empty(n * il, dtype=torch.uint8, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -111,6 +114,42 @@ def ab_trie(a, libs, dev):
     assert len(set(roots.values())) == 1, roots
     for v in a.variants:
         print(json.dumps({"variant": v, "trie_log2n": a.log2n, "median_ms": statistics.median(times[v]),
+                          "min_ms": min(times[v])}))
+    print(json.dumps({"root": next(iter(roots.values()), None)}))
+
+
+def ab_struct(a, libs, dev):
+    import numpy as np
+    import torch
+
+    from prysm_amd import registry as R
+
+    n = 1_000_000
+    reg = R.synthetic_registry(n, 0x5EED000000000003)
+    rec = torch.from_numpy(reg.records.view(np.uint8).reshape(-1).copy()).to(dev)
+    spec = R._fields(R.VALIDATOR_FIELDS)
+    nf = len(R.VALIDATOR_FIELDS)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    first = libs[a.variants[0]]
+    ws = torch.empty(first.mk_ssz_struct_list_workspace_bytes(n, spec, nf) + 4096, dtype=torch.uint8, device=dev)
+    outs = {v: torch.empty(32, dtype=torch.uint8, device=dev) for v in a.variants}
+    times = {v: [] for v in a.variants}
+    for r in range(a.rounds + 1):
+        for v, L in libs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = L.mk_dev_ssz_struct_list_root(ctypes.c_void_p(rec.data_ptr()), n, 160, spec, nf,
+                                               ctypes.c_void_p(outs[v].data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                               ws.numel(), st)
+            e1.record()
+            torch.cuda.synchronize()
+            assert rc == 0, (v, rc)
+            if r:
+                times[v].append(e0.elapsed_time(e1))
+    roots = {v: bytes(o.cpu().numpy()).hex() for v, o in outs.items()}
+    assert len(set(roots.values())) == 1, roots
+    for v in a.variants:
+        print(json.dumps({"variant": v, "struct_n": n, "median_ms": statistics.median(times[v]),
                           "min_ms": min(times[v])}))
     print(json.dumps({"root": next(iter(roots.values()), None)}))
 
