@@ -113,8 +113,9 @@ int mk_dev_ssz_merkle_finish_nodes(const void* d_nodes, uint64_t count, uint64_t
 int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32,
                              void* stream);
 /* Single-process multi-device merkleHash for the cgo caller: shards the host
- * items over devices 0..ndev-1, gathers the shard roots over RCCL (xGMI) and
- * finishes on device 0. */
+ * items over devices 0..ndev-1, reduces every shard to its frontier level
+ * (up to 1024 nodes), all-gathers the frontiers over RCCL (xGMI) and finishes
+ * on device 0. */
 int mk_ssz_merkle_hash_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int ndev,
                              uint8_t out[32]);
 
