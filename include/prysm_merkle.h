@@ -188,9 +188,11 @@ int mk_dev_synth_fill(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t word
 /* ---- measurement -------------------------------------------------------- */
 /* When enabled, every dev merkle call records hipEvents around its dominant
  * (leaf) kernel launches on the call's stream; mk_prof_read synchronises those
- * events and returns the summed milliseconds and launch count, then resets. */
+ * events and returns the summed milliseconds, launch count, algorithmic
+ * Keccak-f permutations and digests (hashes) of those launches, then resets.
+ * Any out-pointer may be NULL. */
 int mk_prof_enable(int on);
-int mk_prof_read(double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms);
+int mk_prof_read(double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms, double* leaf_hashes);
 
 #ifdef __cplusplus
 }

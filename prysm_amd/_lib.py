@@ -70,7 +70,7 @@ _SIGS = {
     "mk_verify_merkle_branches": (_int, [_vp, _vp, _vp, _u64, _u32, _u32, _vp, _vp]),
     "mk_dev_synth_fill": (_int, [_vp, _u64, _u64, _u64, _vp]),
     "mk_prof_enable": (_int, [_int]),
-    "mk_prof_read": (_int, [_vp, _vp, _vp]),
+    "mk_prof_read": (_int, [_vp, _vp, _vp, _vp]),
 }
 
 MK_FIELD_BYTES = 1

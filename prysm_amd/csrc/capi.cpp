@@ -171,7 +171,7 @@ int grow(DevBuf& b, size_t bytes) {
 // ---- measurement -------------------------------------------------------------
 struct ProfRec {
     hipEvent_t a, b;
-    double perms;
+    double perms, hashes;
 };
 std::mutex g_prof_mu;
 bool g_prof_on = false;
@@ -195,6 +195,7 @@ struct Pass {
     int in_ws;   // -1 = user input, else ping-pong slot
     int out_ws;  // -1 = user output, else ping-pong slot
     double perms;
+    double hashes;  // digests produced (each ends in one digest-only permutation)
 };
 
 struct Plan {
@@ -270,7 +271,7 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
             a.c1_full = cin / 2;
         }
         // algorithmic permutations of this pass (first level + fused levels)
-        double perms = 0;
+        double perms = 0, hashes = 0;
         if (leaf) {
             const uint64_t full = total / (2 * cb);
             perms += (double)std::min<uint64_t>(full, c1) * perms_for_len(2 * cb);
@@ -279,8 +280,10 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
                 const uint64_t len = (2 * j + 1 < nchunks) ? std::min(total, lo + 2 * cb) - lo : total - lo + 128;
                 perms += (double)perms_for_len(len);
             }
+            hashes += (double)c1;
         } else if (cin > 1 || pad_at_one) {
             perms += (double)(cin / 2) + (cin % 2 ? 2.0 : 0.0);
+            hashes += (double)ceil_div(cin, 2);
         }
         uint64_t c = c1;
         const bool wave = c1 <= (leaf || !kWave3 ? kLeafWaveMaxC1 : kNodeWaveMaxC1);
@@ -305,9 +308,11 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         for (uint32_t l = 1; l < lv; ++l) {  // fused levels above the first
             if (c <= 1 && !pad_at_one) break;
             perms += (double)(c / 2) + (c % 2 ? 2.0 : 0.0);
+            hashes += (double)ceil_div(c, 2);
             c = ceil_div(c, 2);
         }
         ps.perms = perms;
+        ps.hashes = hashes;
         ps.wave = wave;
         ps.nt = nt;
         a.in_ilv = (w3 && !leaf && !p.passes.empty() && p.passes.back().w3) ? 1 : 0;
@@ -451,6 +456,7 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
         if (rec_this) {
             HIPCHK(hipEventRecord(rec.b, st));
             rec.perms = ps.perms;
+            rec.hashes = ps.hashes;
             std::lock_guard<std::mutex> lk(g_prof_mu);
             g_prof.push_back(rec);
         }
@@ -1197,25 +1203,27 @@ int mk_prof_enable(int on) {
     return MK_OK;
 }
 
-int mk_prof_read(double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms) {
+int mk_prof_read(double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms, double* leaf_hashes) {
     std::vector<ProfRec> recs;
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         recs.swap(g_prof);
     }
-    double ms = 0, perms = 0;
+    double ms = 0, perms = 0, hashes = 0;
     for (auto& r : recs) {
         HIPCHK(hipEventSynchronize(r.b));
         float t = 0;
         HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
         ms += t;
         perms += r.perms;
+        hashes += r.hashes;
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
     }
     if (leaf_ms) *leaf_ms = ms;
     if (leaf_launches) *leaf_launches = recs.size();
     if (leaf_perms) *leaf_perms = perms;
+    if (leaf_hashes) *leaf_hashes = hashes;
     return MK_OK;
 }
 

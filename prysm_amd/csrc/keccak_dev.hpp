@@ -162,6 +162,67 @@ __device__ __forceinline__ void keccak_f(State& s) {
     for (int r = 0; r < 24; ++r) round_fn(s, kRcLo[r], kRcHi[r]);
 }
 
+// Last round when only the 32-byte digest (lanes 0..3) is read afterwards:
+// chi of row 0 needs b[X,0] = rho(theta(A))[X,X] (pi maps the diagonal to
+// row 0), so theta is applied to the 5 diagonal lanes only and chi computed
+// for 4 lanes: 58 VALU instead of 180 (20 parity + 10 D + 10 apply + 8 rho +
+// 8 chi + 2 iota).  Lanes 4..24 are left stale.
+template <int X>
+__device__ __forceinline__ void diag_rho(const State& s, const uint32_t (&clo)[5], const uint32_t (&chi_)[5],
+                                         const uint32_t (&rlo)[5], const uint32_t (&rhi)[5], uint32_t (&blo)[5],
+                                         uint32_t (&bhi)[5]) {
+    constexpr int i = 6 * X;  // lane (X, X)
+    const uint32_t alo = xor3(s.lo[i], clo[(X + 4) % 5], rlo[(X + 1) % 5]);
+    const uint32_t ahi = xor3(s.hi[i], chi_[(X + 4) % 5], rhi[(X + 1) % 5]);
+    rotl64<MK_RHO(i)>(alo, ahi, blo[X], bhi[X]);
+}
+
+__device__ __forceinline__ void last_round_digest(State& s, uint32_t rclo, uint32_t rchi) {
+    uint32_t clo[5], chi_[5];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+        clo[x] = xor3(xor3(s.lo[x], s.lo[x + 5], s.lo[x + 10]), s.lo[x + 15], s.lo[x + 20]);
+        chi_[x] = xor3(xor3(s.hi[x], s.hi[x + 5], s.hi[x + 10]), s.hi[x + 15], s.hi[x + 20]);
+    }
+    uint32_t rlo[5], rhi[5];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) rotl64<1>(clo[x], chi_[x], rlo[x], rhi[x]);
+    uint32_t blo[5], bhi[5];
+    diag_rho<0>(s, clo, chi_, rlo, rhi, blo, bhi);
+    diag_rho<1>(s, clo, chi_, rlo, rhi, blo, bhi);
+    diag_rho<2>(s, clo, chi_, rlo, rhi, blo, bhi);
+    diag_rho<3>(s, clo, chi_, rlo, rhi, blo, bhi);
+    diag_rho<4>(s, clo, chi_, rlo, rhi, blo, bhi);
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+        s.lo[x] = chi3(blo[x], blo[(x + 1) % 5], blo[(x + 2) % 5]);
+        s.hi[x] = chi3(bhi[x], bhi[(x + 1) % 5], bhi[(x + 2) % 5]);
+    }
+    s.lo[0] ^= rclo;
+    s.hi[0] ^= rchi;
+}
+
+#ifndef MK_DIGEST_ROUND
+#define MK_DIGEST_ROUND 1
+#endif
+// Final permutation of a hash: only digest(s) may read the state afterwards.
+__device__ __forceinline__ void keccak_f_digest(State& s) {
+#if MK_DIGEST_ROUND
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < 22; ++r) round_fn(s, kRcLo[r], kRcHi[r]);
+    round_fn(s, kRcLo[22], kRcHi[22]);
+    last_round_digest(s, kRcLo[23], kRcHi[23]);
+    // Pin the digest here: without a use in this block LLVM sinks the two
+    // straight-line rounds towards the digest's consumer (past the next
+    // window's permutations in k_reduce), keeping this state alive across
+    // them (117 -> 159 VGPRs, 4 -> 3 waves/SIMD).
+    asm volatile("" : "+v"(s.lo[0]), "+v"(s.hi[0]), "+v"(s.lo[1]), "+v"(s.hi[1]), "+v"(s.lo[2]), "+v"(s.hi[2]),
+                 "+v"(s.lo[3]), "+v"(s.hi[3]));
+#else
+    keccak_f(s);
+#endif
+}
+
 // ---- absorb helpers --------------------------------------------------------
 __device__ __forceinline__ void xor_lane(State& s, int i, uint2 w) {
     s.lo[i] ^= w.x;

@@ -76,8 +76,9 @@ __device__ __noinline__ void sponge_generic(const uint8_t* __restrict__ p, uint6
     digest(s, d0, d1);
 }
 
-// K(L || R) (64 B, 1 permutation) or K(L || 0^128) (160 B, 2 permutations)
-// with a single keccak_f copy; `padded` may differ between lanes.
+// K(L || R) (64 B, 1 permutation) or K(L || 0^128) (160 B, 2 permutations);
+// `padded` may differ between lanes (the block-1 permutation then diverges).
+// The final permutation computes only the digest lanes (keccak_f_digest).
 __device__ __forceinline__ void hash_pair(uint4 l0, uint4 l1, uint4 r0, uint4 r1, bool padded,
                                           uint4& d0, uint4& d1) {
     State s;
@@ -92,18 +93,13 @@ __device__ __forceinline__ void hash_pair(uint4 l0, uint4 l1, uint4 r0, uint4 r1
         xor_lane(s, 6, make_uint2(r1.x, r1.y));
         xor_lane(s, 7, make_uint2(r1.z, r1.w));
     }
-    const int nperm = padded ? 2 : 1;
-#pragma unroll 1
-    for (int r = 0; r < nperm; ++r) {
-        if (r == nperm - 1) {
-            if (padded)
-                s.lo[3] ^= 1u;  // byte 160 = byte 24 of block 1
-            else
-                s.lo[8] ^= 1u;  // byte 64
-            s.hi[16] ^= 0x80000000u;
-        }
-        keccak_f(s);
-    }
+    if (padded) keccak_f(s);  // block 1 = L || 0^104; block 2 = 0^24 || padding
+    if (padded)
+        s.lo[3] ^= 1u;  // byte 160 = byte 24 of block 1
+    else
+        s.lo[8] ^= 1u;  // byte 64
+    s.hi[16] ^= 0x80000000u;
+    keccak_f_digest(s);
     digest(s, d0, d1);
 }
 
@@ -118,7 +114,7 @@ __device__ __forceinline__ void hash_final(uint4 r0, uint4 r1, uint64_t n, uint4
     xor_lane(s, 4, make_uint2((uint32_t)n, (uint32_t)(n >> 32)));
     s.lo[8] ^= 1u;
     s.hi[16] ^= 0x80000000u;
-    keccak_f(s);
+    keccak_f_digest(s);
     digest(s, d0, d1);
 }
 
@@ -162,7 +158,7 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
     }
     s.lo[15] ^= 1u;
     s.hi[16] ^= 0x80000000u;
-    keccak_f(s);
+    keccak_f_digest(s);
     digest(s, d0, d1);
     return;
 #endif
@@ -1099,7 +1095,7 @@ __global__ __launch_bounds__(256) void k_struct_fields(const uint8_t* __restrict
                     s.lo[q / 2] ^= v;
             }
             s.hi[16] ^= 0x80000000u;
-            keccak_f(s);
+            keccak_f_digest(s);
             digest(s, d0, d1);
         } else {
             sponge_prefix4(r + off, len, d0, d1);
@@ -1196,7 +1192,7 @@ __global__ __launch_bounds__(kStructThreads) void k_struct_fused(const uint8_t* 
                 s.lo[q / 2] ^= v;
         }
         s.hi[16] ^= 0x80000000u;
-        keccak_f(s);
+        keccak_f_digest(s);
         uint4 d0, d1;
         digest(s, d0, d1);
         const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
@@ -1220,7 +1216,10 @@ __global__ __launch_bounds__(kStructThreads) void k_struct_fused(const uint8_t* 
             else
                 s.lo[w / 2] ^= v;
         }
-        keccak_f(s);
+        if (b + 1 < nb)  // nb is uniform (one struct layout)
+            keccak_f(s);
+        else
+            keccak_f_digest(s);
     }
     if (live) {
         uint4 d0, d1;
@@ -1271,7 +1270,10 @@ __global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ 
                 s.hi[w] ^= v.y;
             }
             if (b == nb - 1) s.hi[16] ^= 0x80000000u;
-            keccak_f(s);
+            if (b + 1 < nb)  // nb is uniform (fixed message length)
+                keccak_f(s);
+            else
+                keccak_f_digest(s);
         }
     } else {
 #pragma unroll 1
@@ -1289,7 +1291,10 @@ __global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ 
                 }
             }
             if (b == nb - 1) s.hi[16] ^= 0x80000000u;
-            keccak_f(s);
+            if (b + 1 < nb)  // nb is uniform (fixed message length)
+                keccak_f(s);
+            else
+                keccak_f_digest(s);
         }
     }
     uint4 d0, d1;
@@ -1348,7 +1353,10 @@ __global__ __launch_bounds__(kRecThreads) void k_keccak_rec(const uint2* __restr
                 load(i, b + 1);
             else if (i + stride < n)
                 load(i + stride, 0);
-            keccak_f(s);
+            if (b + 1 < NB)
+                keccak_f(s);
+            else
+                keccak_f_digest(s);
         }
         uint4 d0, d1;
         digest(s, d0, d1);

@@ -154,9 +154,11 @@ def prof_enable(on: bool = True) -> None:
 
 
 def prof_read():
-    """(summed ms, launches, algorithmic permutations) of the recorded leaf passes."""
+    """(summed ms, launches, algorithmic permutations, digests) of the recorded leaf passes."""
     ms = ctypes.c_double()
     cnt = ctypes.c_uint64()
     perms = ctypes.c_double()
-    _lib.check(_lib.load().mk_prof_read(ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(perms)), "mk_prof_read")
-    return ms.value, cnt.value, perms.value
+    hashes = ctypes.c_double()
+    _lib.check(_lib.load().mk_prof_read(ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(perms), ctypes.byref(hashes)),
+               "mk_prof_read")
+    return ms.value, cnt.value, perms.value, hashes.value

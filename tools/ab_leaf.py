@@ -61,7 +61,7 @@ def main():
     for r in range(a.rounds + 1):
         for v, L in libs.items():
             L.mk_prof_enable(1)
-            L.mk_prof_read(None, None, None)
+            L.mk_prof_read(None, None, None, None)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             rc = L.mk_dev_ssz_merkle_hash(ctypes.c_void_p(items.data_ptr()), n, il,
@@ -73,7 +73,7 @@ def main():
             ms = ctypes.c_double()
             cnt = ctypes.c_uint64()
             perms = ctypes.c_double()
-            L.mk_prof_read(ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(perms))
+            L.mk_prof_read(ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(perms), None)
             L.mk_prof_enable(0)
             if r:  # round 0 is warmup
                 times[v].append(e0.elapsed_time(e1))
