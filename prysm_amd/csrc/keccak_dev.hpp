@@ -111,7 +111,105 @@ __device__ __forceinline__ void rho_pi_all(const State& a, uint32_t (&blo)[25], 
 #define MK_SB()
 #endif
 
+// MK_ASM_ROUND=1 (default): the round with its instruction order fixed, one
+// asm volatile statement per VALU op, phases in sequence (20 bitop3 | 10
+// alignbit | 50 bitop3 | 48 alignbit | 52 bitop3/xor): four full-/half-rate
+// class switches per round.  The compiler's own schedule interleaves the
+// classes and issues ~2 % slower (tools/asm_round_probe.hip, register-resident
+// 43.4 vs 42.7 T ops/s; leaf kernel 2^28: 10.35 -> 10.13 ms in one-process
+// A/B); interleaving rho and chi row by row is slower still (41.7-42.1 T).
+// Register allocation stays with the compiler.
+#ifndef MK_ASM_ROUND
+#define MK_ASM_ROUND 1
+#endif
+__device__ __forceinline__ uint32_t ax3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t achi(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xd2" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+template <int S>
+__device__ __forceinline__ uint32_t aalign(uint32_t hi, uint32_t lo) {
+    uint32_t r;
+    asm volatile("v_alignbit_b32 %0, %1, %2, %3" : "=v"(r) : "v"(hi), "v"(lo), "i"(S));
+    return r;
+}
+__device__ __forceinline__ uint32_t axs(uint32_t a, uint32_t s) {
+    uint32_t r;
+    asm volatile("v_xor_b32 %0, %1, %2" : "=v"(r) : "s"(s), "v"(a));
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void arot(uint32_t lo, uint32_t hi, uint32_t& olo, uint32_t& ohi) {
+    if constexpr (N == 0) {
+        olo = lo;
+        ohi = hi;
+    } else if constexpr (N < 32) {
+        ohi = aalign<32 - N>(hi, lo);
+        olo = aalign<32 - N>(lo, hi);
+    } else {
+        ohi = aalign<64 - N>(lo, hi);
+        olo = aalign<64 - N>(hi, lo);
+    }
+}
+template <int I>
+__device__ __forceinline__ void arho(const State& a, uint32_t (&blo)[25], uint32_t (&bhi)[25]) {
+    constexpr int x = I % 5, y = I / 5;
+    constexpr int dst = y + 5 * ((2 * x + 3 * y) % 5);
+    arot<MK_RHO(I)>(a.lo[I], a.hi[I], blo[dst], bhi[dst]);
+}
+template <int... Is>
+__device__ __forceinline__ void arho_all(const State& a, uint32_t (&blo)[25], uint32_t (&bhi)[25],
+                                         std::integer_sequence<int, Is...>) {
+    (arho<Is>(a, blo, bhi), ...);
+}
+
+__device__ __forceinline__ void round_asm(State& s, uint32_t rclo, uint32_t rchi) {
+    uint32_t clo[5], chi_[5];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+        clo[x] = ax3(s.lo[x], s.lo[x + 5], s.lo[x + 10]);
+        chi_[x] = ax3(s.hi[x], s.hi[x + 5], s.hi[x + 10]);
+    }
+#pragma unroll
+    for (int x = 0; x < 5; ++x) {
+        clo[x] = ax3(clo[x], s.lo[x + 15], s.lo[x + 20]);
+        chi_[x] = ax3(chi_[x], s.hi[x + 15], s.hi[x + 20]);
+    }
+    uint32_t rlo[5], rhi[5];
+#pragma unroll
+    for (int x = 0; x < 5; ++x) arot<1>(clo[x], chi_[x], rlo[x], rhi[x]);
+#pragma unroll
+    for (int i = 0; i < 25; ++i) {
+        const int x = i % 5;
+        s.lo[i] = ax3(s.lo[i], clo[(x + 4) % 5], rlo[(x + 1) % 5]);
+        s.hi[i] = ax3(s.hi[i], chi_[(x + 4) % 5], rhi[(x + 1) % 5]);
+    }
+    uint32_t blo[25], bhi[25];
+    arho_all(s, blo, bhi, std::make_integer_sequence<int, 25>{});
+#pragma unroll
+    for (int y = 0; y < 5; ++y) {
+#pragma unroll
+        for (int x = 0; x < 5; ++x) {
+            const int i = x + 5 * y;
+            const int i1 = (x + 1) % 5 + 5 * y, i2 = (x + 2) % 5 + 5 * y;
+            s.lo[i] = achi(blo[i], blo[i1], blo[i2]);
+            s.hi[i] = achi(bhi[i], bhi[i1], bhi[i2]);
+        }
+    }
+    s.lo[0] = axs(s.lo[0], rclo);
+    s.hi[0] = axs(s.hi[0], rchi);
+}
+
 __device__ __forceinline__ void round_fn(State& s, uint32_t rclo, uint32_t rchi) {
+#if MK_ASM_ROUND
+    round_asm(s, rclo, rchi);
+    return;
+#endif
     uint32_t clo[5], chi_[5];
 #pragma unroll
     for (int x = 0; x < 5; ++x) {
