@@ -74,7 +74,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log2n", type=int, default=28)
     ap.add_argument("--item-len", type=int, default=32)
-    ap.add_argument("--cpu-sample-log2n", type=int, default=24)
+    ap.add_argument("--cpu-sample-log2n", type=int, default=26)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N ranks on one GPU)")

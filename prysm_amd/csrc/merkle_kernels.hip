@@ -199,6 +199,56 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
     digest(s, d0, d1);
 }
 
+// MK_STAGE_LDS=1: the same window with its second block parked in this
+// thread's 128-B LDS slot (dword-major across the workgroup:
+// stg[k * kReduceThreads], conflict-free 16-B accesses) for the duration of
+// the first permutation, so the 30 VGPRs it held there are free and the leaf
+// kernel fits 5 waves/SIMD (96 VGPRs, 32 KB LDS per workgroup).
+#ifndef MK_STAGE_LDS
+#define MK_STAGE_LDS 1
+#endif
+#ifndef MK_STAGE_WAVES
+#define MK_STAGE_WAVES 5
+#endif
+
+__device__ __forceinline__ void hash_window256_staged(const uint4* __restrict__ w, uint4* stg, uint4& d0,
+                                                      uint4& d1) {
+    State s;
+    uint4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = ld_nt(w + k);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) stg[k * kReduceThreads] = v[8 + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        s.lo[2 * k] = v[k].x;
+        s.hi[2 * k] = v[k].y;
+        s.lo[2 * k + 1] = v[k].z;
+        s.hi[2 * k + 1] = v[k].w;
+    }
+    s.lo[16] = v[8].x;
+    s.hi[16] = v[8].y;
+#pragma unroll
+    for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+    keccak_f(s);
+    uint4 u[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) u[k] = stg[k * kReduceThreads];
+    s.lo[0] ^= u[0].z;
+    s.hi[0] ^= u[0].w;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        s.lo[1 + 2 * k] ^= u[1 + k].x;
+        s.hi[1 + 2 * k] ^= u[1 + k].y;
+        s.lo[2 + 2 * k] ^= u[1 + k].z;
+        s.hi[2 + 2 * k] ^= u[1 + k].w;
+    }
+    s.lo[15] ^= 1u;
+    s.hi[16] ^= 0x80000000u;
+    keccak_f_digest(s);
+    digest(s, d0, d1);
+}
+
 // ----------------------------------------------------------------------------
 // First-level node j of a reduce pass.
 //   LEAF: window j of the item buffer.
@@ -247,10 +297,13 @@ __device__ __forceinline__ void first_level_generic(const ReduceArgs& a, uint64_
 // Non-final passes write 512 >> (levels-2) nodes per workgroup; the final
 // pass (one workgroup) reduces to the root and applies the length mix-in.
 template <bool LEAF, bool FAST, int NI>
-__global__ __launch_bounds__(kReduceThreads, MK_MIN_WAVES) void k_reduce(ReduceArgs a) {
+__global__ __launch_bounds__(kReduceThreads, (MK_STAGE_LDS && LEAF && FAST) ? MK_STAGE_WAVES : MK_MIN_WAVES) void k_reduce(
+    ReduceArgs a) {
     constexpr uint64_t kSpan1 = 2 * NI * kReduceThreads;  // first-level nodes per workgroup
     constexpr uint64_t kSpan2 = kSpan1 / 2;
-    __shared__ uint4 lds[2 * kSpan2];
+    constexpr bool kStaged = MK_STAGE_LDS && LEAF && FAST;
+    constexpr uint64_t kLdsU4 = kStaged && 8 * kReduceThreads > 2 * kSpan2 ? 8 * kReduceThreads : 2 * kSpan2;
+    __shared__ uint4 lds[kLdsU4];
     const uint32_t tid = threadIdx.x;
     const uint64_t wg = a.wg_base + blockIdx.x;
     const uint64_t lo1 = wg * kSpan1;
@@ -261,7 +314,32 @@ __global__ __launch_bounds__(kReduceThreads, MK_MIN_WAVES) void k_reduce(ReduceA
     const uint64_t m2 = pair ? (m1 + 1) / 2 : m1;
 
     // ---- phase A: first level (+ pair level) from global memory ----------
-    if constexpr (FAST) {
+    if constexpr (kStaged) {
+        // The staging slots alias the level buffer: every pair node stays in
+        // registers until all threads are done with their slots.
+        static_assert(NI == 1 || NI == 2, "staged leaf pass holds at most 2 pair nodes");
+        uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0, d0, d1;
+#pragma unroll 1
+        for (int i = 0; i < NI; ++i) {
+            const uint32_t q = i * kReduceThreads + tid;
+            const uint4* w = reinterpret_cast<const uint4*>(a.items) + (lo1 + 2 * (uint64_t)q) * 16;
+            uint4 l0, l1, r0, r1;
+            hash_window256_staged(w, lds + tid, l0, l1);
+            hash_window256_staged(w + 16, lds + tid, r0, r1);
+            hash_pair(l0, l1, r0, r1, false, d0, d1);
+            if (i == 0) {
+                e0 = d0;
+                e1 = d1;
+            }
+        }
+        __syncthreads();
+        lds[2 * tid] = e0;
+        lds[2 * tid + 1] = e1;
+        if (NI == 2) {
+            lds[2 * (kReduceThreads + tid)] = d0;
+            lds[2 * (kReduceThreads + tid) + 1] = d1;
+        }
+    } else if constexpr (FAST) {
         // Full workgroup of full windows / complete node pairs (host-checked):
         // no bounds checks, no odd padding, one keccak_f copy per call site.
 #pragma unroll 1
