@@ -4,10 +4,15 @@ BASELINE.json configs[3]) on N MI355X, subtree-sharded.
   python bench.py [--gpus N] [--steps K] [--warmup W] [--log2n 28] [--item-len 32]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One step = one complete Merkleization of the whole tree (every rank reduces
-its shard to the level 10 below its shard root (1024 nodes, the "frontier"),
-one 32-KB-per-rank RCCL all-gather, rank 0 finishes the top levels and the
-length mix-in on a side stream that overlaps its next step).  Inputs are generated on the device before timing and
+One step = one complete Merkleization of the whole tree.  N > 1: every rank
+reduces its shard to the level 10 below its shard root (1024 nodes, the
+"frontier"), one 32-KB-per-rank RCCL all-gather, rank 0 finishes the top
+levels and the length mix-in on a side stream that overlaps its next step.
+N = 1 (--pipeline 21): the tree is split the same way 21 levels below its
+root (the leaf pass's output level); the node passes above it run on a side
+stream that overlaps the next step's leaf pass (prysm_amd/pipeline.py); the
+pipelined root is checked against the one-stream root before timing, and
+every step's work completes inside the timed region.  Inputs are generated on the device before timing and
 stay resident in HBM.  Total work is fixed as N grows ("strong" scaling);
 value = 2^log2n leaves x K / max-over-ranks wall time.  Rank 0 prints one
 JSON line; progress goes to stderr.
@@ -83,6 +88,9 @@ def main():
     ap.add_argument("--frontier", type=int, default=10,
                     help="N>1: each rank gathers its tree level this many levels below its shard root "
                          "(2^k nodes) and rank 0 finishes the top (0 = gather the 32-B shard roots)")
+    ap.add_argument("--pipeline", type=int, default=21,
+                    help="N=1: split each tree this many levels below its root; the top runs on a side stream "
+                         "overlapping the next step's leaves (prysm_amd/pipeline.py; 0 = one stream)")
     ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c5"],
                     help="BASELINE.json config: c4 = headline (default); c1/c2/c3/c5 = single-GPU side benches")
     args = ap.parse_args()
@@ -137,7 +145,22 @@ def main():
     log(f"rank {rank}/{world}: {local_n} items ({nbytes / 2**30:.2f} GiB), shard height {sp.height}, "
         f"nonempty {sp.nonempty}, frontier {k}")
 
+    pipe = None
+    if world == 1 and args.pipeline > 0:
+        from prysm_amd.pipeline import MerklePipeline
+
+        pipe = MerklePipeline(n, item_len, dev, frontier_log2=args.pipeline)
+        k = pipe.k
+        # the pipelined root must equal the one-stream root of the same items
+        want = bytes(D.merkle_hash(items, n, item_len, out=root_buf, ws=ws).cpu().numpy())
+        got = pipe.submit(items)
+        torch.cuda.synchronize()
+        assert bytes(got.cpu().numpy()) == want, "pipelined root differs from merkle_hash"
+        log(f"pipelined: frontier {k} levels below the root, top on a side stream")
+
     def step():
+        if pipe is not None:
+            return pipe.submit(items)
         return P.sharded_merkle_hash(
             items, n, item_len, sp, rank, world,
             subtree_fn=lambda it, sn, il, h, pad: D.merkle_subtree(it, sn, il, h, pad, out=root_buf, ws=ws),
@@ -205,7 +228,8 @@ def main():
             "config": {"workload": f"C4: ssz.merkleHash of 2^{args.log2n} x {item_len}-B items "
                                    f"({n * item_len / 2**30:.0f} GiB), subtree-sharded",
                        "n_items": n, "item_len": item_len, "parallelism": f"subtree{world}",
-                       "shard_height": sp.height, "frontier_log2": k, "root": root_hex},
+                       "shard_height": sp.height, "frontier_log2": k, "pipelined": pipe is not None and k > 0,
+                       "root": root_hex},
             "roofline": {
                 "bound": "valu-int",
                 "kernel": "k_reduce<LEAF, FAST, 2> (leaf pass: 256-B windows + 4 fused levels)",

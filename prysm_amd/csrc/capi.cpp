@@ -335,6 +335,9 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
             p.passes.push_back(ps);
             break;
         }
+        if (!wave && lv < 2)  // k_reduce always folds the pair level (a frontier one level above the chunks)
+            return fail(MK_EINVAL, "planner: unsupported single-level pass (frontier %u of height %u)", frontier,
+                        height);
         if (frontier && remaining == lv) {  // the frontier level: plain nodes to the output
             ps.out_ws = -1;
             ps.a.out_ilv = 0;

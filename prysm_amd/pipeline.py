@@ -1,0 +1,69 @@
+"""merkleHash of a stream of trees with each tree's top overlapped with the
+next tree's leaves (one GPU, no collective).
+
+A tree's narrow top levels are latency-bound (one permutation latency per
+level); run on the stream that hashes the leaves they leave the
+chip mostly idle.  ``MerklePipeline.submit`` therefore splits one
+``merkleHash`` (shared/ssz/hash.go:194-239) at the level ``frontier_log2``
+levels below the root: the leaf side (everything up to that level) runs on
+the caller's current stream, the top (the remaining levels and the length
+mix-in, hash.go:225-237) on a side stream, where it overlaps the leaf side of
+the next submitted tree.  The split is the single-shard case of the subtree
+sharding in parallel.py (same planner, same frontier finisher), so each root
+is bit-identical to ``device.merkle_hash`` of the same items.
+
+Frontier levels and roots are double-buffered: a submit waits for the top of
+the tree submitted two calls earlier before it overwrites that tree's
+buffers, and the root returned by a submit stays valid until the submit after
+next.  The root is produced on ``side``; call ``torch.cuda.synchronize()`` or
+make the consuming stream wait on ``side`` before reading it.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import device as D
+from .parallel import frontier_count
+
+
+class MerklePipeline:
+    def __init__(self, n: int, item_len: int, device, frontier_log2: int = 21):
+        self.n, self.item_len = n, item_len
+        self.device = torch.device(device)
+        height, _, _ = D.shard_plan(n, item_len, 1)
+        self.height = height
+        k = min(frontier_log2, height - 2)  # the planner's throughput passes fold at least 2 levels
+        # a frontier level of one node is already the tree root's input: no top to split off
+        self.k = k if k > 0 and frontier_count(n, item_len, height, k) > 1 else 0
+        self.ws = D.subtree_workspace(n, item_len, self.device) if self.k else D.merkle_workspace(n, item_len,
+                                                                                                   self.device)
+        self.outs = [torch.empty(32, dtype=torch.uint8, device=self.device) for _ in range(2)]
+        if self.k:
+            self.count = frontier_count(n, item_len, height, self.k)
+            self.bufs = [torch.empty(32 << self.k, dtype=torch.uint8, device=self.device) for _ in range(2)]
+            self.fin_ws = D.finish_workspace(self.count, self.device)
+            self.side = torch.cuda.Stream(device=self.device)
+        else:
+            self.side = torch.cuda.current_stream(self.device)
+        self._done = [None, None]
+        self._i = 0
+
+    def submit(self, items: torch.Tensor) -> torch.Tensor:
+        """Enqueue merkleHash(items) (n items of item_len bytes); returns the
+        (32,) uint8 root tensor, produced on ``self.side``."""
+        slot = self._i & 1
+        self._i += 1
+        cur = torch.cuda.current_stream(self.device)
+        if not self.k:
+            return D.merkle_hash(items, self.n, self.item_len, out=self.outs[slot], ws=self.ws)
+        if self._done[slot] is not None:  # the top two trees back still reads this slot
+            cur.wait_event(self._done[slot])
+        level = D.merkle_subtree_frontier(items, self.n, self.item_len, self.height, self.k, False,
+                                          out=self.bufs[slot], ws=self.ws)
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            root = D.merkle_finish_nodes(level, self.count, self.n, out=self.outs[slot], ws=self.fin_ws)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        self._done[slot] = ev
+        return root

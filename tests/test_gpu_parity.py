@@ -237,6 +237,37 @@ def test_frontier_sharding_equals_full(gpu, n, world, k):
     assert bytes(root.cpu().numpy()) == O.merkle_hash_gen(n, item_len, SEED + 33, nthreads=16)
 
 
+@pytest.mark.parametrize("n,item_len,k", [(1 << 20, 32, 12), ((1 << 20) + 3, 32, 12), (3_000_017, 32, 16),
+                                          (3_000_017, 32, 21), (100_003, 8, 8), (1000, 32, 21), (5, 32, 4),
+                                          (777, 200, 3)])
+def test_pipeline_roots_equal_merkle_hash(gpu, n, item_len, k):
+    """MerklePipeline (leaf side on the current stream, top on a side stream
+    overlapping the next tree) over 5 consecutive trees of one shape: every
+    root equals merkleHash of its own items (oracle), with the double-buffered
+    frontier levels and roots reused across submits."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+    from prysm_amd.pipeline import MerklePipeline
+
+    pipe = MerklePipeline(n, item_len, gpu, frontier_log2=k)
+    trees = []
+    for t in range(5):
+        items = torch.empty(n * item_len, dtype=torch.uint8, device=gpu)
+        D.synth_fill(items, SEED + 4000 + t)
+        trees.append(items)
+    roots = []
+    for t, items in enumerate(trees):
+        roots.append(pipe.submit(items))
+        if t % 2 == 1 or t == len(trees) - 1:  # a root is valid until the submit after next
+            torch.cuda.synchronize()
+            roots = [r if isinstance(r, bytes) else bytes(r.cpu().numpy()) for r in roots]
+    for t, items in enumerate(trees):
+        want = O.merkle_hash_flat(items.cpu().numpy(), n, item_len)
+        assert roots[t] == want, (t, pipe.k)
+
+
 @pytest.mark.parametrize("count", [2, 3, 64, 65, 127, 1000, 2048, 2049, 5001])
 def test_finish_nodes_vs_reference_loop(gpu, count):
     """The finisher over one gathered tree level: reference level loop with
