@@ -8,10 +8,12 @@ One step = one complete Merkleization of the whole tree.  N > 1: every rank
 reduces its shard to the level 10 below its shard root (1024 nodes, the
 "frontier"), one 32-KB-per-rank RCCL all-gather, rank 0 finishes the top
 levels and the length mix-in on a side stream that overlaps its next step.
-N = 1 (--pipeline 21): the tree is split the same way 21 levels below its
-root (the leaf pass's output level); the node passes above it run on a side
-stream that overlaps the next step's leaf pass (prysm_amd/pipeline.py); the
-pipelined root is checked against the one-stream root before timing, and
+With --pipeline (default) everything above the leaf pass runs on a side
+stream that overlaps the next step's leaf pass: at N = 1 the node passes and
+the length mix-in (prysm_amd/pipeline.py, split 21 levels below the root =
+the leaf pass's output level); at N > 1 each rank's node passes down to its
+frontier, the all-gather and rank 0's finisher (parallel.ShardedMerklePipeline).
+The pipelined root is checked against the one-stream root before timing, and
 every step's work completes inside the timed region.  Inputs are generated on the device before timing and
 stay resident in HBM.  Total work is fixed as N grows ("strong" scaling);
 value = 2^log2n leaves x K / max-over-ranks wall time.  Rank 0 prints one
@@ -89,8 +91,11 @@ def main():
                     help="N>1: each rank gathers its tree level this many levels below its shard root "
                          "(2^k nodes) and rank 0 finishes the top (0 = gather the 32-B shard roots)")
     ap.add_argument("--pipeline", type=int, default=21,
-                    help="N=1: split each tree this many levels below its root; the top runs on a side stream "
-                         "overlapping the next step's leaves (prysm_amd/pipeline.py; 0 = one stream)")
+                    help="N=1: split each tree this many levels below its root (21 = the leaf pass's output "
+                         "level at 2^28); the top runs on a side stream overlapping the next step's leaf pass "
+                         "(prysm_amd/pipeline.py).  N>1: any value > 0 moves each rank's node passes, the "
+                         "all-gather and rank 0's finisher to a side stream (parallel.ShardedMerklePipeline).  "
+                         "0 = one stream")
     ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c5"],
                     help="BASELINE.json config: c4 = headline (default); c1/c2/c3/c5 = single-GPU side benches")
     args = ap.parse_args()
@@ -145,22 +150,7 @@ def main():
     log(f"rank {rank}/{world}: {local_n} items ({nbytes / 2**30:.2f} GiB), shard height {sp.height}, "
         f"nonempty {sp.nonempty}, frontier {k}")
 
-    pipe = None
-    if world == 1 and args.pipeline > 0:
-        from prysm_amd.pipeline import MerklePipeline
-
-        pipe = MerklePipeline(n, item_len, dev, frontier_log2=args.pipeline)
-        k = pipe.k
-        # the pipelined root must equal the one-stream root of the same items
-        want = bytes(D.merkle_hash(items, n, item_len, out=root_buf, ws=ws).cpu().numpy())
-        got = pipe.submit(items)
-        torch.cuda.synchronize()
-        assert bytes(got.cpu().numpy()) == want, "pipelined root differs from merkle_hash"
-        log(f"pipelined: frontier {k} levels below the root, top on a side stream")
-
-    def step():
-        if pipe is not None:
-            return pipe.submit(items)
+    def step_one_stream():
         return P.sharded_merkle_hash(
             items, n, item_len, sp, rank, world,
             subtree_fn=lambda it, sn, il, h, pad: D.merkle_subtree(it, sn, il, h, pad, out=root_buf, ws=ws),
@@ -170,6 +160,33 @@ def main():
             frontier_fn=lambda it, sn, il, h, kk, pad: D.merkle_subtree_frontier(it, sn, il, h, kk, pad,
                                                                                  out=frontier_buf, ws=ws),
             finish_nodes_fn=lambda g, c, nt: D.merkle_finish_nodes(g, c, nt, out=finish_out, ws=finish_ws))
+
+    # --pipeline: everything above the leaf pass of step i runs on a side
+    # stream that overlaps step i+1's leaf pass (N = 1: pipeline.py; N > 1:
+    # node passes, the all-gather and rank 0's finisher, parallel.py)
+    pipe = None
+    if args.pipeline > 0:
+        if world == 1:
+            from prysm_amd.pipeline import MerklePipeline
+
+            pipe = MerklePipeline(n, item_len, dev, frontier_log2=args.pipeline)
+            k = pipe.k
+        else:
+            pipe = P.ShardedMerklePipeline(n, item_len, sp, rank, world, dev, gather_log2=k, workspace=ws)
+            pipe = pipe if pipe.ok else None
+    if pipe is not None:
+        # the pipelined root must equal the one-stream root of the same items
+        want = step_one_stream()
+        torch.cuda.synchronize()
+        want = bytes(want.cpu().numpy()) if want is not None else None
+        got = pipe.submit(items)
+        torch.cuda.synchronize()
+        if rank == 0:
+            assert bytes(got.cpu().numpy()) == want, "pipelined root differs from the one-stream root"
+        log(f"rank {rank}: pipelined (frontier {k}), the levels above the leaf pass on a side stream")
+
+    def step():
+        return pipe.submit(items) if pipe is not None else step_one_stream()
 
     for i in range(args.warmup):
         step()

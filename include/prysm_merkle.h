@@ -101,6 +101,18 @@ int mk_dev_ssz_merkle_subtree(const void* d_shard_items, uint64_t shard_n, uint3
 int mk_dev_ssz_merkle_subtree_frontier(const void* d_shard_items, uint64_t shard_n, uint32_t item_len,
                                        uint32_t height, uint32_t frontier_log2, int pad_at_one, void* d_out,
                                        uint64_t* nodes_out, void* d_ws, uint64_t ws_bytes, void* stream);
+/* The same subtree continued from one of its node levels: `count` 32-B nodes
+ * (a shard's level, e.g. the output of the leaf pass) reduced for `height`
+ * levels with the reference's odd rule (hash.go:225-235; pad_at_one as
+ * above), stopping `frontier_log2` levels below the top (0 = to the top
+ * node).  Lets a rank split its shard into the leaf pass and the narrower
+ * node passes and run the latter on another stream (prysm_amd/parallel.py
+ * ShardedMerklePipeline).  Workspace from
+ * mk_ssz_merkle_node_frontier_workspace_bytes. */
+uint64_t mk_ssz_merkle_node_frontier_workspace_bytes(uint64_t count, uint32_t height, uint32_t frontier_log2);
+int mk_dev_ssz_merkle_node_frontier(const void* d_nodes, uint64_t count, uint32_t height, uint32_t frontier_log2,
+                                    int pad_at_one, void* d_out, uint64_t* nodes_out, void* d_ws,
+                                    uint64_t ws_bytes, void* stream);
 /* Finisher over `count` nodes forming one complete tree level in order (the
  * gathered frontiers): the reference level loop (odd -> 0^128 pad) and
  * Keccak(root || le64(n_total) || 0^24).  Workspace from

@@ -53,6 +53,8 @@ _SIGS = {
     "mk_dev_ssz_merkle_subtree": (_int, [_vp, _u64, _u32, _u32, _int, _vp, _vp, _u64, _vp]),
     "mk_dev_ssz_merkle_finish": (_int, [_vp, _u64, _u64, _vp, _vp]),
     "mk_dev_ssz_merkle_subtree_frontier": (_int, [_vp, _u64, _u32, _u32, _u32, _int, _vp, _vp, _vp, _u64, _vp]),
+    "mk_ssz_merkle_node_frontier_workspace_bytes": (_u64, [_u64, _u32, _u32]),
+    "mk_dev_ssz_merkle_node_frontier": (_int, [_vp, _u64, _u32, _u32, _int, _vp, _vp, _vp, _u64, _vp]),
     "mk_ssz_merkle_finish_workspace_bytes": (_u64, [_u64]),
     "mk_dev_ssz_merkle_finish_nodes": (_int, [_vp, _u64, _u64, _vp, _vp, _u64, _vp]),
     "mk_ssz_merkle_hash_multi": (_int, [_vp, _u64, _u32, _int, _vp]),

@@ -670,6 +670,24 @@ int mk_dev_ssz_merkle_subtree_frontier(const void* d_shard_items, uint64_t shard
                        (hipStream_t)stream);
 }
 
+uint64_t mk_ssz_merkle_node_frontier_workspace_bytes(uint64_t count, uint32_t height, uint32_t frontier_log2) {
+    Plan p;
+    if (make_plan(count, 32, true, height, true, true, p, true, frontier_log2) != MK_OK) return 0;
+    return std::max<uint64_t>(256, plan_ws_bytes(p));
+}
+
+int mk_dev_ssz_merkle_node_frontier(const void* d_nodes, uint64_t count, uint32_t height, uint32_t frontier_log2,
+                                    int pad_at_one, void* d_out, uint64_t* nodes_out, void* d_ws, uint64_t ws_bytes,
+                                    void* stream) {
+    TRY(bind(-1));
+    if (!d_out || !d_nodes || count == 0) return fail(MK_EINVAL, "null pointer or empty level");
+    Plan p;
+    TRY(make_plan(count, 32, true, height, pad_at_one != 0, ((uintptr_t)d_nodes % 16) == 0, p, true,
+                  frontier_log2));
+    if (nodes_out) *nodes_out = frontier_log2 ? p.out_nodes : 1;
+    return launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out, (uint8_t*)d_ws, ws_bytes, (hipStream_t)stream);
+}
+
 uint64_t mk_ssz_merkle_finish_workspace_bytes(uint64_t count) {
     Plan p;
     if (count <= 2 * mk::kWave2Span) return 256;

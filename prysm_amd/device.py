@@ -110,6 +110,29 @@ def merkle_subtree_frontier(items: torch.Tensor, shard_n: int, item_len: int, he
     return out[:32 * nodes]
 
 
+def merkle_node_frontier(nodes: torch.Tensor, count: int, height: int, frontier_log2: int, pad_at_one: bool,
+                         out: torch.Tensor = None, ws: torch.Tensor = None) -> torch.Tensor:
+    """A subtree continued from one of its node levels: `count` 32-B nodes
+    reduced `height` levels (odd rule, hash.go:225-235), stopping
+    `frontier_log2` levels below the top; returns the (nodes*32,) level."""
+    _bind(nodes)
+    lib = _lib.load()
+    want = max(1, -(-count // (1 << (height - frontier_log2)))) if frontier_log2 else 1
+    if out is None:
+        out = torch.empty(32 << frontier_log2, dtype=torch.uint8, device=nodes.device)
+    if out.numel() < 32 * want:
+        raise ValueError("node frontier output buffer too small")
+    if ws is None:
+        ws = torch.empty(max(256, lib.mk_ssz_merkle_node_frontier_workspace_bytes(count, height, frontier_log2)),
+                         dtype=torch.uint8, device=nodes.device)
+    got = ctypes.c_uint64()
+    _lib.check(lib.mk_dev_ssz_merkle_node_frontier(_p(nodes), count, height, frontier_log2, int(pad_at_one), _p(out),
+                                                   ctypes.byref(got), _p(ws), ws.numel(), _stream(nodes.device)),
+               "mk_dev_ssz_merkle_node_frontier")
+    assert got.value == want, (got.value, want)
+    return out[:32 * want]
+
+
 def finish_workspace(count: int, device) -> torch.Tensor:
     return torch.empty(max(256, _lib.load().mk_ssz_merkle_finish_workspace_bytes(count)), dtype=torch.uint8,
                        device=device)

@@ -131,3 +131,109 @@ def frontier_count(shard_n: int, item_len: int, height: int, k: int) -> int:
     cb = (128 // item_len) * item_len if item_len < 128 else item_len
     chunks = -(-shard_n * item_len // cb)
     return max(1, -(-chunks // (1 << (height - k))))
+
+
+class ShardedMerklePipeline:
+    """The sharded merkleHash of a stream of trees (one tree per ``submit``),
+    with everything above each rank's leaf pass moved off the rank's main
+    stream.
+
+    Per tree, on the caller's current stream: the leaf pass of this rank's
+    shard (``frontier_fn`` to the level ``leaf_levels`` above the chunks, the
+    levels one k_reduce leaf pass folds).  On a side stream, overlapping the
+    next tree's leaf pass: the shard's node passes from that level to its
+    frontier ``gather_log2`` levels below the shard root
+    (``node_frontier_fn``), the all-gather of the frontiers (RCCL on the side
+    stream) and, on rank 0, the finisher (``finish_nodes_fn``).  The split
+    levels are the ones ``sharded_merkle_hash`` computes in one piece, so the
+    root is the same.  Buffers are double-buffered like
+    ``pipeline.MerklePipeline``: a submit waits for the side-stream work of
+    the tree submitted two calls earlier; a returned root (rank 0; None
+    elsewhere) stays valid until the submit after next.  Every rank must
+    submit the same sequence of trees (one collective per tree).
+
+    ``ok`` is False when the shard is too small to split (fewer than
+    ``leaf_levels + gather_log2 + 1`` levels): use ``sharded_merkle_hash``.
+    The compute steps are injectable as in ``sharded_merkle_hash``."""
+
+    def __init__(self, n_total: int, item_len: int, sp: ShardPlan, rank: int, world: int, device,
+                 gather_log2: int = 10, leaf_levels: int = 5, group=None,
+                 frontier_fn: Optional[Callable] = None, node_frontier_fn: Optional[Callable] = None,
+                 finish_nodes_fn: Optional[Callable] = None, workspace=None):
+        self.n_total, self.item_len, self.sp = n_total, item_len, sp
+        self.rank, self.world, self.group = rank, world, group
+        self.device = torch.device(device)
+        h = sp.height
+        lo, hi = sp.items(rank)
+        self.sn = hi - lo
+        self.k = gather_log2
+        self.k_leaf = h - leaf_levels  # the leaf pass's output level, counted down from the shard root
+        self.ok = sp.nonempty > 1 and 0 < self.k < self.k_leaf
+        if not self.ok:
+            return
+        self.leaf_count = frontier_count(self.sn, item_len, h, self.k_leaf) if self.sn else 0
+        last = sp.nonempty - 1
+        self.count = (last << self.k) + frontier_count(sp.begin[last + 1] - sp.begin[last], item_len, h, self.k)
+        if frontier_fn is None or node_frontier_fn is None or finish_nodes_fn is None:
+            from . import _lib
+            from . import device as D
+            if workspace is None and self.sn:
+                workspace = D.subtree_workspace(self.sn, item_len, device)
+            nws = torch.empty(max(256, _lib.load().mk_ssz_merkle_node_frontier_workspace_bytes(
+                max(self.leaf_count, 1), self.k_leaf, self.k)), dtype=torch.uint8, device=device)
+            fws = D.finish_workspace(self.count, device) if rank == 0 else None
+            frontier_fn = frontier_fn or (lambda it, sn, il, hh, kk, pad, out: D.merkle_subtree_frontier(
+                it, sn, il, hh, kk, pad, out=out, ws=workspace))
+            node_frontier_fn = node_frontier_fn or (lambda nodes, cnt, hh, kk, pad, out: D.merkle_node_frontier(
+                nodes, cnt, hh, kk, pad, out=out, ws=nws))
+            finish_nodes_fn = finish_nodes_fn or (lambda g, c, nt, out: D.merkle_finish_nodes(g, c, nt, out=out,
+                                                                                               ws=fws))
+        self.frontier_fn, self.node_frontier_fn, self.finish_nodes_fn = frontier_fn, node_frontier_fn, finish_nodes_fn
+        block = 32 << self.k
+        dev = self.device
+        self.levels = [torch.empty(32 << self.k_leaf, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.blocks = [torch.zeros(block, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.gathered = [torch.empty(world * block, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.outs = [torch.empty(32, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.cuda = dev.type == "cuda"
+        self.side = torch.cuda.Stream(device=dev) if self.cuda else None
+        self._done = [None, None]
+        self._i = 0
+
+    def submit(self, local_items: torch.Tensor) -> Optional[torch.Tensor]:
+        slot = self._i & 1
+        self._i += 1
+        cur = torch.cuda.current_stream(self.device) if self.cuda else None
+        if self.cuda and self._done[slot] is not None:  # side work of two trees back reads this slot
+            cur.wait_event(self._done[slot])
+        level = None
+        if self.sn:
+            level = self.frontier_fn(local_items, self.sn, self.item_len, self.sp.height, self.k_leaf, True,
+                                     self.levels[slot])
+        if self.cuda:
+            self.side.wait_stream(cur)
+            with torch.cuda.stream(self.side):
+                root = self._top(level, slot)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+            self._done[slot] = ev
+            return root
+        return self._top(level, slot)
+
+    def _top(self, level, slot):
+        blk = self.blocks[slot]
+        if level is not None:
+            fr = self.node_frontier_fn(level, self.leaf_count, self.k_leaf, self.k, True, blk)
+            if fr.data_ptr() != blk.data_ptr() or fr.numel() > blk.numel():
+                blk[:fr.numel()].copy_(fr)
+        # (an empty shard sends its zero block; only the counted nodes are read)
+        g = self.gathered[slot]
+        if blk.is_cuda and dist.get_backend(self.group) == "gloo":  # one-GPU rehearsal: gloo gathers host tensors
+            host = torch.empty(g.numel(), dtype=torch.uint8)
+            dist.all_gather_into_tensor(host, blk.cpu(), group=self.group)
+            g.copy_(host)
+        else:
+            dist.all_gather_into_tensor(g, blk, group=self.group)
+        if self.rank == 0:
+            return self.finish_nodes_fn(g, self.count, self.n_total, self.outs[slot])
+        return None

@@ -36,7 +36,7 @@ def _plan_cpu(n, item_len, world):
     return h, ne, [min(n, s * (1 << h) * per) for s in range(world + 1)]
 
 
-def _worker(rank, world, port, n, item_len, q, frontier=0):
+def _worker(rank, world, port, n, item_len, q, frontier=0, pipe=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -77,6 +77,26 @@ def _worker(rank, world, port, n, item_len, q, frontier=0):
         def finish_nodes(g, count, nt):
             return finish(g, count, nt)
 
+        if pipe is not None:  # (gather_log2, leaf_levels): ShardedMerklePipeline over 3 submitted trees
+            def node_frontier(level, cnt, hh, kk, pad, out):
+                nodes = [bytes(level[32 * i:32 * i + 32].numpy()) for i in range(cnt)]
+                for _ in range(hh - kk):  # the odd rule incl. a lone node (pad_at_one)
+                    if len(nodes) % 2:
+                        nodes = nodes + [bytes(128)]
+                    nodes = [O.keccak256(nodes[i] + nodes[i + 1]) for i in range(0, len(nodes), 2)]
+                return torch.frombuffer(bytearray(b"".join(nodes)), dtype=torch.uint8)
+
+            pl = P.ShardedMerklePipeline(
+                n, item_len, sp, rank, world, "cpu", gather_log2=pipe[0], leaf_levels=pipe[1],
+                frontier_fn=lambda it, sn, il, h, k, pad, out: frontier_fn(it, sn, il, h, k, pad),
+                node_frontier_fn=node_frontier,
+                finish_nodes_fn=lambda g, c, nt, out: finish_nodes(g, c, nt))
+            assert pl.ok
+            roots = [pl.submit(local) for _ in range(3)]
+            if rank == 0:
+                assert len({bytes(r.numpy()) for r in roots}) == 1
+                q.put(bytes(roots[-1].numpy()))
+            return
         root = P.sharded_merkle_hash(local, n, item_len, sp, rank, world, subtree_fn=subtree, full_fn=full_fn,
                                      finish_fn=finish, frontier_log2=frontier, frontier_fn=frontier_fn,
                                      finish_nodes_fn=finish_nodes)
@@ -114,6 +134,27 @@ def test_frontier_sharded_root_equals_full_root(world, n, k):
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, n, 32, q, k)) for r in range(world)]
+    for p in procs:
+        p.start()
+    root = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert root == O.merkle_hash_gen(n, 32, SEED)
+
+
+@pytest.mark.parametrize("world,n,k,leaf", [(2, 1 << 14, 3, 5), (2, 4 * 1000 + 3, 2, 3), (4, 4 * 3000 + 3, 2, 5),
+                                            (4, 1 << 14, 1, 5)])
+def test_pipelined_sharded_root_equals_full_root(world, n, k, leaf):
+    """ShardedMerklePipeline: leaf pass to `leaf` levels above the chunks,
+    node passes to the 2^k frontier, all-gather and rank-0 finish split off
+    per tree (ragged last shards included)."""
+    from oracle import oracle as O
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, 32, q, 0, (k, leaf))) for r in range(world)]
     for p in procs:
         p.start()
     root = q.get(timeout=120)

@@ -237,6 +237,40 @@ def test_frontier_sharding_equals_full(gpu, n, world, k):
     assert bytes(root.cpu().numpy()) == O.merkle_hash_gen(n, item_len, SEED + 33, nthreads=16)
 
 
+@pytest.mark.parametrize("n,world,k,leaf", [(1 << 20, 8, 8, 5), ((1 << 20) + 12, 8, 5, 5), (999_999, 3, 8, 5),
+                                            (41 * 4 + 3, 4, 1, 2), (1 << 22, 4, 10, 5), ((1 << 22) - 5, 4, 3, 4),
+                                            (1 << 25, 8, 10, 5)])
+def test_split_shard_frontier_equals_one_piece(gpu, n, world, k, leaf):
+    """ShardedMerklePipeline's split of a shard: the leaf pass to `leaf`
+    levels above the chunks, then mk_dev_ssz_merkle_node_frontier from that
+    level to the 2^k frontier, equals the one-piece frontier of every shard
+    (ragged last shards, lone nodes under pad_at_one)."""
+    import torch
+
+    from prysm_amd import device as D
+
+    item_len = 32
+    h, ne, begin = D.shard_plan(n, item_len, world)
+    assert ne > 1 and 0 < k < h - leaf
+    items = torch.empty(n * item_len, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 35)
+    for s in range(ne):
+        sn = begin[s + 1] - begin[s]
+        it = items[begin[s] * item_len:begin[s + 1] * item_len]
+        one = D.merkle_subtree_frontier(it, sn, item_len, h, k, True)
+        lvl = D.merkle_subtree_frontier(it, sn, item_len, h, h - leaf, True)
+        two = D.merkle_node_frontier(lvl, lvl.numel() // 32, h - leaf, k, True)
+        torch.cuda.synchronize()
+        assert torch.equal(one, two), (s, one.numel(), two.numel())
+    # frontier 0: the node levels all the way to the shard root
+    sn = begin[1] - begin[0]
+    lvl = D.merkle_subtree_frontier(items[:sn * item_len], sn, item_len, h, h - leaf, True)
+    top = D.merkle_node_frontier(lvl, lvl.numel() // 32, h - leaf, 0, True)
+    root = D.merkle_subtree(items[:sn * item_len], sn, item_len, h, True)
+    torch.cuda.synchronize()
+    assert torch.equal(top, root)
+
+
 @pytest.mark.parametrize("n,item_len,k", [(1 << 20, 32, 12), ((1 << 20) + 3, 32, 12), (3_000_017, 32, 16),
                                           (3_000_017, 32, 21), (100_003, 8, 8), (1000, 32, 21), (5, 32, 4),
                                           (777, 200, 3)])
