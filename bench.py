@@ -10,8 +10,8 @@ reduces its shard to the level 10 below its shard root (1024 nodes, the
 levels and the length mix-in on a side stream that overlaps its next step.
 With --pipeline (default) everything above the leaf pass runs on a side
 stream that overlaps the next step's leaf pass: at N = 1 the node passes and
-the length mix-in (prysm_amd/pipeline.py, split 21 levels below the root =
-the leaf pass's output level); at N > 1 each rank's node passes down to its
+the length mix-in (prysm_amd/pipeline.py, split at the leaf pass's output
+level, 21 below the root at 2^28); at N > 1 each rank's node passes down to its
 frontier, the all-gather and rank 0's finisher (parallel.ShardedMerklePipeline).
 The pipelined root is checked against the one-stream root before timing, and
 every step's work completes inside the timed region.  Inputs are generated on the device before timing and
@@ -90,12 +90,11 @@ def main():
     ap.add_argument("--frontier", type=int, default=10,
                     help="N>1: each rank gathers its tree level this many levels below its shard root "
                          "(2^k nodes) and rank 0 finishes the top (0 = gather the 32-B shard roots)")
-    ap.add_argument("--pipeline", type=int, default=21,
-                    help="N=1: split each tree this many levels below its root (21 = the leaf pass's output "
-                         "level at 2^28); the top runs on a side stream overlapping the next step's leaf pass "
-                         "(prysm_amd/pipeline.py).  N>1: any value > 0 moves each rank's node passes, the "
-                         "all-gather and rank 0's finisher to a side stream (parallel.ShardedMerklePipeline).  "
-                         "0 = one stream")
+    ap.add_argument("--pipeline", type=int, default=1, choices=[0, 1],
+                    help="1: everything above the leaf pass (5 levels above the chunks) runs on a side stream "
+                         "overlapping the next step's leaf pass: N=1 the node passes and the length mix-in "
+                         "(prysm_amd/pipeline.py), N>1 each rank's node passes, the all-gather and rank 0's "
+                         "finisher (parallel.ShardedMerklePipeline).  0 = one stream")
     ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c5"],
                     help="BASELINE.json config: c4 = headline (default); c1/c2/c3/c5 = single-GPU side benches")
     args = ap.parse_args()
@@ -169,7 +168,7 @@ def main():
         if world == 1:
             from prysm_amd.pipeline import MerklePipeline
 
-            pipe = MerklePipeline(n, item_len, dev, frontier_log2=args.pipeline)
+            pipe = MerklePipeline(n, item_len, dev)
             k = pipe.k
         else:
             pipe = P.ShardedMerklePipeline(n, item_len, sp, rank, world, dev, gather_log2=k, workspace=ws)

@@ -20,6 +20,8 @@ make the consuming stream wait on ``side`` before reading it.
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 
 from . import device as D
@@ -27,11 +29,16 @@ from .parallel import frontier_count
 
 
 class MerklePipeline:
-    def __init__(self, n: int, item_len: int, device, frontier_log2: int = 21):
+    def __init__(self, n: int, item_len: int, device, frontier_log2: Optional[int] = None, leaf_levels: int = 5):
+        """Split ``frontier_log2`` levels below the root; by default at the
+        leaf pass's output level, ``leaf_levels`` above the chunks (21 below
+        the root of a 2^28-item tree of 32-B items)."""
         self.n, self.item_len = n, item_len
         self.device = torch.device(device)
         height, _, _ = D.shard_plan(n, item_len, 1)
         self.height = height
+        if frontier_log2 is None:
+            frontier_log2 = height - leaf_levels
         k = min(frontier_log2, height - 2)  # the planner's throughput passes fold at least 2 levels
         # a frontier level of one node is already the tree root's input: no top to split off
         self.k = k if k > 0 and frontier_count(n, item_len, height, k) > 1 else 0

@@ -273,7 +273,7 @@ def test_split_shard_frontier_equals_one_piece(gpu, n, world, k, leaf):
 
 @pytest.mark.parametrize("n,item_len,k", [(1 << 20, 32, 12), ((1 << 20) + 3, 32, 12), (3_000_017, 32, 16),
                                           (3_000_017, 32, 21), (100_003, 8, 8), (1000, 32, 21), (5, 32, 4),
-                                          (777, 200, 3)])
+                                          (777, 200, 3), (1 << 22, 32, None), ((1 << 22) + 9, 32, None)])
 def test_pipeline_roots_equal_merkle_hash(gpu, n, item_len, k):
     """MerklePipeline (leaf side on the current stream, top on a side stream
     overlapping the next tree) over 5 consecutive trees of one shape: every
