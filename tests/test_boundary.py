@@ -91,6 +91,19 @@ def test_workspace_sizing(lib):
     assert lib.mk_deposit_trie_levels_bytes(5, 2) == 32 * (5 + 3 + 2)
 
 
+def test_node_frontier_planner(lib):
+    """mk_dev_ssz_merkle_node_frontier's planner (no GPU needed for the
+    workspace query): the per-rank split of the 8-GPU C4 shard (2^18 leaf-pass
+    nodes, 18 levels to the shard root, frontier 10) plans; a frontier at or
+    above the top, or more nodes than the height allows, does not."""
+    assert lib.mk_ssz_merkle_node_frontier_workspace_bytes(1 << 18, 18, 10) >= 256
+    assert lib.mk_ssz_merkle_node_frontier_workspace_bytes(1 << 18, 18, 0) >= 256
+    assert lib.mk_ssz_merkle_node_frontier_workspace_bytes((1 << 18) - 7, 18, 10) >= 256  # ragged shard
+    assert lib.mk_ssz_merkle_node_frontier_workspace_bytes(1, 18, 10) >= 256  # lone node (pad_at_one)
+    assert lib.mk_ssz_merkle_node_frontier_workspace_bytes(1 << 18, 18, 18) == 0
+    assert lib.mk_ssz_merkle_node_frontier_workspace_bytes((1 << 18) + 1, 18, 10) == 0
+
+
 def test_oracle_is_not_imported_by_product():
     """The product package never touches oracle/ (it is test infrastructure)."""
     pkg = os.path.join(ROOT, "prysm_amd")
