@@ -4,8 +4,9 @@ the same seeded synthetic inputs bench.py measures, checked bit-exactly.
 
   c2  2^24 x 64-B Hash           (Keccak-256 of the 2^24 digests)
   c3  1,000,000-validator State  (registry root, balances root, state root)
-  c4  2^28 x 32-B merkleHash     (8 GiB on the device), unsharded and as
-      8 frontier shards finished on one device
+  c4  2^28 x 32-B merkleHash     (8 GiB on the device), unsharded, as
+      8 frontier shards finished on one device (one-piece and split per
+      shard), and pipelined (bench.py's N=1 path)
   c5  2^20-deposit trie root
 """
 import json
@@ -53,6 +54,22 @@ def test_c4_full_2p28(gpu):
     root2 = D.merkle_finish_nodes(level, count, n)
     torch.cuda.synchronize()
     assert bytes(root2.cpu().numpy()).hex() == g["root"]
+    # the 8-GPU per-rank split of ShardedMerklePipeline on one device: every
+    # shard's leaf pass (5 levels), then its node passes to the frontier
+    for s in range(ne):
+        sn = begin[s + 1] - begin[s]
+        lvl = D.merkle_subtree_frontier(items[begin[s] * il:begin[s + 1] * il], sn, il, h, h - 5, True, ws=ws)
+        D.merkle_node_frontier(lvl, lvl.numel() // 32, h - 5, k, True, out=level[s << (k + 5):(s + 1) << (k + 5)])
+    root3 = D.merkle_finish_nodes(level, count, n)
+    torch.cuda.synchronize()
+    assert bytes(root3.cpu().numpy()).hex() == g["root"]
+    # bench.py's N=1 path: pipelined back-to-back trees (top on a side stream)
+    from prysm_amd.pipeline import MerklePipeline
+
+    pipe = MerklePipeline(n, il, gpu)
+    roots = [pipe.submit(items), pipe.submit(items)]
+    torch.cuda.synchronize()
+    assert pipe.k == 21 and [bytes(r.cpu().numpy()).hex() for r in roots] == [g["root"]] * 2
     del items
 
 
