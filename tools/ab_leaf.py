@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--trie", action="store_true", help="A/B the depth-32 deposit trie over 2^log2n x 280-B deposits")
     ap.add_argument("--struct", action="store_true", help="A/B the typed registry root of 1,000,000 validators")
+    ap.add_argument("--c2", action="store_true", help="A/B the batched Keccak of 2^log2n x 64-B messages")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -49,6 +50,8 @@ def main():
         return ab_trie(a, libs, dev)
     if a.struct:
         return ab_struct(a, libs, dev)
+    if a.c2:
+        return ab_c2(a, libs, dev)
     n, il = 1 << a.log2n, a.item_len
     items = torch.empty(n * il, dtype=torch.uint8, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -152,6 +155,34 @@ def ab_struct(a, libs, dev):
         print(json.dumps({"variant": v, "struct_n": n, "median_ms": statistics.median(times[v]),
                           "min_ms": min(times[v])}))
     print(json.dumps({"root": next(iter(roots.values()), None)}))
+
+
+
+def ab_c2(a, libs, dev):
+    import torch
+
+    n = 1 << a.log2n
+    msgs = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    first = libs[a.variants[0]]
+    assert first.mk_dev_synth_fill(ctypes.c_void_p(msgs.data_ptr()), n * 64, 0x5EED000000000002, 0, st) == 0
+    outs = {v: torch.empty(n * 32, dtype=torch.uint8, device=dev) for v in a.variants}
+    times = {v: [] for v in a.variants}
+    for r in range(a.rounds + 1):
+        for v, L in libs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = L.mk_dev_hash_batch(ctypes.c_void_p(msgs.data_ptr()), n, 64, ctypes.c_void_p(outs[v].data_ptr()), st)
+            e1.record()
+            torch.cuda.synchronize()
+            assert rc == 0, (v, rc)
+            if r:
+                times[v].append(e0.elapsed_time(e1))
+    ref = next(iter(outs.values()))
+    assert all(torch.equal(ref, o) for o in outs.values())
+    for v in a.variants:
+        print(json.dumps({"variant": v, "c2_log2n": a.log2n, "median_ms": statistics.median(times[v]),
+                          "min_ms": min(times[v]), "hashes_per_s": n / (statistics.median(times[v]) / 1e3)}))
 
 
 if __name__ == "__main__":
