@@ -180,9 +180,17 @@ def main():
         want = bytes(want.cpu().numpy()) if want is not None else None
         got = pipe.submit(items)
         torch.cuda.synchronize()
-        if rank == 0:
-            assert bytes(got.cpu().numpy()) == want, "pipelined root differs from the one-stream root"
-        log(f"rank {rank}: pipelined (frontier {k}), the levels above the leaf pass on a side stream")
+        same = torch.ones(1, dtype=torch.int32, device=dev if args.backend == "nccl" else "cpu")
+        if rank == 0 and bytes(got.cpu().numpy()) != want:
+            same.zero_()
+        if world > 1:  # every rank takes the same path
+            dist.all_reduce(same, op=dist.ReduceOp.MIN)
+        if same.item():
+            log(f"rank {rank}: pipelined (frontier {k}), the levels above the leaf pass on a side stream")
+        else:  # never expected (tests pin the split); measure the one-stream path and say so in the JSON
+            log(f"rank {rank}: ERROR pipelined root differs from the one-stream root; timing one stream")
+            pipe = None
+            k = args.frontier if sp.nonempty > 1 and 0 < args.frontier < sp.height - 4 else 0
 
     def step():
         return pipe.submit(items) if pipe is not None else step_one_stream()
