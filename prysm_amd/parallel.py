@@ -168,7 +168,8 @@ class ShardedMerklePipeline:
         self.sn = hi - lo
         self.k = gather_log2
         self.k_leaf = h - leaf_levels  # the leaf pass's output level, counted down from the shard root
-        self.ok = sp.nonempty > 1 and 0 < self.k < self.k_leaf
+        # the planner's leaf pass folds at least 2 levels (window + pair)
+        self.ok = sp.nonempty > 1 and leaf_levels >= 2 and 0 < self.k < self.k_leaf
         if not self.ok:
             return
         self.leaf_count = frontier_count(self.sn, item_len, h, self.k_leaf) if self.sn else 0
@@ -224,7 +225,7 @@ class ShardedMerklePipeline:
         blk = self.blocks[slot]
         if level is not None:
             fr = self.node_frontier_fn(level, self.leaf_count, self.k_leaf, self.k, True, blk)
-            if fr.data_ptr() != blk.data_ptr() or fr.numel() > blk.numel():
+            if fr.data_ptr() != blk.data_ptr():  # an injected step may return its own buffer
                 blk[:fr.numel()].copy_(fr)
         # (an empty shard sends its zero block; only the counted nodes are read)
         g = self.gathered[slot]
