@@ -59,19 +59,21 @@ def cpu_baseline(item_len: int, log2n_sample: int):
                       f"(same SplitMix64 stream), 1 thread, {dt:.1f} s"}
 
 
-def load_pmc_traffic():
-    """HBM bytes per leaf-kernel launch from the committed rocprofv3 PMC
-    summary (profiles/*_pmc.json written by tools/pmc_summary.py), if any."""
+def load_pmc():
+    """(HBM bytes per leaf-kernel launch, effective clock GHz under that load)
+    from the newest committed rocprofv3 PMC summary (profiles/*_pmc.json,
+    written by tools/pmc_summary.py), or (None, None)."""
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     if not files:
-        return None
+        return None, None
     try:
         with open(files[-1]) as f:
-            return json.load(f).get("hbm_bytes_per_leaf_launch")
+            d = json.load(f)
+        return d.get("hbm_bytes_per_leaf_launch"), d.get("effective_clock_GHz")
     except Exception:
-        return None
+        return None, None
 
 
 def main():
@@ -235,7 +237,7 @@ def main():
         hashes_per_launch = leaf_hashes / max(leaf_launches, 1)
         ops_per_launch = perms_per_launch * INT_OPS_PER_PERM - hashes_per_launch * INT_OPS_SAVED_PER_HASH
         achieved = ops_per_launch / avg_leaf_s if avg_leaf_s > 0 else 0.0
-        traffic = load_pmc_traffic() if world == 1 and args.log2n == 28 else None
+        traffic, clk = load_pmc() if world == 1 and args.log2n == 28 else (None, None)
         out = {
             "metric": "tree-hash leaves/sec @2^28 chunks (ssz.merkleHash, 32-B leaves)",
             "value": value,
@@ -262,6 +264,9 @@ def main():
                 "unit": "Tops/s (int32 VALU)",
                 "frac": achieved / PEAK_INT_OPS,
                 "traffic": traffic,
+                # also against the sustained clock the PMC run measured under this load
+                "effective_clock_GHz": clk,
+                "frac_at_effective_clock": achieved / (PEAK_INT_OPS / 2.4 * clk) if clk else None,
                 "perms_per_launch": perms_per_launch,
                 "hashes_per_launch": hashes_per_launch,
                 "avg_launch_ms": avg_leaf_s * 1e3,
