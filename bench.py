@@ -44,19 +44,20 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(item_len: int, log2n_sample: int):
-    """The oracle (a C port of hash.go:194-239, 1 thread = the reference's
-    single-goroutine shape) on a bounded sample of the same workload."""
+def cpu_baseline(item_len: int, log2n_sample: int, threads: int = 1):
+    """The oracle (a C port of hash.go:194-239; 1 thread = the reference's
+    single-goroutine shape, more threads split the tree by subtrees) on a
+    bounded sample of the same workload."""
     from oracle import oracle as O
 
     n = 1 << log2n_sample
     items = O.splitmix_bytes(n * item_len, SEED)
     t0 = time.perf_counter()
-    O.merkle_hash_flat(items, n, item_len, nthreads=1)
+    O.merkle_hash_flat(items, n, item_len, nthreads=threads)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "leaves/s", "cores": 1, "kind": "port",
+    return {"value": n / dt, "unit": "leaves/s", "cores": threads, "kind": "port",
             "sample": f"oracle/merkle_ref.c or_merkle_hash, 2^{log2n_sample} x {item_len}-B items "
-                      f"(same SplitMix64 stream), 1 thread, {dt:.1f} s"}
+                      f"(same SplitMix64 stream), {threads} thread{'s' if threads > 1 else ''}, {dt:.1f} s"}
 
 
 def load_pmc():
@@ -276,6 +277,9 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline ...")
             out["cpu_baseline"] = cpu_baseline(item_len, args.cpu_sample_log2n)
+            # also the restatement on the host's share of cores (16 on the GPU box)
+            nt = min(16, len(os.sched_getaffinity(0)))
+            out["cpu_baseline_threads"] = cpu_baseline(item_len, args.cpu_sample_log2n, threads=nt)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
