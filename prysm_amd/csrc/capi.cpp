@@ -105,6 +105,10 @@ struct DevCtx {
     std::mutex side_mu;
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    // host-buffer entries: records copied in chunks on `copy` while the
+    // compute stream hashes the previous chunk (guarded by `mu`)
+    hipStream_t copy = nullptr;
+    hipEvent_t h2d = nullptr;
 };
 
 std::mutex g_mu;
@@ -140,7 +144,9 @@ int bind(int dev) {
             if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
                 hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
                 hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess) {
+                hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
+                hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&c->h2d, hipEventDisableTiming) != hipSuccess) {
                 delete c;
                 return fail(MK_EHIP, "stream/event creation failed on device %d", dev);
             }
@@ -889,6 +895,15 @@ extern "C" uint64_t mk_ssz_struct_msg_len(const mk_field* fields, uint32_t nfiel
 }
 
 static uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+// host-buffer entries: H2D in up to kH2dChunks pieces of at least kH2dMinChunk records
+#ifndef MK_H2D_CHUNKS
+#define MK_H2D_CHUNKS 8
+#endif
+#ifndef MK_H2D_MIN_CHUNK
+#define MK_H2D_MIN_CHUNK 65536
+#endif
+constexpr uint64_t kH2dChunks = MK_H2D_CHUNKS;
+constexpr uint64_t kH2dMinChunk = MK_H2D_MIN_CHUNK;
 
 extern "C" uint64_t mk_ssz_struct_list_workspace_bytes(uint64_t n, const mk_field* fields, uint32_t nfields) {
     mk::StructSpec sp;
@@ -943,8 +958,26 @@ extern "C" int mk_ssz_struct_list_root(const uint8_t* records, uint64_t n, uint3
     TRY(grow(L.c->in, n * (size_t)record_len));
     TRY(grow(L.c->ws, wsb));
     TRY(grow(L.c->out, 32));
-    if (n) HIPCHK(hipMemcpyAsync(L.c->in.p, records, n * (size_t)record_len, hipMemcpyHostToDevice, st));
-    TRY(mk_dev_ssz_struct_list_root(L.c->in.p, n, record_len, fields, nfields, L.c->out.p, L.c->ws.p, wsb, st));
+    // Same layout as mk_dev_ssz_struct_list_root.  The records cross PCIe in
+    // chunks on the copy stream; the struct-roots kernel of chunk i runs on
+    // the compute stream while chunk i+1 is in flight, so only the last
+    // chunk's roots and the list merkleHash follow the copy.
+    uint8_t* ws = (uint8_t*)L.c->ws.p;
+    uint8_t* msg = ws;
+    uint8_t* roots = ws + align256(n * sp.msg_len);
+    uint8_t* mws = roots + align256(32 * n);
+    const uint8_t* din = (const uint8_t*)L.c->in.p;
+    uint64_t chunk = std::max<uint64_t>(kH2dMinChunk, ceil_div(n, kH2dChunks));
+    chunk = (chunk + 15) & ~15ull;  // chunk starts keep the records' 16-B alignment
+    for (uint64_t off = 0; off < n; off += chunk) {
+        const uint64_t cnt = std::min(chunk, n - off);
+        HIPCHK(hipMemcpyAsync((uint8_t*)L.c->in.p + off * record_len, records + off * record_len,
+                              cnt * (size_t)record_len, hipMemcpyHostToDevice, L.c->copy));
+        HIPCHK(hipEventRecord(L.c->h2d, L.c->copy));
+        HIPCHK(hipStreamWaitEvent(st, L.c->h2d, 0));
+        TRY(launch_struct_roots(din + off * record_len, cnt, sp, msg + off * sp.msg_len, roots + 32 * off, st));
+    }
+    TRY(mk_dev_ssz_merkle_hash(roots, n, 32, L.c->out.p, mws, wsb - (uint64_t)(mws - ws), st));
     HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return MK_OK;

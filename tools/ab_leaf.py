@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--trie", action="store_true", help="A/B the depth-32 deposit trie over 2^log2n x 280-B deposits")
     ap.add_argument("--struct", action="store_true", help="A/B the typed registry root of 1,000,000 validators")
     ap.add_argument("--c2", action="store_true", help="A/B the batched Keccak of 2^log2n x 64-B messages")
+    ap.add_argument("--host-struct", type=int, default=0,
+                    help="A/B mk_ssz_struct_list_root from host records (this many validators)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -52,6 +54,8 @@ def main():
         return ab_struct(a, libs, dev)
     if a.c2:
         return ab_c2(a, libs, dev)
+    if a.host_struct:
+        return ab_host_struct(a, libs)
     n, il = 1 << a.log2n, a.item_len
     items = torch.empty(n * il, dtype=torch.uint8, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -183,6 +187,39 @@ def ab_c2(a, libs, dev):
     for v in a.variants:
         print(json.dumps({"variant": v, "c2_log2n": a.log2n, "median_ms": statistics.median(times[v]),
                           "min_ms": min(times[v]), "hashes_per_s": n / (statistics.median(times[v]) / 1e3)}))
+
+
+def ab_host_struct(a, libs):
+    """Host-buffer TreeHash of a synthetic registry (H2D + struct kernel +
+    merkleHash + D2H in one library call), wall time per call."""
+    import time
+
+    import numpy as np
+
+    from prysm_amd import registry as R
+
+    n = a.host_struct
+    reg = R.synthetic_registry(n, 0x5EED000000000001)
+    rec = np.ascontiguousarray(reg.records)
+    raw = rec.view(np.uint8).reshape(-1)
+    f = R._fields(R.VALIDATOR_FIELDS)
+    times = {v: [] for v in a.variants}
+    roots = {}
+    for r in range(a.rounds + 1):
+        for v, L in libs.items():
+            out = ctypes.create_string_buffer(32)
+            t0 = time.perf_counter()
+            rc = L.mk_ssz_struct_list_root(raw.ctypes.data_as(ctypes.c_void_p), n, rec.dtype.itemsize, f,
+                                           len(R.VALIDATOR_FIELDS), out)
+            dt = time.perf_counter() - t0
+            assert rc == 0, (v, rc)
+            roots[v] = out.raw
+            if r:
+                times[v].append(dt * 1e3)
+    assert len(set(roots.values())) == 1, roots
+    for v in a.variants:
+        print(json.dumps({"variant": v, "host_struct_n": n, "median_ms": statistics.median(times[v]),
+                          "min_ms": min(times[v])}))
 
 
 if __name__ == "__main__":
