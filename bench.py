@@ -147,7 +147,7 @@ def main():
     finish_out = torch.empty(32, dtype=torch.uint8, device=dev)
     finish_ws = D.finish_workspace(world << k, dev) if k and rank == 0 else None
     # rank 0 finishes the top levels on a side stream, overlapping its next step
-    finish_stream = torch.cuda.Stream(device=dev) if world > 1 and rank == 0 else None
+    finish_stream = torch.cuda.Stream(device=dev, priority=-1) if world > 1 and rank == 0 else None
     torch.cuda.synchronize()
     log(f"rank {rank}/{world}: {local_n} items ({nbytes / 2**30:.2f} GiB), shard height {sp.height}, "
         f"nonempty {sp.nonempty}, frontier {k}")

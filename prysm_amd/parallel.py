@@ -197,7 +197,8 @@ class ShardedMerklePipeline:
         self.gathered = [torch.empty(world * block, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.outs = [torch.empty(32, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.cuda = dev.type == "cuda"
-        self.side = torch.cuda.Stream(device=dev) if self.cuda else None
+        # high priority = its own hardware queue (see MerklePipeline)
+        self.side = torch.cuda.Stream(device=dev, priority=-1) if self.cuda else None
         self._done = [None, None]
         self._i = 0
 

@@ -49,7 +49,11 @@ class MerklePipeline:
             self.count = frontier_count(n, item_len, height, self.k)
             self.bufs = [torch.empty(32 << self.k, dtype=torch.uint8, device=self.device) for _ in range(2)]
             self.fin_ws = D.finish_workspace(self.count, self.device)
-            self.side = torch.cuda.Stream(device=self.device)
+            # high priority: a default-priority side stream can land on the
+            # current stream's hardware queue and serialise behind the next
+            # leaf pass (rocprofv3: same Queue_Id); a priority stream gets
+            # its own queue
+            self.side = torch.cuda.Stream(device=self.device, priority=-1)
         else:
             self.side = torch.cuda.current_stream(self.device)
         self._done = [None, None]
