@@ -19,6 +19,10 @@ namespace {
 using mk::ReduceArgs;
 using mk::kReduceThreads;
 
+#ifndef MK_SIDE_PRIO
+#define MK_SIDE_PRIO 1
+#endif
+constexpr bool kSidePrio = MK_SIDE_PRIO != 0;  // library side/copy streams at high priority
 #ifndef MK_WAVE2
 #define MK_WAVE2 1
 #endif
@@ -141,11 +145,16 @@ int bind(int dev) {
         std::lock_guard<std::mutex> lk(g_mu);
         if (!g_ctx[dev]) {
             auto* c = new DevCtx();
+            // side/copy streams at the highest priority: a default-priority
+            // stream can share the caller's hardware queue (GPU_MAX_HW_QUEUES=4)
+            // and then runs after, not beside, the work it should overlap
+            int lo = 0, hi = 0;
+            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess || !kSidePrio) hi = lo = 0;
             if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-                hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) != hipSuccess ||
                 hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
-                hipStreamCreateWithFlags(&c->copy, hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, hi) != hipSuccess ||
                 hipEventCreateWithFlags(&c->h2d, hipEventDisableTiming) != hipSuccess) {
                 delete c;
                 return fail(MK_EHIP, "stream/event creation failed on device %d", dev);
