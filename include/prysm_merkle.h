@@ -150,6 +150,13 @@ uint64_t mk_ssz_struct_msg_len(const mk_field* fields, uint32_t nfields);
 /* roots of n records -> n x 32 bytes (one struct hash per record). */
 int mk_ssz_struct_roots(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
                         uint32_t nfields, uint8_t* roots);
+/* Device-resident struct roots (makeStructHasher per element,
+ * hash.go:141-159): n records -> d_roots (n x 32) on `stream`; d_ws of at
+ * least n * mk_ssz_struct_msg_len bytes.  Lets a caller run the list's
+ * merkleHash on another stream (a stream of states: struct roots of state
+ * i+1 overlap the merkle top of state i). */
+int mk_dev_ssz_struct_roots(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
+                            uint32_t nfields, void* d_roots, void* d_ws, uint64_t ws_bytes, void* stream);
 /* TreeHash of a list of such structs: merkleHash over the n struct roots. */
 uint64_t mk_ssz_struct_list_workspace_bytes(uint64_t n, const mk_field* fields, uint32_t nfields);
 int mk_dev_ssz_struct_list_root(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,

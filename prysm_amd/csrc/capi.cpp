@@ -936,6 +936,18 @@ extern "C" int mk_dev_ssz_struct_list_root(const void* d_records, uint64_t n, ui
     return mk_dev_ssz_merkle_hash(roots, n, 32, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), stream);
 }
 
+extern "C" int mk_dev_ssz_struct_roots(const void* d_records, uint64_t n, uint32_t record_len,
+                                       const mk_field* fields, uint32_t nfields, void* d_roots, void* d_ws,
+                                       uint64_t ws_bytes, void* stream) {
+    TRY(bind(-1));
+    mk::StructSpec sp;
+    TRY(make_spec(fields, nfields, record_len, sp));
+    if (n && (!d_records || !d_roots)) return fail(MK_EINVAL, "null pointer");
+    if (ws_bytes < n * (uint64_t)sp.msg_len) return fail(MK_ENOMEM, "workspace too small");
+    TRY(launch_struct_roots(d_records, n, sp, d_ws, d_roots, (hipStream_t)stream));
+    return MK_OK;
+}
+
 extern "C" int mk_ssz_struct_roots(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
                                    uint32_t nfields, uint8_t* roots) {
     mk::StructSpec sp;

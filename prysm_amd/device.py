@@ -37,6 +37,28 @@ def synth_fill(dst: torch.Tensor, seed: int, word0: int = 0) -> torch.Tensor:
     return dst
 
 
+def struct_roots(records: torch.Tensor, n: int, record_len: int, spec, out: torch.Tensor = None,
+                 ws: torch.Tensor = None) -> torch.Tensor:
+    """Struct root of each of n records (makeStructHasher per element,
+    shared/ssz/hash.go:141-159; ``spec`` = [(kind, offset, len)] as in
+    registry.VALIDATOR_FIELDS).  Returns an (n*32,) uint8 device tensor."""
+    from .registry import _fields
+
+    _bind(records)
+    if records.numel() < n * record_len:
+        raise ValueError("records tensor shorter than n*record_len")
+    f = _fields(spec)
+    L = _lib.load()
+    if out is None:
+        out = torch.empty(max(32, 32 * n), dtype=torch.uint8, device=records.device)
+    if ws is None:
+        ws = torch.empty(max(256, n * L.mk_ssz_struct_msg_len(f, len(spec))), dtype=torch.uint8,
+                         device=records.device)
+    _lib.check(L.mk_dev_ssz_struct_roots(_p(records), n, record_len, f, len(spec), _p(out), _p(ws), ws.numel(),
+                                         _stream(records.device)), "mk_dev_ssz_struct_roots")
+    return out
+
+
 def merkle_workspace(n: int, item_len: int, device) -> torch.Tensor:
     nbytes = _lib.load().mk_ssz_merkle_workspace_bytes(n, item_len)
     return torch.empty(max(256, nbytes), dtype=torch.uint8, device=device)

@@ -539,3 +539,21 @@ def test_struct_roots_layouts(gpu, layout, n):
     recs = raw.view(np.dtype((np.void, rec_len)))
     want = O.struct_roots(raw, n, rec_len, spec, nthreads=8)
     assert np.array_equal(R.struct_roots(recs, spec), want)
+
+
+@pytest.mark.parametrize("layout", sorted(_STRUCT_LAYOUTS) + ["validator"])
+@pytest.mark.parametrize("n", [1, 257, 70_001])
+def test_dev_struct_roots(gpu, layout, n):
+    """mk_dev_ssz_struct_roots (device records, caller's stream) vs oracle."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+    from prysm_amd import registry as R
+
+    rec_len, spec = (160, list(R.VALIDATOR_FIELDS)) if layout == "validator" else _STRUCT_LAYOUTS[layout]
+    raw = O.splitmix_bytes(n * rec_len, SEED + 98 + rec_len)
+    want = O.struct_roots(raw, n, rec_len, spec, nthreads=8)
+    got = D.struct_roots(torch.from_numpy(raw.copy()).to("cuda:0"), n, rec_len, spec)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().reshape(n, 32), want.reshape(n, 32))
