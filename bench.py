@@ -3,6 +3,11 @@ BASELINE.json configs[3]) on N MI355X, subtree-sharded.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--log2n 28] [--item-len 32]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  python bench.py --gpus N --single-process      (one process, N devices: the cgo caller's form)
+
+With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py launches
+itself as N ranks (torch.distributed.run as a child process, started before
+this process touches the GPU) and exits with the child's status.
 
 One step = one complete Merkleization of the whole tree.  N > 1: every rank
 reduces its shard to the level 10 below its shard root (1024 nodes, the
@@ -24,6 +29,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -44,6 +51,18 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (state the CPU model)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(item_len: int, log2n_sample: int, threads: int = 1):
     """The oracle (a C port of hash.go:194-239; 1 thread = the reference's
     single-goroutine shape, more threads split the tree by subtrees) on a
@@ -55,26 +74,59 @@ def cpu_baseline(item_len: int, log2n_sample: int, threads: int = 1):
     t0 = time.perf_counter()
     O.merkle_hash_flat(items, n, item_len, nthreads=threads)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "leaves/s", "cores": threads, "kind": "port",
+    return {"value": n / dt, "unit": "leaves/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"oracle/merkle_ref.c or_merkle_hash, 2^{log2n_sample} x {item_len}-B items "
                       f"(same SplitMix64 stream), {threads} thread{'s' if threads > 1 else ''}, {dt:.1f} s"}
 
 
 def load_pmc():
-    """(HBM bytes per leaf-kernel launch, effective clock GHz under that load)
-    from the newest committed rocprofv3 PMC summary (profiles/*_pmc.json,
-    written by tools/pmc_summary.py), or (None, None)."""
+    """HBM bytes per leaf-kernel launch and the effective clock under that
+    load from the newest committed rocprofv3 PMC summary (profiles/*_pmc.json,
+    tools/pmc_summary.py), with the file they come from.  These are NOT
+    measured by this run (PMC counters need their own rocprofv3 pass)."""
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     if not files:
-        return None, None
+        return None, None, None
     try:
         with open(files[-1]) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_leaf_launch"), d.get("effective_clock_GHz")
+        return (d.get("hbm_bytes_per_leaf_launch"), d.get("effective_clock_GHz"),
+                os.path.relpath(files[-1], ROOT) + f" ({d.get('box', 'builder lease')}, not this run)")
     except Exception:
-        return None, None
+        return None, None, None
+
+
+def golden_root(log2n: int, item_len: int):
+    """The committed oracle root of this exact workload, if there is one
+    (tests/golden/full_size_roots.json: 2^28 x 32 B, seed 0x5EED..04)."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "full_size_roots.json")) as f:
+            g = json.load(f)["c4"]
+    except (OSError, KeyError, ValueError):
+        return None
+    return g["root"] if (g["n"], g["item_len"], g["seed"]) == (1 << log2n, item_len, SEED) else None
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(nproc: int, argv, script: str = None) -> int:
+    """Runs `script argv` as nproc ranks of one node (torch.distributed.run,
+    127.0.0.1 rendezvous) in a child process and returns its exit status.
+    Called before this process has touched the GPU (it never execs)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script or os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool
+    log(f"launching {nproc} ranks: {' '.join(cmd[1:])}")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -100,11 +152,18 @@ def main():
                          "finisher (parallel.ShardedMerklePipeline).  0 = one stream")
     ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c5"],
                     help="BASELINE.json config: c4 = headline (default); c1/c2/c3/c5 = single-GPU side benches")
+    ap.add_argument("--single-process", action="store_true",
+                    help="N devices from one process through mk_dev_ssz_merkle_hash_multi (the cgo caller's "
+                         "form: one shard per device, RCCL all-gather inside the library)")
     args = ap.parse_args()
     if args.config != "c4":
         from tools.bench_configs import run_config
 
         return run_config(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.single_process:
+        return launch_ranks(args.gpus, sys.argv[1:])
+    if args.single_process:
+        return run_single_process(args)
 
     import torch
     import torch.distributed as dist
@@ -116,7 +175,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+        log(f"ERROR: --gpus {args.gpus} but WORLD_SIZE {world}")
+        return 2
     if args.share_device:
         local = 0
     torch.cuda.set_device(local)
@@ -188,12 +248,12 @@ def main():
             same.zero_()
         if world > 1:  # every rank takes the same path
             dist.all_reduce(same, op=dist.ReduceOp.MIN)
-        if same.item():
-            log(f"rank {rank}: pipelined (frontier {k}), the levels above the leaf pass on a side stream")
-        else:  # never expected (tests pin the split); measure the one-stream path and say so in the JSON
-            log(f"rank {rank}: ERROR pipelined root differs from the one-stream root; timing one stream")
-            pipe = None
-            k = args.frontier if sp.nonempty > 1 and 0 < args.frontier < sp.height - 4 else 0
+        if not same.item():  # never expected (tests pin the split): a wrong root is a failed run
+            log(f"rank {rank}: ERROR pipelined root differs from the one-stream root")
+            if world > 1:
+                dist.destroy_process_group()
+            return 1
+        log(f"rank {rank}: pipelined (frontier {k}), the levels above the leaf pass on a side stream")
 
     def step():
         return pipe.submit(items) if pipe is not None else step_one_stream()
@@ -205,6 +265,7 @@ def main():
         dist.barrier()
     root_hex = None
 
+    status = 0
     D.prof_enable(True)
     D.prof_read()  # reset
     if world > 1:
@@ -225,6 +286,10 @@ def main():
     leaf_ms, leaf_launches, leaf_perms, leaf_hashes = D.prof_read()
     if rank == 0 and r is not None:
         root_hex = bytes(r.cpu().numpy()).hex()
+        want = golden_root(args.log2n, item_len)
+        if want is not None and root_hex != want:
+            log(f"ERROR: root {root_hex} != golden {want}")
+            status = 1
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
@@ -238,7 +303,7 @@ def main():
         hashes_per_launch = leaf_hashes / max(leaf_launches, 1)
         ops_per_launch = perms_per_launch * INT_OPS_PER_PERM - hashes_per_launch * INT_OPS_SAVED_PER_HASH
         achieved = ops_per_launch / avg_leaf_s if avg_leaf_s > 0 else 0.0
-        traffic, clk = load_pmc() if world == 1 and args.log2n == 28 else (None, None)
+        traffic, clk, pmc_src = load_pmc() if world == 1 and args.log2n == 28 else (None, None, None)
         out = {
             "metric": "tree-hash leaves/sec @2^28 chunks (ssz.merkleHash, 32-B leaves)",
             "value": value,
@@ -256,7 +321,9 @@ def main():
                                    f"({n * item_len / 2**30:.0f} GiB), subtree-sharded",
                        "n_items": n, "item_len": item_len, "parallelism": f"subtree{world}",
                        "shard_height": sp.height, "frontier_log2": k, "pipelined": pipe is not None and k > 0,
-                       "root": root_hex},
+                       "root": root_hex, "root_matches_golden": None if golden_root(args.log2n, item_len) is None
+                       else root_hex == golden_root(args.log2n, item_len),
+                       "backend": args.backend if world > 1 else None, "share_device": bool(args.share_device)},
             "roofline": {
                 "bound": "valu-int",
                 "kernel": "k_reduce<LEAF, FAST, 2> (leaf pass: 256-B windows + 4 fused levels)",
@@ -267,6 +334,7 @@ def main():
                 "traffic": traffic,
                 # also against the sustained clock the PMC run measured under this load
                 "effective_clock_GHz": clk,
+                "traffic_source": pmc_src,
                 "frac_at_effective_clock": achieved / (PEAK_INT_OPS / 2.4 * clk) if clk else None,
                 "perms_per_launch": perms_per_launch,
                 "hashes_per_launch": hashes_per_launch,
@@ -282,8 +350,69 @@ def main():
             out["cpu_baseline_threads"] = cpu_baseline(item_len, args.cpu_sample_log2n, threads=nt)
         print(json.dumps(out), flush=True)
     if world > 1:
+        st = torch.tensor([status], dtype=torch.int32, device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        status = int(st.item())
         dist.destroy_process_group()
+    return status
+
+
+def run_single_process(args) -> int:
+    """One process drives args.gpus devices through the library's
+    single-process multi-device entry (mk_dev_ssz_merkle_hash_multi): shard d
+    of the subtree plan lives on device d (generated there), every device
+    reduces its shard to its 1024-node frontier on its own stream, the
+    library all-gathers the frontiers over RCCL and device 0 finishes.  The
+    whole step is inside the timed region (all devices synchronised)."""
+    import torch
+
+    from prysm_amd import device as D
+    from prysm_amd import _lib
+
+    ndev = args.gpus
+    if _lib.device_count() < ndev:
+        log(f"ERROR: {ndev} devices requested, {_lib.device_count()} visible")
+        return 2
+    n, item_len = 1 << args.log2n, args.item_len
+    h, ne, begin = D.shard_plan(n, item_len, ndev)
+    shards = []
+    for d in range(ndev):
+        nb = (begin[d + 1] - begin[d]) * item_len
+        t = torch.empty(max(nb, 16), dtype=torch.uint8, device=f"cuda:{d}")
+        if nb:
+            D.synth_fill(t[:nb], SEED, word0=begin[d] * item_len // 8)
+        shards.append(t)
+    out = torch.empty(32, dtype=torch.uint8, device="cuda:0")
+
+    def sync_all():
+        for d in range(ndev):
+            torch.cuda.synchronize(d)
+
+    sync_all()
+    log(f"single process, {ndev} device(s): shard height {h}, {ne} non-empty shards")
+    for _ in range(args.warmup):
+        D.merkle_hash_multi(shards, n, item_len, out)
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        D.merkle_hash_multi(shards, n, item_len, out)
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    root_hex = bytes(out.cpu().numpy()).hex()
+    want = golden_root(args.log2n, item_len)
+    res = {"metric": "tree-hash leaves/sec @2^28 chunks (ssz.merkleHash, 32-B leaves)",
+           "value": n * args.steps / elapsed, "unit": "leaves/s", "n_gpus": ndev, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "u64 (Keccak lanes as u32 pairs)",
+           "data": "synthetic (device SplitMix64, seed 0x5EED000000000004)",
+           "config": {"workload": f"C4: ssz.merkleHash of 2^{args.log2n} x {item_len}-B items, one process, "
+                                  f"mk_dev_ssz_merkle_hash_multi over {ndev} device(s)",
+                      "n_items": n, "item_len": item_len, "parallelism": f"subtree{ndev}-single-process",
+                      "shard_height": h, "root": root_hex,
+                      "root_matches_golden": None if want is None else root_hex == want}}
+    print(json.dumps(res), flush=True)
+    return 1 if want is not None and root_hex != want else 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

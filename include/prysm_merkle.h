@@ -16,10 +16,22 @@
  *   hashutil.MerkleRoot                      shared/hashutil/merkleRoot.go:12
  *
  * Conventions
+ *   - Every compute entry point takes a per-call context `mk_call*` first
+ *     (NULL = defaults).  cgo may run two consecutive C calls of one goroutine
+ *     on different OS threads, so the device and the error detail travel with
+ *     the call, never with the thread:
+ *       call->device  in:  device index; -1 = for dev entry points the device
+ *                          of `stream` (the thread's current HIP device when
+ *                          stream is NULL), for host-buffer entry points the
+ *                          thread's current HIP device (0 unless set).
+ *       call->code    out: the status returned.
+ *       call->err     out: NUL-terminated detail of a failure ("" on success).
+ *     The calling thread's current HIP device is the same after the call as
+ *     before it.  mk_last_error() keeps the thread's last detail for C callers.
  *   - Every function returns 0 (MK_OK) or a negative MK_E* code; mk_strerror()
- *     names it and mk_last_error() returns the thread's last detailed message.
- *     Nothing panics across the boundary; there is NO CPU fallback: without a
- *     usable gfx950 device every compute entry point returns MK_ENODEV.
+ *     names it.  Nothing panics across the boundary; there is NO CPU
+ *     fallback: without a usable gfx950 device every compute entry point
+ *     returns MK_ENODEV.
  *   - Host-buffer entry points (no `dev` in the name) borrow caller memory for
  *     the duration of the call only (cgo rule: Go memory is never retained);
  *     `[][]byte` inputs are passed flattened as (data, offs[n+1]).
@@ -28,14 +40,15 @@
  *     enqueue work and return without synchronising.  Their scratch space is
  *     caller-provided (size from the *_workspace_bytes query), so they never
  *     allocate and can be captured into a hipGraph.
- *   - Thread safety: host-buffer entry points may be called concurrently from
- *     any OS thread; each takes the current device's lock.  mk_init selects the
- *     device for the calling thread.
+ *   - Thread safety: every entry point may be called concurrently from any OS
+ *     thread; host-buffer entry points take a per-device lock, deposit-trie
+ *     handles a per-handle lock.
  *   - Digests are 32 bytes; node arrays are n x 32 contiguous bytes.
  */
 #ifndef PRYSM_MERKLE_H
 #define PRYSM_MERKLE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -46,35 +59,59 @@ extern "C" {
 #define MK_EINVAL (-22)  /* bad argument (also: reference panics, e.g. len(list[0]) == 0) */
 #define MK_ENODEV (-19)  /* no usable gfx950 device / device index out of range */
 #define MK_ENOMEM (-12)  /* device or host allocation failed / workspace too small */
-#define MK_EHIP (-5)     /* a HIP runtime call failed (see mk_last_error) */
+#define MK_EHIP (-5)     /* a HIP runtime call failed (see call->err) */
 #define MK_ECOMM (-71)   /* RCCL failure in the multi-device path */
 
+#define MK_ERR_LEN 256
+typedef struct mk_call {
+    int32_t device;         /* in: device index, -1 = default (see Conventions) */
+    int32_t code;           /* out: status of the call */
+    char err[MK_ERR_LEN];   /* out: detail of a failure, "" on success */
+} mk_call;
+
 /* ---- lifecycle --------------------------------------------------------- */
-int mk_init(int device);          /* idempotent; binds the calling thread to `device` */
+int mk_init(int device);          /* idempotent: creates `device`'s streams; 0 ok */
 int mk_device_count(void);        /* number of visible gfx950 devices (0 if none) */
 const char* mk_strerror(int code);
-const char* mk_last_error(void);  /* thread-local detail of the last failure */
+const char* mk_last_error(void);  /* the calling thread's last failure detail */
 const char* mk_version(void);
 
 /* ---- hashutil.Hash (hash.go:11-25): legacy Keccak-256 ------------------- */
 /* Single message.  Provided for completeness; Go keeps single Hash calls on
  * the CPU (launch latency, and Hash cannot return an error). */
-int mk_hash(const uint8_t* data, uint64_t len, uint8_t out[32]);
+int mk_hash(mk_call* call, const uint8_t* data, uint64_t len, uint8_t out[32]);
 /* Batched form ("HashBatch"): n messages of msg_len bytes, contiguous -> n*32. */
-int mk_hash_batch(const uint8_t* in, uint64_t n, uint32_t msg_len, uint8_t* out);
+int mk_hash_batch(mk_call* call, const uint8_t* in, uint64_t n, uint32_t msg_len, uint8_t* out);
 /* Variable-length batch: message i = in[offs[i], offs[i+1]) -> n*32. */
-int mk_hash_batch_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint8_t* out);
-int mk_dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, void* stream);
-int mk_dev_hash_batch_var(const void* d_in, const uint64_t* d_offs, uint64_t n, void* d_out, void* stream);
+int mk_hash_batch_var(mk_call* call, const uint8_t* in, const uint64_t* offs, uint64_t n, uint8_t* out);
+int mk_dev_hash_batch(mk_call* call, const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, void* stream);
+int mk_dev_hash_batch_var(mk_call* call, const void* d_in, const uint64_t* d_offs, uint64_t n, void* d_out,
+                          void* stream);
 
 /* ---- ssz.merkleHash (hash.go:194-239) ---------------------------------- */
 /* n items of item_len bytes each, contiguous (the flattened [][]byte; every
  * list TreeHash builds has uniform element length).  out = 32-B result.
  * item_len == 0 with n > 0 is the reference's divide-by-zero panic: MK_EINVAL. */
-int mk_ssz_merkle_hash(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t out[32]);
+int mk_ssz_merkle_hash(mk_call* call, const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t out[32]);
 uint64_t mk_ssz_merkle_workspace_bytes(uint64_t n, uint32_t item_len);
-int mk_dev_ssz_merkle_hash(const void* d_items, uint64_t n, uint32_t item_len, void* d_out32,
+int mk_dev_ssz_merkle_hash(mk_call* call, const void* d_items, uint64_t n, uint32_t item_len, void* d_out32,
                            void* d_ws, uint64_t ws_bytes, void* stream);
+
+/* Many lists in one call (makeSliceHasher over a list of lists, a struct's
+ * list fields, a state's lists): list i = n[i] items of item_len[i] bytes at
+ * byte offset offs[i] of d_items (16-B aligned offsets take the streaming
+ * path); d_roots[i] (32 B each) = merkleHash(list i).  offs, n and item_len
+ * are HOST arrays (the library plans on the host and uploads the per-list
+ * descriptors into the workspace).  Lists of up to 2^15 chunks share one leaf
+ * launch and one launch per level; longer lists run their own fused passes.
+ * Workspace from mk_ssz_merkle_many_workspace_bytes (same n, item_len). */
+uint64_t mk_ssz_merkle_many_workspace_bytes(const uint64_t* n, const uint32_t* item_len, uint32_t nlists);
+int mk_dev_ssz_merkle_many(mk_call* call, const void* d_items, const uint64_t* offs, const uint64_t* n,
+                           const uint32_t* item_len, uint32_t nlists, void* d_roots, void* d_ws, uint64_t ws_bytes,
+                           void* stream);
+/* Host-buffer form: list i = items[offs[i], offs[i] + n[i]*item_len[i]). */
+int mk_ssz_merkle_many(mk_call* call, const uint8_t* items, const uint64_t* offs, const uint64_t* n,
+                       const uint32_t* item_len, uint32_t nlists, uint8_t* roots);
 
 /* ---- subtree sharding across GPUs ----------------------- */
 /* Split a merkleHash of n items over `nshards` devices: every shard is a
@@ -83,14 +120,14 @@ int mk_dev_ssz_merkle_hash(const void* d_items, uint64_t n, uint32_t item_len, v
  * number of non-empty shards.  When the tree is too small to shard
  * (*nonempty == 1) shard 0 holds everything and is hashed with
  * mk_dev_ssz_merkle_hash instead. */
-int mk_ssz_merkle_shard_plan(uint64_t n, uint32_t item_len, uint32_t nshards, uint32_t* height,
+int mk_ssz_merkle_shard_plan(mk_call* call, uint64_t n, uint32_t item_len, uint32_t nshards, uint32_t* height,
                              uint32_t* nonempty, uint64_t* item_begin);
 /* Root (32 B, height `height` above the chunks) of one shard.  pad_at_one=1
  * for every shard of a tree with >1 non-empty shard: a ragged last shard keeps
  * applying the reference's odd rule (node || 0^128) up to `height`. */
-int mk_dev_ssz_merkle_subtree(const void* d_shard_items, uint64_t shard_n, uint32_t item_len,
-                              uint32_t height, int pad_at_one, void* d_out32, void* d_ws,
-                              uint64_t ws_bytes, void* stream);
+int mk_dev_ssz_merkle_subtree(mk_call* call, const void* d_shard_items, uint64_t shard_n, uint32_t item_len,
+                              uint32_t height, int pad_at_one, void* d_out32, void* d_ws, uint64_t ws_bytes,
+                              void* stream);
 /* Frontier variant: stop `frontier_log2` levels below the shard root and
  * write the shard's nodes at height (height - frontier_log2) to d_out (32 B
  * each, 2^frontier_log2 of them, fewer for a ragged last shard; *nodes_out
@@ -98,9 +135,10 @@ int mk_dev_ssz_merkle_subtree(const void* d_shard_items, uint64_t shard_n, uint3
  * that level of the whole tree, so ranks gather a few KB each and the top
  * levels move to the finisher (mk_dev_ssz_merkle_finish_nodes), which can
  * overlap the ranks' next Merkleization.  0 < frontier_log2 < height. */
-int mk_dev_ssz_merkle_subtree_frontier(const void* d_shard_items, uint64_t shard_n, uint32_t item_len,
-                                       uint32_t height, uint32_t frontier_log2, int pad_at_one, void* d_out,
-                                       uint64_t* nodes_out, void* d_ws, uint64_t ws_bytes, void* stream);
+int mk_dev_ssz_merkle_subtree_frontier(mk_call* call, const void* d_shard_items, uint64_t shard_n,
+                                       uint32_t item_len, uint32_t height, uint32_t frontier_log2, int pad_at_one,
+                                       void* d_out, uint64_t* nodes_out, void* d_ws, uint64_t ws_bytes,
+                                       void* stream);
 /* The same subtree continued from one of its node levels: `count` 32-B nodes
  * (a shard's level, e.g. the output of the leaf pass) reduced for `height`
  * levels with the reference's odd rule (hash.go:225-235; pad_at_one as
@@ -110,26 +148,41 @@ int mk_dev_ssz_merkle_subtree_frontier(const void* d_shard_items, uint64_t shard
  * ShardedMerklePipeline).  Workspace from
  * mk_ssz_merkle_node_frontier_workspace_bytes. */
 uint64_t mk_ssz_merkle_node_frontier_workspace_bytes(uint64_t count, uint32_t height, uint32_t frontier_log2);
-int mk_dev_ssz_merkle_node_frontier(const void* d_nodes, uint64_t count, uint32_t height, uint32_t frontier_log2,
-                                    int pad_at_one, void* d_out, uint64_t* nodes_out, void* d_ws,
-                                    uint64_t ws_bytes, void* stream);
+int mk_dev_ssz_merkle_node_frontier(mk_call* call, const void* d_nodes, uint64_t count, uint32_t height,
+                                    uint32_t frontier_log2, int pad_at_one, void* d_out, uint64_t* nodes_out,
+                                    void* d_ws, uint64_t ws_bytes, void* stream);
 /* Finisher over `count` nodes forming one complete tree level in order (the
  * gathered frontiers): the reference level loop (odd -> 0^128 pad) and
  * Keccak(root || le64(n_total) || 0^24).  Workspace from
  * mk_ssz_merkle_finish_workspace_bytes(count). */
 uint64_t mk_ssz_merkle_finish_workspace_bytes(uint64_t count);
-int mk_dev_ssz_merkle_finish_nodes(const void* d_nodes, uint64_t count, uint64_t n_total, void* d_out32,
-                                   void* d_ws, uint64_t ws_bytes, void* stream);
+int mk_dev_ssz_merkle_finish_nodes(mk_call* call, const void* d_nodes, uint64_t count, uint64_t n_total,
+                                   void* d_out32, void* d_ws, uint64_t ws_bytes, void* stream);
 /* Finisher on one device: the reference level loop over the `nroots`
  * gathered shard roots (odd -> 0^128 pad), then Keccak(root || le64(n) || 0^24). */
-int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32,
+int mk_dev_ssz_merkle_finish(mk_call* call, const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32,
                              void* stream);
-/* Single-process multi-device merkleHash for the cgo caller: shards the host
- * items over devices 0..ndev-1, reduces every shard to its frontier level
- * (up to 1024 nodes), all-gathers the frontiers over RCCL (xGMI) and finishes
- * on device 0. */
-int mk_ssz_merkle_hash_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int ndev,
-                             uint8_t out[32]);
+/* Single-process multi-device merkleHash for the cgo caller.  The items are
+ * split by mk_ssz_merkle_shard_plan into `nshards` shards; shard s runs on
+ * device devs[s] (devs == NULL: device s).  Every device uploads its shards
+ * from its own host thread through pinned staging buffers, so the PCIe links
+ * copy in parallel and a shard's passes overlap the upload of the device's
+ * next shard; every shard is reduced to its frontier level (up to 1024
+ * nodes).  When each device holds exactly one shard the frontiers are
+ * all-gathered over RCCL (xGMI); otherwise they are copied to devs[0].  The
+ * top levels and the length mix-in finish on devs[0]. */
+int mk_ssz_merkle_hash_multi(mk_call* call, const uint8_t* items, uint64_t n, uint32_t item_len, int nshards,
+                             const int* devs, uint8_t out[32]);
+/* Device-resident form on devices 0..ndev-1 (one shard per device, shard d =
+ * items [item_begin[d], item_begin[d+1]) of mk_ssz_merkle_shard_plan(n,
+ * item_len, ndev), at d_shards[d] on device d).  Each device reduces its
+ * shard to its frontier on streams[d] (NULL entries: the library's stream of
+ * that device), the frontiers are all-gathered over RCCL and device 0
+ * finishes into d_out32 (device 0 memory).  Enqueues only; the library's
+ * per-device workspaces are reused by the next call, so successive calls
+ * must be on the same streams (or synchronised). */
+int mk_dev_ssz_merkle_hash_multi(mk_call* call, const void* const* d_shards, uint64_t n, uint32_t item_len,
+                                 int ndev, void* d_out32, void* const* streams);
 
 /* ---- struct hashing (hash.go:141-159) for flat fixed-layout records ------ */
 /* The typed-registry path behind ssz.Hashable (hash.go:18-20, 57-58): a Go
@@ -148,21 +201,21 @@ typedef struct mk_field {
 } mk_field;
 uint64_t mk_ssz_struct_msg_len(const mk_field* fields, uint32_t nfields);
 /* roots of n records -> n x 32 bytes (one struct hash per record). */
-int mk_ssz_struct_roots(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
-                        uint32_t nfields, uint8_t* roots);
+int mk_ssz_struct_roots(mk_call* call, const uint8_t* records, uint64_t n, uint32_t record_len,
+                        const mk_field* fields, uint32_t nfields, uint8_t* roots);
 /* Device-resident struct roots (makeStructHasher per element,
  * hash.go:141-159): n records -> d_roots (n x 32) on `stream`; d_ws of at
- * least n * mk_ssz_struct_msg_len bytes.  Lets a caller run the list's
- * merkleHash on another stream (a stream of states: struct roots of state
- * i+1 overlap the merkle top of state i). */
-int mk_dev_ssz_struct_roots(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
-                            uint32_t nfields, void* d_roots, void* d_ws, uint64_t ws_bytes, void* stream);
+ * least n * mk_ssz_struct_msg_len bytes. */
+int mk_dev_ssz_struct_roots(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
+                            const mk_field* fields, uint32_t nfields, void* d_roots, void* d_ws, uint64_t ws_bytes,
+                            void* stream);
 /* TreeHash of a list of such structs: merkleHash over the n struct roots. */
 uint64_t mk_ssz_struct_list_workspace_bytes(uint64_t n, const mk_field* fields, uint32_t nfields);
-int mk_dev_ssz_struct_list_root(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
-                                uint32_t nfields, void* d_out32, void* d_ws, uint64_t ws_bytes, void* stream);
-int mk_ssz_struct_list_root(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
-                            uint32_t nfields, uint8_t out[32]);
+int mk_dev_ssz_struct_list_root(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
+                                const mk_field* fields, uint32_t nfields, void* d_out32, void* d_ws,
+                                uint64_t ws_bytes, void* stream);
+int mk_ssz_struct_list_root(mk_call* call, const uint8_t* records, uint64_t n, uint32_t record_len,
+                            const mk_field* fields, uint32_t nfields, uint8_t out[32]);
 
 /* ---- hashutil.MerkleRoot (merkleRoot.go:12-30) -------------------------- */
 /* Root of the heap o[i] = Hash(o[2i] || o[2i+1]) over leaves
@@ -170,39 +223,68 @@ int mk_ssz_struct_list_root(const uint8_t* records, uint64_t n, uint32_t record_
  * (optional, n x 32) receives Hash(values[i]): the reference overwrites its
  * input slice with them (merkleRoot.go:16-19) and a drop-in keeps that side
  * effect.  n == 0 is MK_EINVAL (the reference panics: index out of range). */
-int mk_merkle_root(const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_t* leaves_out, uint8_t out[32]);
+int mk_merkle_root(mk_call* call, const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_t* leaves_out,
+                   uint8_t out[32]);
 uint64_t mk_merkle_root_workspace_bytes(uint64_t n);
 /* Device-resident: d_offs (n+1, device) or fixed_len; d_heap of
  * mk_merkle_root_workspace_bytes(n); d_leaves32 optional (n x 32). */
-int mk_dev_merkle_root(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len, void* d_heap,
-                       uint64_t heap_bytes, void* d_leaves32, void* d_out32, void* stream);
+int mk_dev_merkle_root(mk_call* call, const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len,
+                       void* d_heap, uint64_t heap_bytes, void* d_leaves32, void* d_out32, void* stream);
 
 /* ---- trieutil deposit trie (deposit_trie.go:29-81) ---------------------- */
-/* Batch build of the depth-`depth` sparse trie over n deposits (message i =
- * data[offs[i], offs[i+1])).  Equals n calls of UpdateDepositTrie: empty nodes
- * are 0^32 (map miss), root = node 1 (0^32 when n == 0).  levels_out
- * (nullable) receives, for d = 0..depth, ceil(n / 2^d) nodes of level d
- * (d = 0: leaf hashes), concatenated — the data GenerateMerkleBranch reads. */
-uint64_t mk_deposit_trie_levels_bytes(uint64_t n, uint32_t depth);
-int mk_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
+/* Level array of a depth-`depth` trie with room for `capacity` leaves: level
+ * d (d = 0: leaf hashes Hash(deposit)) starts at node
+ * sum_{i<d} ceil(capacity / 2^i) and holds ceil(count / 2^d) nodes.  Empty
+ * nodes are 0^32 (Go map miss), root = level `depth` node 0 (0^32 when
+ * count == 0). */
+uint64_t mk_deposit_trie_levels_bytes(uint64_t capacity, uint32_t depth);
+/* Batch build of n deposits (message i = data[offs[i], offs[i+1])) = n calls
+ * of UpdateDepositTrie.  levels_out (nullable) receives the level array with
+ * capacity n (the data GenerateMerkleBranch reads). */
+int mk_deposit_trie_build(mk_call* call, const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
                           uint8_t* levels_out, uint8_t root[32]);
-/* Device-resident build: d_levels (mk_deposit_trie_levels_bytes) and the
- * deposits in device memory; root to d_root32.  Deposit i is
- * d_data[d_offs[i], d_offs[i+1]) or, with d_offs == NULL, the fixed-length
- * record d_data[i*fixed_len, (i+1)*fixed_len) (the 280-B deposit-data layout
- * of core/blocks/block.go:103-130). */
-int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len,
-                              uint32_t depth, void* d_levels, void* d_root32, void* stream);
+/* Device-resident append: the trie in d_levels (capacity `capacity`) holds
+ * `count` deposits; deposits count .. count+k-1 are d_data[d_offs[i],
+ * d_offs[i+1]) (i < k) or, with d_offs == NULL, fixed_len-byte records (the
+ * 280-B deposit-data layout of core/blocks/block.go:103-130).  Hashes the k
+ * leaves and recomputes only the right edge of every level above them
+ * (<= k/2^d + 2 nodes at level d): UpdateDepositTrie's O(depth) path per
+ * deposit (deposit_trie.go:29-40), batched.  count == 0 is the batch build.
+ * The new root goes to d_root32.  count + k <= capacity. */
+int mk_dev_deposit_trie_append(mk_call* call, void* d_levels, uint64_t capacity, uint64_t count, const void* d_data,
+                               const uint64_t* d_offs, uint64_t k, uint32_t fixed_len, uint32_t depth,
+                               void* d_root32, void* stream);
+/* GenerateMerkleBranch (deposit_trie.go:43-58) from a device level array:
+ * d_branch[d] = sibling of `index`'s ancestor at level d (0^32 if absent). */
+int mk_dev_deposit_trie_branch(mk_call* call, const void* d_levels, uint64_t capacity, uint64_t count,
+                               uint32_t depth, uint64_t index, void* d_branch, void* stream);
+
+/* Device-resident trie handle: the Go DepositTrie (deposit_trie.go:13-16)
+ * holds one.  Levels stay in HBM (capacity doubles on demand); appends
+ * recompute only the right edge, so powchain's read-Root-then-Update loop
+ * (powchain/service.go:379-386) costs O(depth) hashes per deposit. */
+typedef struct mk_trie mk_trie;
+int mk_deposit_trie_new(mk_call* call, uint32_t depth, uint64_t capacity, mk_trie** out);
+void mk_deposit_trie_free(mk_trie* t);
+uint64_t mk_deposit_trie_count(const mk_trie* t);
+/* Appends k deposits (host data, message i = data[offs[i], offs[i+1])). */
+int mk_deposit_trie_append(mk_call* call, mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k);
+int mk_deposit_trie_root(mk_call* call, mk_trie* t, uint8_t root[32]);
+/* depth x 32 bytes: GenerateMerkleBranch(index). */
+int mk_deposit_trie_branch(mk_call* call, mk_trie* t, uint64_t index, uint8_t* branch);
+/* Leaf hashes [first, first + cnt) (Hash(deposit)), cnt x 32 bytes. */
+int mk_deposit_trie_leaves(mk_call* call, mk_trie* t, uint64_t first, uint64_t cnt, uint8_t* out);
+
 /* Batched VerifyMerkleBranch: ok[i] = fold(leaves[i], branches[i*depth..],
  * indices[i] + 2^tree_depth) == roots[i]. */
-int mk_verify_merkle_branches(const uint8_t* leaves, const uint8_t* branches, const uint64_t* indices,
-                              uint64_t n, uint32_t depth, uint32_t tree_depth, const uint8_t* roots,
-                              uint8_t* ok);
+int mk_verify_merkle_branches(mk_call* call, const uint8_t* leaves, const uint8_t* branches,
+                              const uint64_t* indices, uint64_t n, uint32_t depth, uint32_t tree_depth,
+                              const uint8_t* roots, uint8_t* ok);
 
 /* ---- synthetic inputs (bench / tests) ----------------------------------- */
 /* Bytes [8*word0, 8*word0 + nbytes) of the SplitMix64 stream;
  * nbytes must be a multiple of 8. */
-int mk_dev_synth_fill(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t word0, void* stream);
+int mk_dev_synth_fill(mk_call* call, void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t word0, void* stream);
 
 /* ---- measurement -------------------------------------------------------- */
 /* When enabled, every dev merkle call records hipEvents around its dominant
@@ -211,7 +293,7 @@ int mk_dev_synth_fill(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t word
  * Keccak-f permutations and digests (hashes) of those launches, then resets.
  * Any out-pointer may be NULL. */
 int mk_prof_enable(int on);
-int mk_prof_read(double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms, double* leaf_hashes);
+int mk_prof_read(mk_call* call, double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms, double* leaf_hashes);
 
 #ifdef __cplusplus
 }

@@ -178,6 +178,33 @@ def deposit_trie_levels(deposits, depth: int = DEPOSIT_TREE_DEPTH):
     return root.raw, levels
 
 
+class DictTrie:
+    """Literal restatement of shared/trieutil/deposit_trie.go:13-63: the
+    incremental trie over a map whose missing keys read as 0^32."""
+
+    def __init__(self, depth: int = DEPOSIT_TREE_DEPTH):
+        self.depth, self.count, self.m = depth, 0, {}
+
+    def update(self, data: bytes) -> None:  # UpdateDepositTrie (:29-40)
+        idx = self.count + (1 << self.depth)
+        self.m[idx] = keccak256(data)
+        for _ in range(self.depth):
+            idx //= 2
+            self.m[idx] = keccak256(self.m.get(idx * 2, bytes(32)) + self.m.get(idx * 2 + 1, bytes(32)))
+        self.count += 1
+
+    def branch(self, index: int):  # GenerateMerkleBranch (:43-58)
+        idx = index + (1 << self.depth)
+        out = []
+        for _ in range(self.depth):
+            out.append(self.m.get(idx - 1 if idx % 2 else idx + 1, bytes(32)))
+            idx //= 2
+        return out
+
+    def root(self) -> bytes:  # Root (:61-63)
+        return self.m.get(1, bytes(32))
+
+
 def verify_merkle_branch(leaf: bytes, branch, depth: int, index: int, root: bytes,
                          tree_depth: int = DEPOSIT_TREE_DEPTH) -> bool:
     br = b"".join(bytes(b) for b in branch)

@@ -34,46 +34,67 @@ _c = ctypes
 _vp = _c.c_void_p
 _u64, _u32, _int = _c.c_uint64, _c.c_uint32, _c.c_int
 
-# name -> (restype, argtypes)
+
+class Call(ctypes.Structure):
+    """mk_call: per-call device selection and error detail (include/prysm_merkle.h)."""
+    _fields_ = [("device", ctypes.c_int32), ("code", ctypes.c_int32), ("err", ctypes.c_char * 256)]
+
+
+_cp = _c.POINTER(Call)
+
+# name -> (restype, argtypes); entry points taking a per-call context list it first
 _SIGS = {
     "mk_init": (_int, [_int]),
     "mk_device_count": (_int, []),
     "mk_strerror": (_c.c_char_p, [_int]),
     "mk_last_error": (_c.c_char_p, []),
     "mk_version": (_c.c_char_p, []),
-    "mk_hash": (_int, [_vp, _u64, _vp]),
-    "mk_hash_batch": (_int, [_vp, _u64, _u32, _vp]),
-    "mk_hash_batch_var": (_int, [_vp, _vp, _u64, _vp]),
-    "mk_dev_hash_batch": (_int, [_vp, _u64, _u32, _vp, _vp]),
-    "mk_dev_hash_batch_var": (_int, [_vp, _vp, _u64, _vp, _vp]),
-    "mk_ssz_merkle_hash": (_int, [_vp, _u64, _u32, _vp]),
+    "mk_hash": (_int, [_cp, _vp, _u64, _vp]),
+    "mk_hash_batch": (_int, [_cp, _vp, _u64, _u32, _vp]),
+    "mk_hash_batch_var": (_int, [_cp, _vp, _vp, _u64, _vp]),
+    "mk_dev_hash_batch": (_int, [_cp, _vp, _u64, _u32, _vp, _vp]),
+    "mk_dev_hash_batch_var": (_int, [_cp, _vp, _vp, _u64, _vp, _vp]),
+    "mk_ssz_merkle_hash": (_int, [_cp, _vp, _u64, _u32, _vp]),
     "mk_ssz_merkle_workspace_bytes": (_u64, [_u64, _u32]),
-    "mk_dev_ssz_merkle_hash": (_int, [_vp, _u64, _u32, _vp, _vp, _u64, _vp]),
-    "mk_ssz_merkle_shard_plan": (_int, [_u64, _u32, _u32, _vp, _vp, _vp]),
-    "mk_dev_ssz_merkle_subtree": (_int, [_vp, _u64, _u32, _u32, _int, _vp, _vp, _u64, _vp]),
-    "mk_dev_ssz_merkle_finish": (_int, [_vp, _u64, _u64, _vp, _vp]),
-    "mk_dev_ssz_merkle_subtree_frontier": (_int, [_vp, _u64, _u32, _u32, _u32, _int, _vp, _vp, _vp, _u64, _vp]),
+    "mk_dev_ssz_merkle_hash": (_int, [_cp, _vp, _u64, _u32, _vp, _vp, _u64, _vp]),
+    "mk_ssz_merkle_many_workspace_bytes": (_u64, [_vp, _vp, _u32]),
+    "mk_dev_ssz_merkle_many": (_int, [_cp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _u64, _vp]),
+    "mk_ssz_merkle_many": (_int, [_cp, _vp, _vp, _vp, _vp, _u32, _vp]),
+    "mk_ssz_merkle_shard_plan": (_int, [_cp, _u64, _u32, _u32, _vp, _vp, _vp]),
+    "mk_dev_ssz_merkle_subtree": (_int, [_cp, _vp, _u64, _u32, _u32, _int, _vp, _vp, _u64, _vp]),
+    "mk_dev_ssz_merkle_finish": (_int, [_cp, _vp, _u64, _u64, _vp, _vp]),
+    "mk_dev_ssz_merkle_subtree_frontier": (_int, [_cp, _vp, _u64, _u32, _u32, _u32, _int, _vp, _vp, _vp, _u64,
+                                                  _vp]),
     "mk_ssz_merkle_node_frontier_workspace_bytes": (_u64, [_u64, _u32, _u32]),
-    "mk_dev_ssz_merkle_node_frontier": (_int, [_vp, _u64, _u32, _u32, _int, _vp, _vp, _vp, _u64, _vp]),
+    "mk_dev_ssz_merkle_node_frontier": (_int, [_cp, _vp, _u64, _u32, _u32, _int, _vp, _vp, _vp, _u64, _vp]),
     "mk_ssz_merkle_finish_workspace_bytes": (_u64, [_u64]),
-    "mk_dev_ssz_merkle_finish_nodes": (_int, [_vp, _u64, _u64, _vp, _vp, _u64, _vp]),
-    "mk_ssz_merkle_hash_multi": (_int, [_vp, _u64, _u32, _int, _vp]),
+    "mk_dev_ssz_merkle_finish_nodes": (_int, [_cp, _vp, _u64, _u64, _vp, _vp, _u64, _vp]),
+    "mk_ssz_merkle_hash_multi": (_int, [_cp, _vp, _u64, _u32, _int, _vp, _vp]),
+    "mk_dev_ssz_merkle_hash_multi": (_int, [_cp, _vp, _u64, _u32, _int, _vp, _vp]),
     "mk_ssz_struct_msg_len": (_u64, [_vp, _u32]),
-    "mk_ssz_struct_roots": (_int, [_vp, _u64, _u32, _vp, _u32, _vp]),
+    "mk_ssz_struct_roots": (_int, [_cp, _vp, _u64, _u32, _vp, _u32, _vp]),
     "mk_ssz_struct_list_workspace_bytes": (_u64, [_u64, _vp, _u32]),
-    "mk_dev_ssz_struct_list_root": (_int, [_vp, _u64, _u32, _vp, _u32, _vp, _vp, _u64, _vp]),
-    "mk_dev_ssz_struct_roots": (_int, [_vp, _u64, _u32, _vp, _u32, _vp, _vp, _u64, _vp]),
-    "mk_ssz_struct_list_root": (_int, [_vp, _u64, _u32, _vp, _u32, _vp]),
-    "mk_merkle_root": (_int, [_vp, _vp, _u64, _vp, _vp]),
+    "mk_dev_ssz_struct_list_root": (_int, [_cp, _vp, _u64, _u32, _vp, _u32, _vp, _vp, _u64, _vp]),
+    "mk_dev_ssz_struct_roots": (_int, [_cp, _vp, _u64, _u32, _vp, _u32, _vp, _vp, _u64, _vp]),
+    "mk_ssz_struct_list_root": (_int, [_cp, _vp, _u64, _u32, _vp, _u32, _vp]),
+    "mk_merkle_root": (_int, [_cp, _vp, _vp, _u64, _vp, _vp]),
     "mk_merkle_root_workspace_bytes": (_u64, [_u64]),
-    "mk_dev_merkle_root": (_int, [_vp, _vp, _u64, _u32, _vp, _u64, _vp, _vp, _vp]),
+    "mk_dev_merkle_root": (_int, [_cp, _vp, _vp, _u64, _u32, _vp, _u64, _vp, _vp, _vp]),
     "mk_deposit_trie_levels_bytes": (_u64, [_u64, _u32]),
-    "mk_deposit_trie_build": (_int, [_vp, _vp, _u64, _u32, _vp, _vp]),
-    "mk_dev_deposit_trie_build": (_int, [_vp, _vp, _u64, _u32, _u32, _vp, _vp, _vp]),
-    "mk_verify_merkle_branches": (_int, [_vp, _vp, _vp, _u64, _u32, _u32, _vp, _vp]),
-    "mk_dev_synth_fill": (_int, [_vp, _u64, _u64, _u64, _vp]),
+    "mk_deposit_trie_build": (_int, [_cp, _vp, _vp, _u64, _u32, _vp, _vp]),
+    "mk_dev_deposit_trie_append": (_int, [_cp, _vp, _u64, _u64, _vp, _vp, _u64, _u32, _u32, _vp, _vp]),
+    "mk_dev_deposit_trie_branch": (_int, [_cp, _vp, _u64, _u64, _u32, _u64, _vp, _vp]),
+    "mk_deposit_trie_new": (_int, [_cp, _u32, _u64, _vp]),
+    "mk_deposit_trie_free": (None, [_vp]),
+    "mk_deposit_trie_count": (_u64, [_vp]),
+    "mk_deposit_trie_append": (_int, [_cp, _vp, _vp, _vp, _u64]),
+    "mk_deposit_trie_root": (_int, [_cp, _vp, _vp]),
+    "mk_deposit_trie_branch": (_int, [_cp, _vp, _u64, _vp]),
+    "mk_deposit_trie_leaves": (_int, [_cp, _vp, _u64, _u64, _vp]),
+    "mk_verify_merkle_branches": (_int, [_cp, _vp, _vp, _vp, _u64, _u32, _u32, _vp, _vp]),
+    "mk_dev_synth_fill": (_int, [_cp, _vp, _u64, _u64, _u64, _vp]),
     "mk_prof_enable": (_int, [_int]),
-    "mk_prof_read": (_int, [_vp, _vp, _vp, _vp]),
+    "mk_prof_read": (_int, [_cp, _vp, _vp, _vp, _vp]),
 }
 
 MK_FIELD_BYTES = 1
@@ -92,7 +113,7 @@ def header_symbols():
     """Every mk_* function declared in include/prysm_merkle.h."""
     with open(HEADER) as f:
         txt = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|const char\*)\s+(mk_[a-z0-9_]+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|uint64_t|void|const char\*)\s+(mk_[a-z0-9_]+)\s*\(", txt, re.M)))
 
 
 def load():
@@ -112,11 +133,21 @@ def load():
     return L
 
 
-def check(rc: int, what: str = "") -> None:
+def check(rc: int, what: str = "", call: "Call" = None) -> None:
+    """Raise MerkleError for a failed call; the detail comes from the call's
+    own context (never from another call on this thread)."""
     if rc != MK_OK:
         L = load()
-        detail = L.mk_last_error().decode(errors="replace")
+        detail = call.err.decode(errors="replace") if call is not None else L.mk_last_error().decode(errors="replace")
         raise MerkleError(rc, f"{what}: {L.mk_strerror(rc).decode()}: {detail}")
+
+
+def invoke(name: str, *args, device: int = -1) -> None:
+    """Call entry point `name` with a fresh per-call context (device: -1 =
+    the stream's / thread's current device) and raise on failure."""
+    call = Call(device, 0, b"")
+    rc = getattr(load(), name)(ctypes.byref(call), *args)
+    check(rc, name, call)
 
 
 def device_count() -> int:

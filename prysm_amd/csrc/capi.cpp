@@ -1,63 +1,35 @@
-// C-ABI of the MI355X Merkleization engine: device management, the
-// merkleHash pass planner, and the host/device entry points declared in
-// include/prysm_merkle.h.  Compiled with hipcc into libprysm_merkle.so.
+// C-ABI of the MI355X Merkleization engine: devices, streams and buffers,
+// the launch side of the pass planner (planner.cpp), and the host/device
+// entry points declared in include/prysm_merkle.h.  Built with hipcc into
+// libprysm_merkle.so.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
-#include <cstdarg>
-#include <cstdio>
+#include <algorithm>
 #include <cstring>
+#include <map>
 #include <mutex>
-#include <string>
+#include <thread>
 #include <vector>
 
 #include "merkle_kernels.hpp"
+#include "planner.hpp"
 #include "prysm_merkle.h"
 
-namespace {
-
+using mk::ceil_div;
+using mk::fail;
+using mk::ilog2;
+using mk::Plan;
+using mk::Pass;
 using mk::ReduceArgs;
 using mk::kReduceThreads;
+
+namespace {
 
 #ifndef MK_SIDE_PRIO
 #define MK_SIDE_PRIO 1
 #endif
 constexpr bool kSidePrio = MK_SIDE_PRIO != 0;  // library side/copy streams at high priority
-#ifndef MK_WAVE2
-#define MK_WAVE2 1
-#endif
-constexpr bool kWave2 = MK_WAVE2 != 0;  // two-lanes-per-state latency pass
-#ifndef MK_WAVE3
-#define MK_WAVE3 1
-#endif
-constexpr bool kWave3 = kWave2 && MK_WAVE3 != 0;  // node latency passes bit-interleaved (k_wave3)
-#ifndef MK_NODE_WAVE_MAX_LOG2
-#define MK_NODE_WAVE_MAX_LOG2 17
-#endif
-// node passes switch to the latency form at or below this width: the first
-// level is throughput-bound either way, but the throughput kernel spends ~9
-// serial permutations on its 5 levels where the wave pass spends 6
-constexpr uint64_t kNodeWaveMaxC1 = 1ull << MK_NODE_WAVE_MAX_LOG2;
-#ifndef MK_NODE_WAVE_WGS
-#define MK_NODE_WAVE_WGS 256
-#endif
-constexpr uint64_t kNodeWaveWgs = MK_NODE_WAVE_WGS;
-#ifndef MK_LEAF_WAVE3
-#define MK_LEAF_WAVE3 1
-#endif
-constexpr bool kLeafWave3 = MK_LEAF_WAVE3 != 0;  // narrow leaf passes bit-interleaved too
-#ifndef MK_LEAF_WAVE_MAX_LOG2
-#define MK_LEAF_WAVE_MAX_LOG2 17
-#endif
-constexpr uint64_t kLeafWaveMaxC1 = 1ull << MK_LEAF_WAVE_MAX_LOG2;  // leaf passes at or below: latency form
-#ifndef MK_REDUCE_NI2_MIN_LOG2
-#define MK_REDUCE_NI2_MIN_LOG2 18
-#endif
-constexpr uint64_t kReduceNi2MinC1 = 1ull << MK_REDUCE_NI2_MIN_LOG2;  // leaf passes narrower than this use NI = 1
-#ifndef MK_TOP_ONE_WG
-#define MK_TOP_ONE_WG 1
-#endif
-constexpr bool kTopOneWg = MK_TOP_ONE_WG != 0;
 #ifndef MK_REC_KERNEL
 #define MK_REC_KERNEL 1
 #endif
@@ -66,32 +38,27 @@ constexpr bool kRecKernel = MK_REC_KERNEL != 0;  // k_keccak_rec<35> for 280-B d
 #define MK_STRUCT_FUSED 1
 #endif
 constexpr bool kStructFused = MK_STRUCT_FUSED != 0;  // k_struct_fused instead of fields + message kernels
-uint32_t ilog2(uint64_t v) {
-    uint32_t l = 0;
-    while (v > 1) {
-        v >>= 1;
-        ++l;
-    }
-    return l;
-}
-
-thread_local std::string t_err;
-thread_local int t_dev = -1;
-
-int fail(int code, const char* fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    t_err = buf;
-    return code;
-}
+#ifndef MK_TRIE_TOP_MAX_LOG2
+#define MK_TRIE_TOP_MAX_LOG2 17
+#endif
+constexpr uint64_t kTrieTopMax = 1ull << MK_TRIE_TOP_MAX_LOG2;  // trie levels at or below: k_trie_top3
+constexpr uint64_t kTrieTopWgs = 256;
+constexpr uint64_t kAppendMaxRange = 1020;  // k_trie_append<1024>: one parent per lane pair
+#ifndef MK_STAGE_BYTES
+#define MK_STAGE_BYTES (32ull << 20)
+#endif
+constexpr size_t kStageBytes = MK_STAGE_BYTES;  // pinned H2D staging slot (2 per device)
 
 #define HIPCHK(x)                                                                            \
     do {                                                                                     \
         hipError_t e_ = (x);                                                                 \
         if (e_ != hipSuccess) return fail(MK_EHIP, "%s: %s", #x, hipGetErrorString(e_));     \
+    } while (0)
+
+#define TRY(x)                        \
+    do {                              \
+        int rc_ = (x);                \
+        if (rc_ != MK_OK) return rc_; \
     } while (0)
 
 // ---- devices ---------------------------------------------------------------
@@ -100,24 +67,53 @@ struct DevBuf {
     size_t cap = 0;
 };
 
-struct DevCtx {
+int grow(DevBuf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.cap >= bytes) return MK_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    if (hipMalloc(&b.p, bytes) != hipSuccess) return fail(MK_ENOMEM, "hipMalloc(%zu) failed", bytes);
+    b.cap = bytes;
+    return MK_OK;
+}
+
+// small pinned upload ring: descriptor tables for dev entry points (the
+// source must outlive the async copy; a slot is reused after its event)
+struct SmallStage {
     std::mutex mu;
+    static constexpr int kSlots = 4;
+    void* host[kSlots] = {};
+    size_t cap[kSlots] = {};
+    hipEvent_t ev[kSlots] = {};
+    bool used[kSlots] = {};
+    int next = 0;
+};
+
+struct DevCtx {
+    std::mutex mu;  // host-buffer entry points: in/out/ws/aux and the big staging
     hipStream_t stream = nullptr;
-    DevBuf in, out, ws, aux, aux2;
+    DevBuf in, out, ws, aux, in2;
     // side stream + events: the ragged last workgroup of a pass runs
     // concurrently with the pass's full workgroups (fork/join on events)
     std::mutex side_mu;
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    // host-buffer entries: records copied in chunks on `copy` while the
-    // compute stream hashes the previous chunk (guarded by `mu`)
+    // host-buffer uploads on `copy` overlapping compute on `stream`
     hipStream_t copy = nullptr;
     hipEvent_t h2d = nullptr;
+    void* stage[2] = {nullptr, nullptr};  // pinned H2D staging slots
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    bool stage_used[2] = {false, false};
+    hipEvent_t region_ev[2] = {nullptr, nullptr};  // multi: compute of a shard region done
+    bool region_used[2] = {false, false};
+    SmallStage small;
 };
 
 std::mutex g_mu;
 int g_ndev = -1;
 std::vector<DevCtx*> g_ctx;
+thread_local int t_bound = -1;  // device bound by the current call
 
 int probe_devices() {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -136,52 +132,115 @@ int probe_devices() {
     return g_ndev;
 }
 
-int bind(int dev) {
+// Makes `dev` the thread's current device and creates its context once.
+int bind_dev(int dev) {
     if (probe_devices() <= 0) return fail(MK_ENODEV, "no gfx950 device visible");
-    if (dev < 0) dev = t_dev >= 0 ? t_dev : 0;
-    if (dev >= g_ndev) return fail(MK_ENODEV, "device %d out of range (%d visible)", dev, g_ndev);
+    if (dev < 0 || dev >= g_ndev) return fail(MK_ENODEV, "device %d out of range (%d visible)", dev, g_ndev);
     HIPCHK(hipSetDevice(dev));
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        if (!g_ctx[dev]) {
-            auto* c = new DevCtx();
-            // side/copy streams at the highest priority: a default-priority
-            // stream can share the caller's hardware queue (GPU_MAX_HW_QUEUES=4)
-            // and then runs after, not beside, the work it should overlap
-            int lo = 0, hi = 0;
-            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess || !kSidePrio) hi = lo = 0;
-            if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-                hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) != hipSuccess ||
-                hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&c->join, hipEventDisableTiming) != hipSuccess ||
-                hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, hi) != hipSuccess ||
-                hipEventCreateWithFlags(&c->h2d, hipEventDisableTiming) != hipSuccess) {
-                delete c;
-                return fail(MK_EHIP, "stream/event creation failed on device %d", dev);
-            }
-            g_ctx[dev] = c;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_ctx[dev]) {
+        auto* c = new DevCtx();
+        // side/copy streams at the highest priority: a default-priority
+        // stream can share the caller's hardware queue (GPU_MAX_HW_QUEUES=4)
+        // and then runs after, not beside, the work it should overlap
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess || !kSidePrio) hi = lo = 0;
+        bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+                  hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) == hipSuccess &&
+                  hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&c->join, hipEventDisableTiming) == hipSuccess &&
+                  hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, hi) == hipSuccess &&
+                  hipEventCreateWithFlags(&c->h2d, hipEventDisableTiming) == hipSuccess;
+        for (int i = 0; ok && i < 2; ++i)
+            ok = hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming) == hipSuccess &&
+                 hipEventCreateWithFlags(&c->region_ev[i], hipEventDisableTiming) == hipSuccess;
+        for (int i = 0; ok && i < SmallStage::kSlots; ++i)
+            ok = hipEventCreateWithFlags(&c->small.ev[i], hipEventDisableTiming) == hipSuccess;
+        if (!ok) {
+            delete c;
+            return fail(MK_EHIP, "stream/event creation failed on device %d", dev);
         }
+        g_ctx[dev] = c;
     }
-    t_dev = dev;
+    t_bound = dev;
     return MK_OK;
 }
 
-int grow(DevBuf& b, size_t bytes) {
-    if (bytes == 0) bytes = 16;
-    if (b.cap >= bytes) return MK_OK;
-    if (b.p) (void)hipFree(b.p);
-    b.p = nullptr;
-    b.cap = 0;
-    if (hipMalloc(&b.p, bytes) != hipSuccess) return fail(MK_ENOMEM, "hipMalloc(%zu) failed", bytes);
-    b.cap = bytes;
-    return MK_OK;
+DevCtx* ctx() { return g_ctx[t_bound]; }
+
+// The device a call runs on: call->device, else the thread's current device.
+int bind_call() {
+    const mk_call* c = mk::current_call();
+    int dev = c ? c->device : -1;
+    if (dev < 0) {
+        if (probe_devices() <= 0) return fail(MK_ENODEV, "no gfx950 device visible");
+        if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    }
+    return bind_dev(dev);
 }
 
-#define TRY(x)                      \
-    do {                            \
-        int rc_ = (x);              \
-        if (rc_ != MK_OK) return rc_; \
-    } while (0)
+// dev entry points: the device of `stream` (call->device must agree), else as bind_call
+int bind_stream(hipStream_t st) {
+    if (!st) return bind_call();
+    if (probe_devices() <= 0) return fail(MK_ENODEV, "no gfx950 device visible");
+    hipDevice_t d = -1;
+    HIPCHK(hipStreamGetDevice(st, &d));
+    const mk_call* c = mk::current_call();
+    if (c && c->device >= 0 && c->device != (int)d)
+        return fail(MK_EINVAL, "stream belongs to device %d, call->device is %d", (int)d, c->device);
+    return bind_dev((int)d);
+}
+
+// Per-call scope of an extern "C" entry point: installs the call context,
+// restores the thread's current device on exit.
+struct Scope {
+    mk_call* prev;
+    int saved = -1;
+    bool restore = false;
+    explicit Scope(mk_call* c, bool gpu = true) {
+        prev = mk::swap_call(c);
+        if (c) {
+            c->code = MK_OK;
+            c->err[0] = 0;
+        }
+        if (gpu && probe_devices() > 0) restore = hipGetDevice(&saved) == hipSuccess;
+    }
+    int done(int rc) {
+        if (mk::current_call()) mk::current_call()->code = rc;
+        return rc;
+    }
+    ~Scope() {
+        int cur = -1;
+        if (restore && hipGetDevice(&cur) == hipSuccess && cur != saved) (void)hipSetDevice(saved);
+        t_bound = -1;
+        mk::swap_call(prev);
+    }
+};
+
+// Uploads `bytes` of host data to device memory on `st` through the
+// context's small pinned ring (the caller's buffer may die on return).
+int upload_small(DevCtx* c, void* d_dst, const void* src, size_t bytes, hipStream_t st) {
+    if (!bytes) return MK_OK;
+    SmallStage& S = c->small;
+    std::lock_guard<std::mutex> lk(S.mu);
+    const int i = S.next;
+    S.next = (S.next + 1) % SmallStage::kSlots;
+    if (S.used[i]) HIPCHK(hipEventSynchronize(S.ev[i]));
+    if (S.cap[i] < bytes) {
+        if (S.host[i]) (void)hipHostFree(S.host[i]);
+        S.host[i] = nullptr;
+        S.cap[i] = 0;
+        const size_t cap = std::max<size_t>(bytes, 64 << 10);
+        if (hipHostMalloc(&S.host[i], cap, hipHostMallocDefault) != hipSuccess)
+            return fail(MK_ENOMEM, "hipHostMalloc(%zu) failed", cap);
+        S.cap[i] = cap;
+    }
+    std::memcpy(S.host[i], src, bytes);
+    HIPCHK(hipMemcpyAsync(d_dst, S.host[i], bytes, hipMemcpyHostToDevice, st));
+    HIPCHK(hipEventRecord(S.ev[i], st));
+    S.used[i] = true;
+    return MK_OK;
+}
 
 // ---- measurement -------------------------------------------------------------
 struct ProfRec {
@@ -192,186 +251,12 @@ std::mutex g_prof_mu;
 bool g_prof_on = false;
 std::vector<ProfRec> g_prof;
 
-// ---- merkleHash planner ---------------------------------------------------------
-uint64_t chunk_bytes(uint32_t item_len) {
-    return item_len < 128 ? (uint64_t)(128 / item_len) * item_len : item_len;
-}
-uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
-uint64_t perms_for_len(uint64_t len) { return len / 136 + 1; }
-
-struct Pass {
-    bool leaf;
-    bool wave;  // latency pass (k_wave) instead of the throughput pass (k_reduce)
-    uint64_t nwg, nfast;
-    bool w3;      // k_wave3 (bit-interleaved latency form)
-    uint32_t nt;  // threads per workgroup
-    uint32_t ni;  // k_reduce: window pairs per thread (span 512 * ni)
-    ReduceArgs a;
-    int in_ws;   // -1 = user input, else ping-pong slot
-    int out_ws;  // -1 = user output, else ping-pong slot
-    double perms;
-    double hashes;  // digests produced (each ends in one digest-only permutation)
-};
-
-struct Plan {
-    bool small = false;  // <= 1 chunk: one final hash of the raw bytes
-    std::vector<Pass> passes;
-    uint64_t slot_nodes[2] = {0, 0};
-    uint64_t total = 0, n = 0;
-    uint64_t out_nodes = 1;  // nodes written to the output (frontier mode: > 1)
-};
-
-// Hashing levels from `count` nodes down to one (reference loop length).
-uint32_t levels_to_one(uint64_t count) {
-    uint32_t l = 0;
-    while (count > 1) {
-        count = (count + 1) / 2;
-        ++l;
-    }
-    return l;
+bool prof_on() {
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    return g_prof_on;
 }
 
-// Builds the pass sequence.  subtree=false: full merkleHash with the length
-// mix-in; subtree=true: exactly `height` levels above the chunks, output one
-// node (pad_at_one keeps the odd rule alive at count 1).
-// node_input: the input is n 32-B nodes reduced pairwise (a plain binary
-// tree, no chunking; hashutil.MerkleRoot's heap bands, or a gathered tree
-// level for the multi-GPU finisher).  Without subtree mode the final pass
-// mixes in `mixin_n` (the item count of the whole tree), n must be >= 2.
-// frontier (subtree mode): stop `frontier` levels below the subtree root and
-// write the level there (2^frontier nodes, fewer for a ragged shard).
-int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool pad_at_one,
-              bool aligned16, Plan& p, bool node_input = false, uint32_t frontier = 0, uint64_t mixin_n = 0) {
-    p = Plan();
-    p.n = n;
-    if (n > 0 && item_len == 0) return fail(MK_EINVAL, "item_len == 0 (reference: integer divide by zero)");
-    if (node_input && item_len != 32) return fail(MK_EINVAL, "planner: node input is 32-B nodes");
-    if (node_input && !subtree && n < 2) return fail(MK_EINVAL, "planner: node finisher needs >= 2 nodes");
-    if (frontier && (!subtree || frontier >= height)) return fail(MK_EINVAL, "planner: bad frontier %u", frontier);
-    const uint64_t total = n * (uint64_t)item_len;
-    const uint64_t cb = node_input ? 32 : n ? chunk_bytes(item_len) : 128;
-    const uint64_t nchunks = node_input ? n : n ? ceil_div(total, cb) : 0;
-    p.total = total;
-    if (!subtree && nchunks <= 1) {
-        p.small = true;
-        return MK_OK;
-    }
-    if (subtree && (height == 0 || nchunks == 0 || nchunks > (1ull << height)))
-        return fail(MK_EINVAL, "subtree: bad height %u for %llu chunks", height, (unsigned long long)nchunks);
-
-    uint32_t remaining = subtree ? height - frontier : levels_to_one(nchunks);
-    if (frontier) {  // nodes at the frontier level (the odd rule keeps >= 1 with pad_at_one)
-        const uint64_t span = 1ull << (height - frontier);
-        p.out_nodes = std::max<uint64_t>(1, ceil_div(nchunks, span));
-    }
-    bool leaf = !node_input;
-    uint64_t cin = nchunks;  // leaf: chunks; node: input nodes
-    int slot = 0;
-    int in_slot = -1;
-    while (true) {
-        Pass ps{};
-        ps.leaf = leaf;
-        ReduceArgs& a = ps.a;
-        const uint64_t c1 = (cin > 1 || pad_at_one) ? ceil_div(cin, 2) : 1;
-        a.c1 = c1;
-        a.pad_at_one = pad_at_one ? 1 : 0;
-        a.n_items = (node_input && !subtree) ? mixin_n : n;
-        if (leaf) {
-            a.total = total;
-            a.cb = cb;
-            a.nchunks = nchunks;
-            a.c1_full = (cb == 128 && aligned16) ? total / 256 : 0;
-        } else {
-            a.cin = cin;
-            a.c1_full = cin / 2;
-        }
-        // algorithmic permutations of this pass (first level + fused levels)
-        double perms = 0, hashes = 0;
-        if (leaf) {
-            const uint64_t full = total / (2 * cb);
-            perms += (double)std::min<uint64_t>(full, c1) * perms_for_len(2 * cb);
-            for (uint64_t j = full; j < c1; ++j) {  // at most one ragged window
-                const uint64_t lo = j * 2 * cb;
-                const uint64_t len = (2 * j + 1 < nchunks) ? std::min(total, lo + 2 * cb) - lo : total - lo + 128;
-                perms += (double)perms_for_len(len);
-            }
-            hashes += (double)c1;
-        } else if (cin > 1 || pad_at_one) {
-            perms += (double)(cin / 2) + (cin % 2 ? 2.0 : 0.0);
-            hashes += (double)ceil_div(cin, 2);
-        }
-        uint64_t c = c1;
-        const bool wave = c1 <= (leaf || !kWave3 ? kLeafWaveMaxC1 : kNodeWaveMaxC1);
-        const bool w3 = kWave3 && wave && (!leaf || kLeafWave3);
-        // k_wave3: the smallest workgroup (64..1024 threads, 2 per pair) that
-        // keeps the pass within ~256 workgroups, one per CU
-        uint32_t nt = w3 ? mk::kWaveThreads : (wave ? mk::kWaveThreads : kReduceThreads);
-        if (w3) {
-            while (nt < mk::kMidThreads && ceil_div(c1, nt / 2) > kNodeWaveWgs) nt *= 2;
-            if (kTopOneWg)  // the last <= 512 pairs in one workgroup: one launch to the root
-                while (nt < mk::kMidThreads && c1 <= mk::kMidThreads / 2 && c1 > nt / 2) nt *= 2;
-        }
-        // throughput pass: 2 window pairs per thread on wide passes, 1 on mid-size
-        // leaf passes so they still spread over the CUs
-        const uint32_t ni = (!wave && leaf && c1 < kReduceNi2MinC1) ? 1 : 2;
-        const uint64_t span = w3 ? nt / 2 : wave ? (kWave2 ? mk::kWave2Span : mk::kWaveThreads)
-                                                 : (uint64_t)2 * ni * kReduceThreads;
-        const bool final_pass = c1 <= span;
-        const uint32_t max_lv = w3 ? 1 + ilog2(nt / 2)
-                              : wave ? (kWave2 ? mk::kWave2Levels : mk::kWaveLevels) : mk::kMaxPassLevels;
-        uint32_t lv = final_pass ? remaining : std::min<uint32_t>(max_lv, remaining);
-        for (uint32_t l = 1; l < lv; ++l) {  // fused levels above the first
-            if (c <= 1 && !pad_at_one) break;
-            perms += (double)(c / 2) + (c % 2 ? 2.0 : 0.0);
-            hashes += (double)ceil_div(c, 2);
-            c = ceil_div(c, 2);
-        }
-        ps.perms = perms;
-        ps.hashes = hashes;
-        ps.wave = wave;
-        ps.nt = nt;
-        a.in_ilv = (w3 && !leaf && !p.passes.empty() && p.passes.back().w3) ? 1 : 0;
-        ps.w3 = w3;
-        a.out_ilv = w3 ? 1 : 0;  // cleared below for the final pass
-        a.levels = lv;
-        ps.nwg = ceil_div(c1, span);
-        ps.nfast = wave ? 0 : std::min<uint64_t>(ps.nwg, a.c1_full / span);
-        ps.ni = ni;
-        ps.in_ws = in_slot;
-        if (final_pass) {
-            if (!subtree) {
-                a.finalize = 1;
-                a.levels = 64;
-            } else if (!wave && c1 > span / 2 && lv < 2) {
-                return fail(MK_EINVAL, "planner: unsupported single-level pass");
-            }
-            ps.out_ws = -1;
-            ps.a.out_ilv = 0;
-            p.passes.push_back(ps);
-            break;
-        }
-        if (!wave && lv < 2)  // k_reduce always folds the pair level (a frontier one level above the chunks)
-            return fail(MK_EINVAL, "planner: unsupported single-level pass (frontier %u of height %u)", frontier,
-                        height);
-        if (frontier && remaining == lv) {  // the frontier level: plain nodes to the output
-            ps.out_ws = -1;
-            ps.a.out_ilv = 0;
-            p.passes.push_back(ps);
-            break;
-        }
-        ps.out_ws = slot;
-        p.slot_nodes[slot] = std::max<uint64_t>(p.slot_nodes[slot], c);
-        p.passes.push_back(ps);
-        remaining -= lv;
-        in_slot = slot;
-        slot ^= 1;
-        leaf = false;
-        cin = c;
-        if (remaining == 0) return fail(MK_EINVAL, "planner: ran out of levels");
-    }
-    return MK_OK;
-}
-
+// ---- merkleHash plan launch --------------------------------------------------------
 template <bool LEAF>
 void launch_wave3(uint32_t nt, uint64_t nwg, const ReduceArgs& a, hipStream_t st) {
     switch (nt) {
@@ -383,8 +268,6 @@ void launch_wave3(uint32_t nt, uint64_t nwg, const ReduceArgs& a, hipStream_t st
     }
 }
 
-uint64_t plan_ws_bytes(const Plan& p) { return 32 * (p.slot_nodes[0] + p.slot_nodes[1]) + 256; }
-
 int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t* d_ws, uint64_t ws_bytes,
                 hipStream_t st) {
     if (p.small) {
@@ -392,14 +275,11 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
         HIPCHK(hipGetLastError());
         return MK_OK;
     }
-    if (ws_bytes < plan_ws_bytes(p)) return fail(MK_ENOMEM, "workspace too small: %llu < %llu",
-                                                 (unsigned long long)ws_bytes, (unsigned long long)plan_ws_bytes(p));
+    if (ws_bytes < mk::plan_ws_bytes(p))
+        return fail(MK_ENOMEM, "workspace too small: %llu < %llu", (unsigned long long)ws_bytes,
+                    (unsigned long long)mk::plan_ws_bytes(p));
     uint8_t* slots[2] = {d_ws, d_ws + 32 * p.slot_nodes[0]};
-    bool prof;
-    {
-        std::lock_guard<std::mutex> lk(g_prof_mu);
-        prof = g_prof_on;
-    }
+    const bool prof = prof_on();
     for (const Pass& ps : p.passes) {
         ReduceArgs a = ps.a;
         a.items = ps.in_ws < 0 ? d_items : slots[ps.in_ws];
@@ -418,16 +298,11 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                     launch_wave3<true>(ps.nt, ps.nwg, a, st);
                 else
                     launch_wave3<false>(ps.nt, ps.nwg, a, st);
-            } else if (kWave2) {
+            } else {
                 if (ps.leaf)
                     hipLaunchKernelGGL((mk::k_wave2<true>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
                 else
                     hipLaunchKernelGGL((mk::k_wave2<false>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
-            } else {
-                if (ps.leaf)
-                    hipLaunchKernelGGL((mk::k_wave<true>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
-                else
-                    hipLaunchKernelGGL((mk::k_wave<false>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
             }
             HIPCHK(hipGetLastError());
         } else {
@@ -435,7 +310,7 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
             // also has full workgroups they go first, on the side stream, so
             // they overlap the full ones (fork/join through events on `st`).
             const bool ragged = ps.nwg > ps.nfast;
-            DevCtx* c = (ragged && ps.nfast) ? g_ctx[t_dev] : nullptr;
+            DevCtx* c = (ragged && ps.nfast) ? ctx() : nullptr;
             std::unique_lock<std::mutex> lk;
             if (ragged) {
                 hipStream_t gs = st;
@@ -482,75 +357,10 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
     return MK_OK;
 }
 
-struct Locked {
-    DevCtx* c;
-    std::unique_lock<std::mutex> lk;
-};
-
-int lock_current(Locked& L) {
-    TRY(bind(-1));
-    L.c = g_ctx[t_dev];
-    L.lk = std::unique_lock<std::mutex>(L.c->mu);
-    return MK_OK;
-}
-
-int shard_plan(uint64_t n, uint32_t item_len, uint32_t nshards, uint32_t* height, uint32_t* nonempty,
-               uint64_t* begin) {
-    if (nshards == 0) return fail(MK_EINVAL, "nshards == 0");
-    if (n > 0 && item_len == 0) return fail(MK_EINVAL, "item_len == 0");
-    const uint64_t total = n * (uint64_t)item_len;
-    const uint64_t cb = n ? chunk_bytes(item_len) : 128;
-    const uint64_t per_chunk_items = item_len < 128 ? 128 / item_len : 1;
-    const uint64_t nchunks = n ? ceil_div(total, cb) : 0;
-    uint32_t h = 0;
-    while ((1ull << h) * nshards < nchunks) ++h;
-    uint64_t ne = nchunks ? ceil_div(nchunks, 1ull << h) : 0;
-    if (h == 0 || ne <= 1) {  // too small to shard: everything on shard 0
-        *height = h;
-        *nonempty = 1;
-        for (uint32_t s = 0; s <= nshards; ++s) begin[s] = s == 0 ? 0 : n;
-        return MK_OK;
-    }
-    *height = h;
-    *nonempty = (uint32_t)ne;
-    for (uint32_t s = 0; s <= nshards; ++s) {
-        const uint64_t item = (uint64_t)s * (1ull << h) * per_chunk_items;
-        begin[s] = item < n ? item : n;
-    }
-    return MK_OK;
-}
-
-}  // namespace
-
-// =============================================================================
-extern "C" {
-
-const char* mk_version(void) { return "prysm_merkle 0.1 (gfx950)"; }
-
-const char* mk_strerror(int code) {
-    switch (code) {
-        case MK_OK: return "ok";
-        case MK_EINVAL: return "invalid argument";
-        case MK_ENODEV: return "no usable gfx950 device";
-        case MK_ENOMEM: return "out of memory";
-        case MK_EHIP: return "HIP runtime error";
-        case MK_ECOMM: return "RCCL error";
-        default: return "unknown error";
-    }
-}
-
-const char* mk_last_error(void) { return t_err.c_str(); }
-
-int mk_device_count(void) { return probe_devices(); }
-
-int mk_init(int device) { return bind(device < 0 ? 0 : device); }
-
-// ---- hashing ------------------------------------------------------------------
-int mk_dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, void* stream) {
-    TRY(bind(-1));
+// ---- hashing ----------------------------------------------------------------------
+int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, hipStream_t st) {
     if (n == 0) return MK_OK;
-    if (!d_in || !d_out) return fail(MK_EINVAL, "null pointer");
-    hipStream_t st = (hipStream_t)stream;
+    if (!d_out || (!d_in && msg_len)) return fail(MK_EINVAL, "null pointer");
     const uint64_t grid = ceil_div(n, 256);
     if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0)
         hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
@@ -568,165 +378,46 @@ int mk_dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_ou
     return MK_OK;
 }
 
-int mk_dev_hash_batch_var(const void* d_in, const uint64_t* d_offs, uint64_t n, void* d_out, void* stream) {
-    TRY(bind(-1));
+int dev_hash_var(const void* d_in, const uint64_t* d_offs, uint64_t n, void* d_out, hipStream_t st) {
     if (n == 0) return MK_OK;
-    hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, (hipStream_t)stream,
-                       (const uint8_t*)d_in, d_offs, n, (uint4*)d_out);
+    if (!d_offs || !d_out) return fail(MK_EINVAL, "null pointer");
+    hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_in, d_offs, n,
+                       (uint4*)d_out);
     HIPCHK(hipGetLastError());
     return MK_OK;
 }
 
-int mk_hash_batch(const uint8_t* in, uint64_t n, uint32_t msg_len, uint8_t* out) {
-    if (n && (!in && msg_len) ) return fail(MK_EINVAL, "null input");
-    if (n && !out) return fail(MK_EINVAL, "null output");
-    Locked L;
-    TRY(lock_current(L));
+// Leaf hashes of deposits/values: offsets (device) or fixed-length records.
+int dev_leaf_hashes(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len, uint4* out,
+                    hipStream_t st) {
     if (n == 0) return MK_OK;
-    const size_t inb = n * (size_t)msg_len;
-    TRY(grow(L.c->in, inb));
-    TRY(grow(L.c->out, 32 * n));
-    hipStream_t st = L.c->stream;
-    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, in, inb, hipMemcpyHostToDevice, st));
-    TRY(mk_dev_hash_batch(L.c->in.p, n, msg_len, L.c->out.p, st));
-    HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32 * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return MK_OK;
+    if (d_offs) return dev_hash_var(d_data, d_offs, n, out, st);
+    return dev_hash_batch(d_data, n, fixed_len, out, st);
 }
 
-int mk_hash(const uint8_t* data, uint64_t len, uint8_t out[32]) {
-    if (len > UINT32_MAX) {
-        uint64_t offs[2] = {0, len};
-        return mk_hash_batch_var(data, offs, 1, out);
-    }
-    static const uint8_t empty = 0;
-    return mk_hash_batch(len ? data : &empty, 1, (uint32_t)len, out);
+// Uniform message length of offs[0..n] (relative), or -1.
+int64_t uniform_len(const uint64_t* offs, uint64_t n) {
+    const uint64_t len0 = offs[1] - offs[0];
+    for (uint64_t i = 1; i < n; ++i)
+        if (offs[i + 1] - offs[i] != len0) return -1;
+    return len0 <= UINT32_MAX ? (int64_t)len0 : -1;
 }
 
-int mk_hash_batch_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint8_t* out) {
-    if (n && (!offs || !out)) return fail(MK_EINVAL, "null pointer");
-    Locked L;
-    TRY(lock_current(L));
-    if (n == 0) return MK_OK;
-    const size_t inb = offs[n];
-    TRY(grow(L.c->in, inb));
-    TRY(grow(L.c->aux, 8 * (n + 1)));
-    TRY(grow(L.c->out, 32 * n));
-    hipStream_t st = L.c->stream;
-    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, in, inb, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(L.c->aux.p, offs, 8 * (n + 1), hipMemcpyHostToDevice, st));
-    TRY(mk_dev_hash_batch_var(L.c->in.p, (const uint64_t*)L.c->aux.p, n, L.c->out.p, st));
-    HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32 * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return MK_OK;
-}
-
-// ---- merkleHash ---------------------------------------------------------------
-uint64_t mk_ssz_merkle_workspace_bytes(uint64_t n, uint32_t item_len) {
+// ---- merkleHash entry bodies -------------------------------------------------------
+int dev_merkle_hash(const void* d_items, uint64_t n, uint32_t item_len, void* d_out32, void* d_ws, uint64_t ws_bytes,
+                    hipStream_t st) {
+    if (!d_out32 || (n && item_len && !d_items)) return fail(MK_EINVAL, "null pointer");
     Plan p;
-    if (make_plan(n, item_len, false, 0, false, true, p) != MK_OK) return 0;
-    return p.small ? 256 : plan_ws_bytes(p);
+    TRY(mk::make_plan(n, item_len, false, 0, false, ((uintptr_t)d_items % 16) == 0, p));
+    return launch_plan(p, (const uint8_t*)d_items, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st);
 }
 
-int mk_dev_ssz_merkle_hash(const void* d_items, uint64_t n, uint32_t item_len, void* d_out32, void* d_ws,
-                           uint64_t ws_bytes, void* stream) {
-    TRY(bind(-1));
-    if (!d_out32 || (n && !d_items)) return fail(MK_EINVAL, "null pointer");
-    Plan p;
-    TRY(make_plan(n, item_len, false, 0, false, ((uintptr_t)d_items % 16) == 0, p));
-    return launch_plan(p, (const uint8_t*)d_items, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes,
-                       (hipStream_t)stream);
-}
-
-int mk_ssz_merkle_hash(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t out[32]) {
-    if (!out || (n && item_len && !items)) return fail(MK_EINVAL, "null pointer");
-    Locked L;
-    TRY(lock_current(L));
-    Plan p;
-    TRY(make_plan(n, item_len, false, 0, false, true, p));
-    const size_t inb = n * (size_t)item_len;
-    TRY(grow(L.c->in, inb));
-    TRY(grow(L.c->out, 32));
-    TRY(grow(L.c->ws, p.small ? 256 : plan_ws_bytes(p)));
-    hipStream_t st = L.c->stream;
-    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, items, inb, hipMemcpyHostToDevice, st));
-    TRY(launch_plan(p, (const uint8_t*)L.c->in.p, (uint8_t*)L.c->out.p, (uint8_t*)L.c->ws.p, L.c->ws.cap, st));
-    HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return MK_OK;
-}
-
-// ---- sharding -------------------------------------------------------------------
-int mk_ssz_merkle_shard_plan(uint64_t n, uint32_t item_len, uint32_t nshards, uint32_t* height,
-                             uint32_t* nonempty, uint64_t* item_begin) {
-    if (!height || !nonempty || !item_begin) return fail(MK_EINVAL, "null pointer");
-    return shard_plan(n, item_len, nshards, height, nonempty, item_begin);
-}
-
-int mk_dev_ssz_merkle_subtree(const void* d_shard_items, uint64_t shard_n, uint32_t item_len, uint32_t height,
-                              int pad_at_one, void* d_out32, void* d_ws, uint64_t ws_bytes, void* stream) {
-    TRY(bind(-1));
-    Plan p;
-    TRY(make_plan(shard_n, item_len, true, height, pad_at_one != 0, ((uintptr_t)d_shard_items % 16) == 0, p));
-    return launch_plan(p, (const uint8_t*)d_shard_items, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes,
-                       (hipStream_t)stream);
-}
-
-int mk_dev_ssz_merkle_subtree_frontier(const void* d_shard_items, uint64_t shard_n, uint32_t item_len,
-                                       uint32_t height, uint32_t frontier_log2, int pad_at_one, void* d_out,
-                                       uint64_t* nodes_out, void* d_ws, uint64_t ws_bytes, void* stream) {
-    TRY(bind(-1));
-    if (!d_out || (shard_n && !d_shard_items)) return fail(MK_EINVAL, "null pointer");
-    Plan p;
-    TRY(make_plan(shard_n, item_len, true, height, pad_at_one != 0, ((uintptr_t)d_shard_items % 16) == 0, p, false,
-                  frontier_log2));
-    if (nodes_out) *nodes_out = p.out_nodes;
-    return launch_plan(p, (const uint8_t*)d_shard_items, (uint8_t*)d_out, (uint8_t*)d_ws, ws_bytes,
-                       (hipStream_t)stream);
-}
-
-uint64_t mk_ssz_merkle_node_frontier_workspace_bytes(uint64_t count, uint32_t height, uint32_t frontier_log2) {
-    Plan p;
-    if (make_plan(count, 32, true, height, true, true, p, true, frontier_log2) != MK_OK) return 0;
-    return std::max<uint64_t>(256, plan_ws_bytes(p));
-}
-
-int mk_dev_ssz_merkle_node_frontier(const void* d_nodes, uint64_t count, uint32_t height, uint32_t frontier_log2,
-                                    int pad_at_one, void* d_out, uint64_t* nodes_out, void* d_ws, uint64_t ws_bytes,
-                                    void* stream) {
-    TRY(bind(-1));
-    if (!d_out || !d_nodes || count == 0) return fail(MK_EINVAL, "null pointer or empty level");
-    Plan p;
-    TRY(make_plan(count, 32, true, height, pad_at_one != 0, ((uintptr_t)d_nodes % 16) == 0, p, true,
-                  frontier_log2));
-    if (nodes_out) *nodes_out = frontier_log2 ? p.out_nodes : 1;
-    return launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out, (uint8_t*)d_ws, ws_bytes, (hipStream_t)stream);
-}
-
-uint64_t mk_ssz_merkle_finish_workspace_bytes(uint64_t count) {
-    Plan p;
-    if (count <= 2 * mk::kWave2Span) return 256;
-    if (make_plan(count, 32, false, 0, false, true, p, true, 0, 1) != MK_OK) return 0;
-    return plan_ws_bytes(p);
-}
-
-int mk_dev_ssz_merkle_finish_nodes(const void* d_nodes, uint64_t count, uint64_t n_total, void* d_out32,
-                                   void* d_ws, uint64_t ws_bytes, void* stream) {
-    if (count <= 2 * mk::kWave2Span) return mk_dev_ssz_merkle_finish(d_nodes, count, n_total, d_out32, stream);
-    TRY(bind(-1));
-    if (!d_nodes || !d_out32) return fail(MK_EINVAL, "null pointer");
-    Plan p;
-    TRY(make_plan(count, 32, false, 0, false, ((uintptr_t)d_nodes % 16) == 0, p, true, 0, n_total));
-    return launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, (hipStream_t)stream);
-}
-
-int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32, void* stream) {
-    TRY(bind(-1));
+int dev_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32, hipStream_t st) {
     if (nroots == 0 || nroots > 2 * mk::kWave2Span)
         return fail(MK_EINVAL, "nroots %llu out of range (1..%u)", (unsigned long long)nroots, 2 * mk::kWave2Span);
+    if (!d_roots || !d_out32) return fail(MK_EINVAL, "null pointer");
     // the reference level loop over the shard roots (odd -> 0^128) plus the
     // length mix-in is one finalizing node pass of the two-lane latency kernel
-    // (plain 32-B roots in, plain digest out)
     ReduceArgs a{};
     a.items = (const uint8_t*)d_roots;
     a.cin = nroots;
@@ -736,94 +427,88 @@ int mk_dev_ssz_merkle_finish(const void* d_roots, uint64_t nroots, uint64_t n_to
     a.n_items = n_total;
     a.levels = 64;
     a.finalize = 1;
-    launch_wave3<false>(mk::kWaveThreads, 1, a, (hipStream_t)stream);
+    launch_wave3<false>(mk::kWaveThreads, 1, a, st);
     HIPCHK(hipGetLastError());
     return MK_OK;
 }
 
-int mk_ssz_merkle_hash_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int ndev, uint8_t out[32]) {
-    if (ndev <= 1) return mk_ssz_merkle_hash(items, n, item_len, out);
-    if (probe_devices() < ndev) return fail(MK_ENODEV, "%d devices requested, %d visible", ndev, g_ndev);
-    uint32_t h = 0, ne = 0;
-    std::vector<uint64_t> begin(ndev + 1);
-    TRY(shard_plan(n, item_len, (uint32_t)ndev, &h, &ne, begin.data()));
-    if (ne <= 1) return mk_ssz_merkle_hash(items, n, item_len, out);
+uint64_t finish_ws_bytes(uint64_t count) {
+    Plan p;
+    if (count <= 2 * mk::kWave2Span) return 256;
+    if (mk::make_plan(count, 32, false, 0, false, true, p, true, 0, 1) != MK_OK) return 0;
+    return mk::plan_ws_bytes(p);
+}
 
-    static std::mutex comm_mu;
-    static std::vector<ncclComm_t> comms;
-    std::lock_guard<std::mutex> clk(comm_mu);
-    if ((int)comms.size() != ndev) {
-        for (auto c : comms) ncclCommDestroy(c);
-        comms.assign(ndev, nullptr);
-        std::vector<int> devs(ndev);
-        for (int d = 0; d < ndev; ++d) devs[d] = d;
-        if (ncclCommInitAll(comms.data(), ndev, devs.data()) != ncclSuccess) {
-            comms.clear();
-            return fail(MK_ECOMM, "ncclCommInitAll(%d) failed", ndev);
-        }
+int dev_finish_nodes(const void* d_nodes, uint64_t count, uint64_t n_total, void* d_out32, void* d_ws,
+                     uint64_t ws_bytes, hipStream_t st) {
+    if (count <= 2 * mk::kWave2Span) return dev_finish(d_nodes, count, n_total, d_out32, st);
+    if (!d_nodes || !d_out32) return fail(MK_EINVAL, "null pointer");
+    Plan p;
+    TRY(mk::make_plan(count, 32, false, 0, false, ((uintptr_t)d_nodes % 16) == 0, p, true, 0, n_total));
+    return launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st);
+}
+
+int host_merkle_hash(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t* out) {
+    if (!out || (n && item_len && !items)) return fail(MK_EINVAL, "null pointer");
+    TRY(bind_call());
+    DevCtx* c = ctx();
+    std::lock_guard<std::mutex> lk(c->mu);
+    Plan p;
+    TRY(mk::make_plan(n, item_len, false, 0, false, true, p));
+    const size_t inb = n * (size_t)item_len;
+    TRY(grow(c->in, inb));
+    TRY(grow(c->out, 32));
+    TRY(grow(c->ws, p.small ? 256 : mk::plan_ws_bytes(p)));
+    hipStream_t st = c->stream;
+    if (inb) HIPCHK(hipMemcpyAsync(c->in.p, items, inb, hipMemcpyHostToDevice, st));
+    TRY(launch_plan(p, (const uint8_t*)c->in.p, (uint8_t*)c->out.p, (uint8_t*)c->ws.p, c->ws.cap, st));
+    HIPCHK(hipMemcpyAsync(out, c->out.p, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+// ---- many lists ------------------------------------------------------------------------
+int dev_merkle_many(const void* d_items, const mk::ManyPlan& mp, uint32_t nlists, void* d_roots, void* d_ws,
+                    uint64_t ws_bytes, hipStream_t st) {
+    if (ws_bytes < mp.ws_bytes)
+        return fail(MK_ENOMEM, "workspace too small: %llu < %llu", (unsigned long long)ws_bytes,
+                    (unsigned long long)mp.ws_bytes);
+    if (nlists == 0) return MK_OK;
+    if (!d_roots || !d_ws) return fail(MK_EINVAL, "null pointer");
+    uint8_t* ws = (uint8_t*)d_ws;
+    auto* lists = (mk::ManyList*)(ws + mp.off_lists);
+    auto* act = (mk::ManyAct*)(ws + mp.off_act);
+    uint4* buf[2] = {(uint4*)(ws + mp.off_buf0), (uint4*)(ws + mp.off_buf1)};
+    DevCtx* c = ctx();
+    TRY(upload_small(c, lists, mp.lists.data(), sizeof(mk::ManyList) * nlists, st));
+    TRY(upload_small(c, act, mp.act.data(), sizeof(mk::ManyAct) * mp.act.size(), st));
+    const uint8_t* items = (const uint8_t*)d_items;
+    for (uint32_t l = 0; l < mp.nlevels; ++l) {  // level l+1 into buffer l % 2
+        const uint64_t nodes = mp.lvl_nodes[l];
+        const uint32_t nact = (uint32_t)(mp.lvl_begin[l + 1] - mp.lvl_begin[l]);
+        if (!nodes) continue;
+        const mk::ManyAct* a = act + mp.lvl_begin[l];
+        if (l == 0)
+            hipLaunchKernelGGL((mk::k_many_level<true>), dim3(ceil_div(nodes, 256)), dim3(256), 0, st, items, lists, a,
+                               nact, nodes, (const uint4*)nullptr, buf[0]);
+        else
+            hipLaunchKernelGGL((mk::k_many_level<false>), dim3(ceil_div(nodes, 256)), dim3(256), 0, st, items, lists,
+                               a, nact, nodes, (const uint4*)buf[(l - 1) % 2], buf[l % 2]);
+        HIPCHK(hipGetLastError());
     }
-    std::vector<std::unique_lock<std::mutex>> locks;
-    std::vector<DevCtx*> ctx(ndev);
-    for (int d = 0; d < ndev; ++d) {
-        TRY(bind(d));
-        ctx[d] = g_ctx[d];
-        locks.emplace_back(ctx[d]->mu);
+    hipLaunchKernelGGL(mk::k_many_final, dim3(ceil_div(nlists, 256)), dim3(256), 0, st, items, lists, nlists,
+                       (const uint4*)buf[0], (const uint4*)buf[1], (uint4*)d_roots);
+    HIPCHK(hipGetLastError());
+    for (size_t b = 0; b < mp.big.size(); ++b) {  // big lists: their own fused plans, one shared workspace
+        const mk::ManyList& L = mp.lists[mp.big[b]];
+        TRY(launch_plan(mp.big_plans[b], items + L.items_off, (uint8_t*)d_roots + 32 * (uint64_t)mp.big[b],
+                        ws + mp.off_big, ws_bytes - mp.off_big, st));
     }
-    // per device: shard upload + reduce to the shard's frontier level (2^k
-    // nodes, k levels below the shard root) into block `d` of the level buffer
-    const uint32_t k = h > 5 ? std::min<uint32_t>(10, h - 5) : 0;
-    const size_t block = (size_t)32 << k;
-    uint64_t last_nodes = 1;
-    for (int d = 0; d < ndev; ++d) {
-        TRY(bind(d));
-        DevCtx* c = ctx[d];
-        const uint64_t sn = begin[d + 1] - begin[d];
-        const size_t inb = sn * (size_t)item_len;
-        TRY(grow(c->in, inb));
-        TRY(grow(c->out, block * ndev + 32));
-        uint8_t* lvl = (uint8_t*)c->out.p;
-        if (sn) {
-            Plan p;
-            TRY(make_plan(sn, item_len, true, h, true, true, p, false, k));
-            if (d == (int)ne - 1) last_nodes = p.out_nodes;
-            TRY(grow(c->ws, plan_ws_bytes(p)));
-            HIPCHK(hipMemcpyAsync(c->in.p, items + begin[d] * item_len, inb, hipMemcpyHostToDevice, c->stream));
-            TRY(launch_plan(p, (const uint8_t*)c->in.p, lvl + block * d, (uint8_t*)c->ws.p, c->ws.cap, c->stream));
-        } else {
-            HIPCHK(hipMemsetAsync(lvl + block * d, 0, block, c->stream));
-        }
-    }
-    // gather the frontier blocks over RCCL (in place: block d of every device)
-    if (ncclGroupStart() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupStart");
-    for (int d = 0; d < ndev; ++d) {
-        uint8_t* lvl = (uint8_t*)ctx[d]->out.p;
-        if (ncclAllGather(lvl + block * d, lvl, block, ncclUint8, comms[d], ctx[d]->stream) != ncclSuccess) {
-            ncclGroupEnd();
-            return fail(MK_ECOMM, "ncclAllGather on device %d", d);
-        }
-    }
-    if (ncclGroupEnd() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupEnd");
-    TRY(bind(0));
-    uint8_t* lvl0 = (uint8_t*)ctx[0]->out.p;
-    const uint64_t count = ((uint64_t)(ne - 1) << k) + last_nodes;
-    if (k) {
-        TRY(grow(ctx[0]->ws, mk_ssz_merkle_finish_workspace_bytes(count)));
-        TRY(mk_dev_ssz_merkle_finish_nodes(lvl0, count, n, lvl0 + block * ndev, ctx[0]->ws.p, ctx[0]->ws.cap,
-                                           ctx[0]->stream));
-    } else {
-        TRY(mk_dev_ssz_merkle_finish(lvl0, ne, n, lvl0 + block * ndev, ctx[0]->stream));
-    }
-    HIPCHK(hipMemcpyAsync(out, lvl0 + block * ndev, 32, hipMemcpyDeviceToHost, ctx[0]->stream));
-    for (int d = 0; d < ndev; ++d) {
-        TRY(bind(d));
-        HIPCHK(hipStreamSynchronize(ctx[d]->stream));
-    }
-    TRY(bind(0));
     return MK_OK;
 }
 
 // ---- struct hashing ---------------------------------------------------------------
-static int make_spec(const mk_field* fields, uint32_t nfields, uint32_t record_len, mk::StructSpec& sp) {
+int make_spec(const mk_field* fields, uint32_t nfields, uint32_t record_len, mk::StructSpec& sp) {
     if (!fields || nfields == 0 || nfields > mk::kMaxStructFields)
         return fail(MK_EINVAL, "nfields %u out of range (1..%u)", nfields, mk::kMaxStructFields);
     std::memset(&sp, 0, sizeof sp);
@@ -854,8 +539,8 @@ static int make_spec(const mk_field* fields, uint32_t nfields, uint32_t record_l
 }
 
 // roots of n records into d_roots (n x 32); d_msg holds n x msg_len bytes
-static int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp, void* d_msg, void* d_roots,
-                               hipStream_t st) {
+int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp, void* d_msg, void* d_roots,
+                        hipStream_t st) {
     if (n == 0) return MK_OK;
     // fused path: dword-granular single-block fields, dword-aligned message
     bool fused = kStructFused && sp.msg_len % 4 == 0 && sp.msg_len <= mk::kStructFusedMaxMsg &&
@@ -897,13 +582,7 @@ static int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSp
     return MK_OK;
 }
 
-extern "C" uint64_t mk_ssz_struct_msg_len(const mk_field* fields, uint32_t nfields) {
-    mk::StructSpec sp;
-    if (make_spec(fields, nfields, 0, sp) != MK_OK) return 0;
-    return sp.msg_len;
-}
-
-static uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 // host-buffer entries: H2D in up to kH2dChunks pieces of at least kH2dMinChunk records
 #ifndef MK_H2D_CHUNKS
 #define MK_H2D_CHUNKS 8
@@ -914,94 +593,11 @@ static uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 constexpr uint64_t kH2dChunks = MK_H2D_CHUNKS;
 constexpr uint64_t kH2dMinChunk = MK_H2D_MIN_CHUNK;
 
-extern "C" uint64_t mk_ssz_struct_list_workspace_bytes(uint64_t n, const mk_field* fields, uint32_t nfields) {
-    mk::StructSpec sp;
-    if (make_spec(fields, nfields, 0, sp) != MK_OK) return 0;
-    return align256(n * sp.msg_len) + align256(32 * n) + mk_ssz_merkle_workspace_bytes(n, 32);
-}
-
-extern "C" int mk_dev_ssz_struct_list_root(const void* d_records, uint64_t n, uint32_t record_len,
-                                           const mk_field* fields, uint32_t nfields, void* d_out32, void* d_ws,
-                                           uint64_t ws_bytes, void* stream) {
-    TRY(bind(-1));
-    mk::StructSpec sp;
-    TRY(make_spec(fields, nfields, record_len, sp));
-    if (ws_bytes < mk_ssz_struct_list_workspace_bytes(n, fields, nfields)) return fail(MK_ENOMEM, "workspace too small");
-    uint8_t* ws = (uint8_t*)d_ws;
-    uint8_t* msg = ws;
-    uint8_t* roots = ws + align256(n * sp.msg_len);
-    uint8_t* mws = roots + align256(32 * n);
-    hipStream_t st = (hipStream_t)stream;
-    TRY(launch_struct_roots(d_records, n, sp, msg, roots, st));
-    return mk_dev_ssz_merkle_hash(roots, n, 32, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), stream);
-}
-
-extern "C" int mk_dev_ssz_struct_roots(const void* d_records, uint64_t n, uint32_t record_len,
-                                       const mk_field* fields, uint32_t nfields, void* d_roots, void* d_ws,
-                                       uint64_t ws_bytes, void* stream) {
-    TRY(bind(-1));
-    mk::StructSpec sp;
-    TRY(make_spec(fields, nfields, record_len, sp));
-    if (n && (!d_records || !d_roots)) return fail(MK_EINVAL, "null pointer");
-    if (ws_bytes < n * (uint64_t)sp.msg_len) return fail(MK_ENOMEM, "workspace too small");
-    TRY(launch_struct_roots(d_records, n, sp, d_ws, d_roots, (hipStream_t)stream));
-    return MK_OK;
-}
-
-extern "C" int mk_ssz_struct_roots(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
-                                   uint32_t nfields, uint8_t* roots) {
-    mk::StructSpec sp;
-    TRY(make_spec(fields, nfields, record_len, sp));
-    if (n && (!records || !roots)) return fail(MK_EINVAL, "null pointer");
-    Locked L;
-    TRY(lock_current(L));
-    if (n == 0) return MK_OK;
-    hipStream_t st = L.c->stream;
-    TRY(grow(L.c->in, n * (size_t)record_len));
-    TRY(grow(L.c->ws, align256(n * sp.msg_len)));
-    TRY(grow(L.c->out, 32 * n));
-    HIPCHK(hipMemcpyAsync(L.c->in.p, records, n * (size_t)record_len, hipMemcpyHostToDevice, st));
-    TRY(launch_struct_roots(L.c->in.p, n, sp, L.c->ws.p, L.c->out.p, st));
-    HIPCHK(hipMemcpyAsync(roots, L.c->out.p, 32 * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return MK_OK;
-}
-
-extern "C" int mk_ssz_struct_list_root(const uint8_t* records, uint64_t n, uint32_t record_len,
-                                       const mk_field* fields, uint32_t nfields, uint8_t out[32]) {
-    mk::StructSpec sp;
-    TRY(make_spec(fields, nfields, record_len, sp));
-    if (!out || (n && !records)) return fail(MK_EINVAL, "null pointer");
-    Locked L;
-    TRY(lock_current(L));
-    hipStream_t st = L.c->stream;
-    const uint64_t wsb = mk_ssz_struct_list_workspace_bytes(n, fields, nfields);
-    TRY(grow(L.c->in, n * (size_t)record_len));
-    TRY(grow(L.c->ws, wsb));
-    TRY(grow(L.c->out, 32));
-    // Same layout as mk_dev_ssz_struct_list_root.  The records cross PCIe in
-    // chunks on the copy stream; the struct-roots kernel of chunk i runs on
-    // the compute stream while chunk i+1 is in flight, so only the last
-    // chunk's roots and the list merkleHash follow the copy.
-    uint8_t* ws = (uint8_t*)L.c->ws.p;
-    uint8_t* msg = ws;
-    uint8_t* roots = ws + align256(n * sp.msg_len);
-    uint8_t* mws = roots + align256(32 * n);
-    const uint8_t* din = (const uint8_t*)L.c->in.p;
-    uint64_t chunk = std::max<uint64_t>(kH2dMinChunk, ceil_div(n, kH2dChunks));
-    chunk = (chunk + 15) & ~15ull;  // chunk starts keep the records' 16-B alignment
-    for (uint64_t off = 0; off < n; off += chunk) {
-        const uint64_t cnt = std::min(chunk, n - off);
-        HIPCHK(hipMemcpyAsync((uint8_t*)L.c->in.p + off * record_len, records + off * record_len,
-                              cnt * (size_t)record_len, hipMemcpyHostToDevice, L.c->copy));
-        HIPCHK(hipEventRecord(L.c->h2d, L.c->copy));
-        HIPCHK(hipStreamWaitEvent(st, L.c->h2d, 0));
-        TRY(launch_struct_roots(din + off * record_len, cnt, sp, msg + off * sp.msg_len, roots + 32 * off, st));
-    }
-    TRY(mk_dev_ssz_merkle_hash(roots, n, 32, L.c->out.p, mws, wsb - (uint64_t)(mws - ws), st));
-    HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    return MK_OK;
+uint64_t struct_list_ws(uint64_t n, const mk::StructSpec& sp) {
+    Plan p;
+    uint64_t mws = 256;
+    if (mk::make_plan(n, 32, false, 0, false, true, p) == MK_OK && !p.small) mws = mk::plan_ws_bytes(p);
+    return align256(n * sp.msg_len) + align256(32 * n) + mws;
 }
 
 // ---- hashutil.MerkleRoot (merkleRoot.go:12-30) ------------------------------------
@@ -1012,43 +608,29 @@ extern "C" int mk_ssz_struct_list_root(const uint8_t* records, uint64_t n, uint3
 // level over o[2P, 2n), and everything above is a power-of-two binary tree
 // over o[P, 2P) -- a node-input merkle plan.  (The reference's spurious
 // newSet[0] = Hash(nil || o[1]) is computed and discarded; it is skipped.)
-static uint64_t pow2_floor(uint64_t n) {
+uint64_t pow2_floor(uint64_t n) {
     uint64_t p = 1;
     while (p * 2 <= n) p *= 2;
     return p;
 }
 
-extern "C" uint64_t mk_merkle_root_workspace_bytes(uint64_t n) {
+uint64_t merkle_root_ws(uint64_t n) {
     if (n == 0) return 0;
     const uint64_t P = pow2_floor(n);
     Plan p;
     uint64_t ws = 0;
-    if (P > 1 && make_plan(P, 32, true, ilog2(P), false, true, p, true) == MK_OK) ws = plan_ws_bytes(p);
+    if (P > 1 && mk::make_plan(P, 32, true, ilog2(P), false, true, p, true) == MK_OK) ws = mk::plan_ws_bytes(p);
     return 64 * n + align256(ws) + 256;
 }
 
-extern "C" int mk_dev_merkle_root(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len,
-                                  void* d_heap, uint64_t heap_bytes, void* d_leaves32, void* d_out32, void* stream) {
-    TRY(bind(-1));
+int dev_merkle_root(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len, void* d_heap,
+                    uint64_t heap_bytes, void* d_leaves32, void* d_out32, hipStream_t st) {
     if (n == 0) return fail(MK_EINVAL, "MerkleRoot of an empty list (reference: index out of range)");
     if (!d_heap || !d_out32 || (!d_offs && !d_data && fixed_len)) return fail(MK_EINVAL, "null pointer");
-    if (heap_bytes < mk_merkle_root_workspace_bytes(n)) return fail(MK_ENOMEM, "heap workspace too small");
-    hipStream_t st = (hipStream_t)stream;
+    if (heap_bytes < merkle_root_ws(n)) return fail(MK_ENOMEM, "heap workspace too small");
     uint8_t* heap = (uint8_t*)d_heap;  // node i at heap + 32 i (node 0 unused)
     uint4* leaves = (uint4*)(heap + 32 * n);
-    if (d_offs) {
-        hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, d_offs,
-                           n, leaves);
-    } else if (fixed_len == 64 && ((uintptr_t)d_data % 16) == 0) {
-        hipLaunchKernelGGL(mk::k_keccak64, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint4*)d_data, n, leaves);
-    } else if (fixed_len % 8 == 0 && ((uintptr_t)d_data % 8) == 0) {
-        hipLaunchKernelGGL(mk::k_keccak_words, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint2*)d_data, n,
-                           fixed_len / 8, leaves);
-    } else {
-        hipLaunchKernelGGL(mk::k_keccak_fixed, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, n,
-                           fixed_len, leaves);
-    }
-    HIPCHK(hipGetLastError());
+    TRY(dev_leaf_hashes(d_data, d_offs, n, fixed_len, leaves, st));
     if (d_leaves32 && d_leaves32 != (void*)leaves)
         HIPCHK(hipMemcpyAsync(d_leaves32, leaves, 32 * n, hipMemcpyDeviceToDevice, st));
     if (n == 1) {  // the loop body never runs: o[1] is the hashed value
@@ -1056,219 +638,1088 @@ extern "C" int mk_dev_merkle_root(const void* d_data, const uint64_t* d_offs, ui
         return MK_OK;
     }
     const uint64_t P = pow2_floor(n);
-    if (P < n)  // partial band [P, n): o[i] = Hash(o[2i] || o[2i+1]) over o[2P, 2n)
+    if (P < n) {  // partial band [P, n): o[i] = Hash(o[2i] || o[2i+1]) over o[2P, 2n)
         hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(n - P, 256)), dim3(256), 0, st,
                            (const uint4*)(heap + 64 * P), 2 * (n - P), (uint4*)(heap + 32 * P));
-    HIPCHK(hipGetLastError());
+        HIPCHK(hipGetLastError());
+    }
     Plan p;
-    TRY(make_plan(P, 32, true, ilog2(P), false, true, p, true));
+    TRY(mk::make_plan(P, 32, true, ilog2(P), false, true, p, true));
     uint8_t* ws = heap + 64 * n;
     return launch_plan(p, heap + 32 * P, (uint8_t*)d_out32, ws, heap_bytes - 64 * n, st);
 }
 
-extern "C" int mk_merkle_root(const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_t* leaves_out,
-                              uint8_t out[32]) {
-    if (!out || (n && !offs)) return fail(MK_EINVAL, "null pointer");
-    if (n == 0) return fail(MK_EINVAL, "MerkleRoot of an empty list (reference: index out of range)");
-    Locked L;
-    TRY(lock_current(L));
-    hipStream_t st = L.c->stream;
-    const size_t inb = offs[n] - offs[0];
-    bool uniform = true;
-    const uint64_t len0 = offs[1] - offs[0];
-    for (uint64_t i = 1; uniform && i < n; ++i) uniform = (offs[i + 1] - offs[i]) == len0;
-    uniform = uniform && len0 <= UINT32_MAX;
-    const uint64_t wsb = mk_merkle_root_workspace_bytes(n);
-    TRY(grow(L.c->in, inb + 16));
-    TRY(grow(L.c->aux, 8 * (n + 1)));
-    TRY(grow(L.c->ws, wsb));
-    TRY(grow(L.c->out, 32));
-    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, data + offs[0], inb, hipMemcpyHostToDevice, st));
-    if (!uniform) {
-        std::vector<uint64_t> rel(offs, offs + n + 1);
-        for (auto& o : rel) o -= offs[0];
-        HIPCHK(hipMemcpyAsync(L.c->aux.p, rel.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
-        TRY(mk_dev_merkle_root(L.c->in.p, (const uint64_t*)L.c->aux.p, n, 0, L.c->ws.p, wsb, nullptr, L.c->out.p,
-                               st));
-        HIPCHK(hipStreamSynchronize(st));  // rel is a stack vector
-    } else {
-        TRY(mk_dev_merkle_root(L.c->in.p, nullptr, n, (uint32_t)len0, L.c->ws.p, wsb, nullptr, L.c->out.p, st));
-    }
-    HIPCHK(hipMemcpyAsync(out, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
-    if (leaves_out) HIPCHK(hipMemcpyAsync(leaves_out, (uint8_t*)L.c->ws.p + 32 * n, 32 * n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+// ---- deposit trie -------------------------------------------------------------------
+uint4* trie_level(void* d_levels, uint64_t cap, uint32_t d) {
+    return (uint4*)d_levels + 2 * mk::trie_level_off(cap, d);
+}
+
+int check_trie(uint64_t cap, uint64_t count, uint64_t k, uint32_t depth) {
+    if (depth == 0 || depth > 63) return fail(MK_EINVAL, "depth %u out of range (1..63)", depth);
+    if (count + k > cap) return fail(MK_EINVAL, "trie capacity %llu < %llu deposits", (unsigned long long)cap,
+                                     (unsigned long long)(count + k));
+    if (count + k > (1ull << depth))
+        return fail(MK_EINVAL, "%llu deposits do not fit a depth-%u trie", (unsigned long long)(count + k), depth);
     return MK_OK;
 }
 
-// ---- deposit trie -------------------------------------------------------------------
-uint64_t mk_deposit_trie_levels_bytes(uint64_t n, uint32_t depth) {
-    if (n == 0) return 0;
-    uint64_t nodes = 0, c = n;
-    for (uint32_t d = 0; d <= depth; ++d) {
-        nodes += c;
-        c = (c + 1) / 2;
-    }
-    return 32 * nodes;
-}
-
-int mk_dev_deposit_trie_build(const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len,
-                              uint32_t depth, void* d_levels, void* d_root32, void* stream) {
-    TRY(bind(-1));
-    if (!d_root32 || (n && !d_levels) || (n && !d_offs && !d_data && fixed_len)) return fail(MK_EINVAL, "null pointer");
-    if (depth > 63) return fail(MK_EINVAL, "depth %u > 63", depth);
-    hipStream_t st = (hipStream_t)stream;
-    if (n == 0) {
-        HIPCHK(hipMemsetAsync(d_root32, 0, 32, st));
-        return MK_OK;
-    }
-    uint4* lv = (uint4*)d_levels;
-    if (d_offs) {
-        hipLaunchKernelGGL(mk::k_keccak_var, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, d_offs,
-                           n, lv);
-    } else if (kRecKernel && fixed_len == 280 && ((uintptr_t)d_data % 8) == 0) {  // deposit leaves
-        hipLaunchKernelGGL((mk::k_keccak_rec<35>),
-                           dim3(std::min<uint64_t>(ceil_div(n, mk::kRecThreads), mk::kRecGridMax)),
-                           dim3(mk::kRecThreads), 0, st, (const uint2*)d_data, n, lv);
-    } else if (fixed_len % 8 == 0 && ((uintptr_t)d_data % 8) == 0) {
-        hipLaunchKernelGGL(mk::k_keccak_words, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint2*)d_data, n,
-                           fixed_len / 8, lv);
-    } else {
-        hipLaunchKernelGGL(mk::k_keccak_fixed, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_data, n,
-                           fixed_len, lv);
-    }
-    HIPCHK(hipGetLastError());
-    // level d lives at lv + 2 * sum_{i<d} count_i (uint4 units).  Wide levels:
-    // one launch per level (every lane busy); the narrow top (<= 2^17 nodes)
-    // plus the zero-sibling tail: k_trie_top3 (bit-interleaved lane pairs),
-    // log2(NT) levels per workgroup of NT inputs, the last launch to the top.
+// Batch build of levels 1..depth over the `n` leaf hashes already in level 0.
+int trie_levels_build(void* d_levels, uint64_t cap, uint64_t n, uint32_t depth, void* d_root32, hipStream_t st) {
+    // Wide levels: one launch per level (every lane busy); the narrow top
+    // (<= 2^17 nodes) plus the zero-sibling tail: k_trie_top3 (bit-interleaved
+    // lane pairs), log2(NT) levels per workgroup of NT inputs, the last
+    // launch to the top.
     uint64_t c = n;
-    uint4* cur = lv;
     uint32_t d = 0;
-    const uint64_t top_max = kWave3 ? kNodeWaveMaxC1 : (1ull << 15);
-    while (d < depth && c > top_max) {
-        uint4* nxt = cur + 2 * c;
+    while (d < depth && c > kTrieTopMax) {
         const uint64_t cn = (c + 1) / 2;
-        hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(cn, 256)), dim3(256), 0, st, cur, c, nxt);
+        hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(cn, 256)), dim3(256), 0, st,
+                           (const uint4*)trie_level(d_levels, cap, d), c, trie_level(d_levels, cap, d + 1));
         HIPCHK(hipGetLastError());
-        cur = nxt;
         c = cn;
         ++d;
     }
     while (d < depth) {
-        uint32_t k = 0, nt = 0;
-        uint64_t nwg = 0;
-        if (kWave3) {
-            nt = mk::kWaveThreads;
-            while (nt < mk::kMidThreads && ceil_div(c, nt) > kNodeWaveWgs) nt *= 2;
-            if (kTopOneWg)  // the last <= 1024 nodes in one workgroup
-                while (nt < mk::kMidThreads && c <= mk::kMidThreads && c > nt) nt *= 2;
-            nwg = ceil_div(c, nt);
-            k = nwg == 1 ? depth - d : std::min<uint32_t>(ilog2(nt), depth - d);
-        } else {
-            nwg = ceil_div(c, 2 * mk::kWave2Span);
-            uint64_t cc = c;
-            if (nwg == 1) {
-                k = depth - d;
-            } else {
-                while (k < mk::kWave2Levels && cc > 1) {
-                    cc = (cc + 1) / 2;
-                    ++k;
-                }
-            }
-        }
-        const uint32_t* src = (const uint32_t*)cur;
-        uint32_t* dst = (uint32_t*)(cur + 2 * c);
+        uint32_t nt = mk::kWaveThreads;
+        while (nt < mk::kMidThreads && ceil_div(c, nt) > kTrieTopWgs) nt *= 2;
+        while (nt < mk::kMidThreads && c <= mk::kMidThreads && c > nt) nt *= 2;  // the last <= 1024 nodes in one WG
+        const uint64_t nwg = ceil_div(c, nt);
+        const uint32_t k = nwg == 1 ? depth - d : std::min<uint32_t>(ilog2(nt), depth - d);
+        const uint32_t* src = (const uint32_t*)trie_level(d_levels, cap, d);
+        uint32_t* dst = (uint32_t*)trie_level(d_levels, cap, d + 1);
+        const uint64_t capn = mk::trie_count(cap, d + 1);
         switch (nt) {
-            case 0: hipLaunchKernelGGL(mk::k_trie_top2, dim3(nwg), dim3(mk::kWaveThreads), 0, st, src, c, dst, k); break;
-            case 64: hipLaunchKernelGGL(mk::k_trie_top3<64>, dim3(nwg), dim3(64), 0, st, src, c, dst, k); break;
-            case 128: hipLaunchKernelGGL(mk::k_trie_top3<128>, dim3(nwg), dim3(128), 0, st, src, c, dst, k); break;
-            case 256: hipLaunchKernelGGL(mk::k_trie_top3<256>, dim3(nwg), dim3(256), 0, st, src, c, dst, k); break;
-            case 512: hipLaunchKernelGGL(mk::k_trie_top3<512>, dim3(nwg), dim3(512), 0, st, src, c, dst, k); break;
-            default: hipLaunchKernelGGL(mk::k_trie_top3<1024>, dim3(nwg), dim3(1024), 0, st, src, c, dst, k); break;
+            case 64: hipLaunchKernelGGL(mk::k_trie_top3<64>, dim3(nwg), dim3(64), 0, st, src, c, dst, k, capn); break;
+            case 128: hipLaunchKernelGGL(mk::k_trie_top3<128>, dim3(nwg), dim3(128), 0, st, src, c, dst, k, capn); break;
+            case 256: hipLaunchKernelGGL(mk::k_trie_top3<256>, dim3(nwg), dim3(256), 0, st, src, c, dst, k, capn); break;
+            case 512: hipLaunchKernelGGL(mk::k_trie_top3<512>, dim3(nwg), dim3(512), 0, st, src, c, dst, k, capn); break;
+            default: hipLaunchKernelGGL(mk::k_trie_top3<1024>, dim3(nwg), dim3(1024), 0, st, src, c, dst, k, capn); break;
         }
         HIPCHK(hipGetLastError());
-        for (uint32_t i = 0; i < k; ++i) {
-            cur += 2 * c;
-            c = (c + 1) / 2;
-        }
+        for (uint32_t i = 0; i < k; ++i) c = (c + 1) / 2;
         d += k;
     }
-    uint4* root_node = cur;
-    HIPCHK(hipMemcpyAsync(d_root32, root_node, 32, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(d_root32, trie_level(d_levels, cap, depth), 32, hipMemcpyDeviceToDevice, st));
     return MK_OK;
 }
 
-int mk_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
-                          uint8_t* levels_out, uint8_t root[32]) {
-    if (!root || (n && !offs)) return fail(MK_EINVAL, "null pointer");
-    if (depth > 63) return fail(MK_EINVAL, "depth %u > 63", depth);
-    Locked L;
-    TRY(lock_current(L));
-    if (n == 0) {
-        std::memset(root, 0, 32);
+int dev_trie_append(void* d_levels, uint64_t cap, uint64_t count, const void* d_data, const uint64_t* d_offs,
+                    uint64_t k, uint32_t fixed_len, uint32_t depth, void* d_root32, hipStream_t st) {
+    TRY(check_trie(cap, count, k, depth));
+    if (!d_root32 || (cap && !d_levels)) return fail(MK_EINVAL, "null pointer");
+    if (k && !d_offs && !d_data && fixed_len) return fail(MK_EINVAL, "null deposits");
+    if (count + k == 0) {
+        HIPCHK(hipMemsetAsync(d_root32, 0, 32, st));
         return MK_OK;
     }
-    hipStream_t st = L.c->stream;
-    const size_t inb = offs[n];
-    const uint64_t lv_bytes = mk_deposit_trie_levels_bytes(n, depth);
-    TRY(grow(L.c->in, inb));
-    TRY(grow(L.c->aux, 8 * (n + 1)));
-    TRY(grow(L.c->ws, lv_bytes));
-    TRY(grow(L.c->out, 32));
-    bool uniform = offs[0] == 0;
-    const uint64_t len0 = offs[1] - offs[0];
-    for (uint64_t i = 1; uniform && i < n; ++i) uniform = (offs[i + 1] - offs[i]) == len0;
-    uniform = uniform && len0 <= UINT32_MAX;
-    if (inb) HIPCHK(hipMemcpyAsync(L.c->in.p, data, inb, hipMemcpyHostToDevice, st));
-    if (!uniform) HIPCHK(hipMemcpyAsync(L.c->aux.p, offs, 8 * (n + 1), hipMemcpyHostToDevice, st));
-    TRY(mk_dev_deposit_trie_build(L.c->in.p, uniform ? nullptr : (const uint64_t*)L.c->aux.p, n,
-                                  uniform ? (uint32_t)len0 : 0, depth, L.c->ws.p, L.c->out.p, st));
-    HIPCHK(hipMemcpyAsync(root, L.c->out.p, 32, hipMemcpyDeviceToHost, st));
-    if (levels_out) HIPCHK(hipMemcpyAsync(levels_out, L.c->ws.p, lv_bytes, hipMemcpyDeviceToHost, st));
+    // leaf hashes of the new deposits: Hash(depositData) (deposit_trie.go:32)
+    TRY(dev_leaf_hashes(d_data, d_offs, k, fixed_len, trie_level(d_levels, cap, 0) + 2 * count, st));
+    if (count == 0) return trie_levels_build(d_levels, cap, k, depth, d_root32, st);
+    // right edge only: level d changes on [lo, c)
+    uint64_t lo = count, c = count + k;
+    uint32_t d = 0;
+    while (d < depth && c - lo > kAppendMaxRange) {
+        const uint64_t plo = lo >> 1;
+        hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(((c + 1) >> 1) - plo, 256)), dim3(256), 0, st,
+                           (const uint4*)(trie_level(d_levels, cap, d) + 2 * (2 * plo)), c - 2 * plo,
+                           trie_level(d_levels, cap, d + 1) + 2 * plo);
+        HIPCHK(hipGetLastError());
+        lo = plo;
+        c = (c + 1) >> 1;
+        ++d;
+    }
+    if (d == depth) {
+        HIPCHK(hipMemcpyAsync(d_root32, trie_level(d_levels, cap, depth), 32, hipMemcpyDeviceToDevice, st));
+        return MK_OK;
+    }
+    const uint64_t r = c - lo;
+    uint32_t* lv = (uint32_t*)d_levels;
+    if (r <= 60)
+        hipLaunchKernelGGL(mk::k_trie_append<64>, dim3(1), dim3(64), 0, st, lv, cap, d, lo, c, depth,
+                           (uint32_t*)d_root32);
+    else if (r <= 252)
+        hipLaunchKernelGGL(mk::k_trie_append<256>, dim3(1), dim3(256), 0, st, lv, cap, d, lo, c, depth,
+                           (uint32_t*)d_root32);
+    else
+        hipLaunchKernelGGL(mk::k_trie_append<1024>, dim3(1), dim3(1024), 0, st, lv, cap, d, lo, c, depth,
+                           (uint32_t*)d_root32);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
+int dev_trie_branch(const void* d_levels, uint64_t cap, uint64_t count, uint32_t depth, uint64_t index,
+                    void* d_branch, hipStream_t st) {
+    if (depth == 0 || depth > 63) return fail(MK_EINVAL, "depth %u out of range (1..63)", depth);
+    if (!d_branch || (count && !d_levels)) return fail(MK_EINVAL, "null pointer");
+    if (count > cap) return fail(MK_EINVAL, "count > capacity");
+    hipLaunchKernelGGL(mk::k_trie_branch, dim3(1), dim3(64), 0, st, (const uint4*)d_levels, cap, count, depth, index,
+                       (uint4*)d_branch);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
+// ---- multi-device ------------------------------------------------------------------------
+std::mutex g_multi_mu;  // one multi-device call at a time (device locks are taken per device)
+std::map<std::vector<int>, std::vector<ncclComm_t>> g_comms;
+
+int comms_for(const std::vector<int>& devs, std::vector<ncclComm_t>*& out) {
+    auto it = g_comms.find(devs);
+    if (it == g_comms.end()) {
+        std::vector<ncclComm_t> comms(devs.size(), nullptr);
+        if (ncclCommInitAll(comms.data(), (int)devs.size(), devs.data()) != ncclSuccess)
+            return fail(MK_ECOMM, "ncclCommInitAll(%zu) failed", devs.size());
+        it = g_comms.emplace(devs, std::move(comms)).first;
+    }
+    out = &it->second;
+    return MK_OK;
+}
+
+// Shard s of the frontier sharding reduced on the bound device: nodes of
+// level (h - k) into d_block (k = 0: the 32-B shard root).
+int launch_shard(const uint8_t* d_items, uint64_t sn, uint32_t item_len, uint32_t h, uint32_t k, uint8_t* d_block,
+                 DevBuf& ws, hipStream_t st, bool grow_ws) {
+    if (sn == 0) {
+        HIPCHK(hipMemsetAsync(d_block, 0, (size_t)32 << k, st));
+        return MK_OK;
+    }
+    Plan p;
+    TRY(mk::make_plan(sn, item_len, true, h, true, ((uintptr_t)d_items % 16) == 0, p, false, k));
+    if (grow_ws) TRY(grow(ws, mk::plan_ws_bytes(p)));
+    return launch_plan(p, d_items, d_block, (uint8_t*)ws.p, ws.cap, st);
+}
+
+uint32_t multi_frontier(uint32_t h) { return h > 5 ? std::min<uint32_t>(10, h - 5) : 0; }
+
+// Uploads items[0, bytes) into d_dst through the device's two pinned staging
+// slots (host memcpy into slot i while slot i^1 crosses PCIe) on `copy`.
+int staged_upload(DevCtx* c, uint8_t* d_dst, const uint8_t* src, size_t bytes) {
+    for (int i = 0; i < 2; ++i)
+        if (!c->stage[i] && hipHostMalloc(&c->stage[i], kStageBytes, hipHostMallocDefault) != hipSuccess) {
+            c->stage[i] = nullptr;
+            return fail(MK_ENOMEM, "hipHostMalloc(%zu) failed", kStageBytes);
+        }
+    int slot = 0;
+    for (size_t off = 0; off < bytes; off += kStageBytes) {
+        const size_t len = std::min(kStageBytes, bytes - off);
+        if (c->stage_used[slot]) HIPCHK(hipEventSynchronize(c->stage_ev[slot]));
+        std::memcpy(c->stage[slot], src + off, len);
+        HIPCHK(hipMemcpyAsync(d_dst + off, c->stage[slot], len, hipMemcpyHostToDevice, c->copy));
+        HIPCHK(hipEventRecord(c->stage_ev[slot], c->copy));
+        c->stage_used[slot] = true;
+        slot ^= 1;
+    }
+    return MK_OK;
+}
+
+struct MultiJob {
+    int dev;
+    std::vector<uint32_t> shards;  // shard indices on this device, in order
+};
+
+// Worker of mk_ssz_merkle_hash_multi for one device: its shards are uploaded
+// into two alternating regions on the copy stream; each shard's passes run on
+// the compute stream once its upload landed, while the next shard uploads.
+int multi_device_worker(const MultiJob& job, const uint8_t* items, const std::vector<uint64_t>& begin,
+                        uint32_t item_len, uint32_t h, uint32_t k, size_t block) {
+    TRY(bind_dev(job.dev));
+    DevCtx* c = ctx();
+    const size_t region = (size_t)((1ull << h) * mk::chunk_bytes(item_len));
+    const int nreg = job.shards.size() > 1 ? 2 : 1;
+    TRY(grow(c->in, region * nreg));
+    TRY(grow(c->out, block * (begin.size() - 1) + 32));
+    Plan p;
+    uint64_t wsb = 256;
+    for (uint32_t s : job.shards) {
+        const uint64_t sn = begin[s + 1] - begin[s];
+        if (sn && mk::make_plan(sn, item_len, true, h, true, true, p, false, k) == MK_OK)
+            wsb = std::max(wsb, mk::plan_ws_bytes(p));
+    }
+    TRY(grow(c->ws, wsb));
+    c->region_used[0] = c->region_used[1] = false;
+    for (size_t i = 0; i < job.shards.size(); ++i) {
+        const uint32_t s = job.shards[i];
+        const int r = (int)(i % 2);
+        uint8_t* dreg = (uint8_t*)c->in.p + region * r;
+        const uint64_t sn = begin[s + 1] - begin[s];
+        if (c->region_used[r]) HIPCHK(hipStreamWaitEvent(c->copy, c->region_ev[r], 0));  // its last shard is done
+        TRY(staged_upload(c, dreg, items + begin[s] * item_len, sn * (size_t)item_len));
+        HIPCHK(hipEventRecord(c->h2d, c->copy));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->h2d, 0));
+        TRY(launch_shard(dreg, sn, item_len, h, k, (uint8_t*)c->out.p + block * s, c->ws, c->stream, false));
+        HIPCHK(hipEventRecord(c->region_ev[r], c->stream));
+        c->region_used[r] = true;
+    }
+    return MK_OK;
+}
+
+int host_merkle_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int nshards, const int* devs_in,
+                      uint8_t* out) {
+    if (nshards <= 0) return fail(MK_EINVAL, "nshards %d <= 0", nshards);
+    if (!out || (n && item_len && !items)) return fail(MK_EINVAL, "null pointer");
+    const int nvis = probe_devices();
+    if (nvis <= 0) return fail(MK_ENODEV, "no gfx950 device visible");
+    std::vector<int> devs(nshards);
+    for (int s = 0; s < nshards; ++s) {
+        devs[s] = devs_in ? devs_in[s] : s;
+        if (devs[s] < 0 || devs[s] >= nvis)
+            return fail(MK_ENODEV, "shard %d: device %d out of range (%d visible)", s, devs[s], nvis);
+    }
+    uint32_t h = 0, ne = 0;
+    std::vector<uint64_t> begin(nshards + 1);
+    TRY(mk::shard_plan(n, item_len, (uint32_t)nshards, &h, &ne, begin.data()));
+    if (ne <= 1) {  // too small to shard: one device
+        mk_call local{};
+        local.device = devs[0];
+        mk_call* prev = mk::swap_call(&local);
+        const int rc = host_merkle_hash(items, n, item_len, out);
+        mk::swap_call(prev);
+        return rc ? fail(rc, "%s", local.err) : MK_OK;
+    }
+    std::lock_guard<std::mutex> mlk(g_multi_mu);
+    std::vector<int> uniq;
+    for (int d : devs)
+        if (std::find(uniq.begin(), uniq.end(), d) == uniq.end()) uniq.push_back(d);
+    const bool one_each = (int)uniq.size() == nshards;
+    const uint32_t k = multi_frontier(h);
+    const size_t block = (size_t)32 << k;
+    std::vector<MultiJob> jobs;
+    for (int d : uniq) {
+        MultiJob j{d, {}};
+        for (int s = 0; s < nshards; ++s)
+            if (devs[s] == d && begin[s + 1] > begin[s]) j.shards.push_back((uint32_t)s);
+        jobs.push_back(j);
+    }
+    std::vector<std::unique_lock<std::mutex>> locks;
+    for (int d : uniq) {
+        TRY(bind_dev(d));
+        locks.emplace_back(g_ctx[d]->mu);
+    }
+    // one host thread per device: uploads through pinned staging + the shard passes
+    std::vector<int> rcs(jobs.size(), MK_OK);
+    std::vector<std::string> errs(jobs.size());
+    std::vector<std::thread> th;
+    mk_call* parent = mk::current_call();
+    for (size_t j = 0; j < jobs.size(); ++j)
+        th.emplace_back([&, j]() {
+            mk_call local{};
+            local.device = jobs[j].dev;
+            mk::swap_call(&local);
+            rcs[j] = multi_device_worker(jobs[j], items, begin, item_len, h, k, block);
+            if (rcs[j] == MK_OK && !one_each && hipStreamSynchronize(g_ctx[jobs[j].dev]->stream) != hipSuccess)
+                rcs[j] = fail(MK_EHIP, "hipStreamSynchronize failed on device %d", jobs[j].dev);
+            errs[j] = local.err;
+            mk::swap_call(nullptr);
+        });
+    for (auto& t : th) t.join();
+    for (size_t j = 0; j < jobs.size(); ++j)
+        if (rcs[j] != MK_OK) {
+            mk::swap_call(parent);
+            return fail(rcs[j], "device %d: %s", jobs[j].dev, errs[j].c_str());
+        }
+    DevCtx* c0 = g_ctx[devs[0]];
+    uint8_t* lvl0 = (uint8_t*)c0->out.p;
+    if (one_each) {  // gather the frontier blocks over RCCL (in place: block s of every device)
+        std::vector<ncclComm_t>* comms = nullptr;
+        TRY(comms_for(devs, comms));
+        // (blocks of empty shards are never read: they follow the non-empty ones)
+        if (ncclGroupStart() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupStart");
+        for (int s = 0; s < nshards; ++s) {
+            uint8_t* lvl = (uint8_t*)g_ctx[devs[s]]->out.p;
+            if (ncclAllGather(lvl + block * s, lvl, block, ncclUint8, (*comms)[s], g_ctx[devs[s]]->stream) !=
+                ncclSuccess) {
+                ncclGroupEnd();
+                return fail(MK_ECOMM, "ncclAllGather on device %d", devs[s]);
+            }
+        }
+        if (ncclGroupEnd() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupEnd");
+    } else {  // several shards per device: copy the other devices' blocks to devs[0]
+        TRY(bind_dev(devs[0]));
+        for (uint32_t s = 0; s < ne; ++s)  // (blocks of the trailing empty shards are never read)
+            if (devs[s] != devs[0])
+                HIPCHK(hipMemcpyPeerAsync(lvl0 + block * s, devs[0], (uint8_t*)g_ctx[devs[s]]->out.p + block * s,
+                                          devs[s], block, c0->stream));
+    }
+    TRY(bind_dev(devs[0]));
+    const uint64_t last_nodes = k ? mk::frontier_nodes(begin[ne] - begin[ne - 1], item_len, h, k) : 1;
+    const uint64_t count = ((uint64_t)(ne - 1) << k) + last_nodes;
+    uint8_t* root = lvl0 + block * nshards;
+    if (k) {
+        TRY(grow(c0->aux, finish_ws_bytes(count)));
+        TRY(dev_finish_nodes(lvl0, count, n, root, c0->aux.p, c0->aux.cap, c0->stream));
+    } else {
+        TRY(dev_finish(lvl0, ne, n, root, c0->stream));
+    }
+    HIPCHK(hipMemcpyAsync(out, root, 32, hipMemcpyDeviceToHost, c0->stream));
+    for (int d : uniq) {
+        TRY(bind_dev(d));
+        HIPCHK(hipStreamSynchronize(g_ctx[d]->stream));
+    }
+    return MK_OK;
+}
+
+int dev_merkle_multi(const void* const* d_shards, uint64_t n, uint32_t item_len, int ndev, void* d_out32,
+                     void* const* streams) {
+    if (ndev <= 0 || !d_shards || !d_out32) return fail(MK_EINVAL, "bad arguments");
+    if (probe_devices() < ndev) return fail(MK_ENODEV, "%d devices requested, %d visible", ndev, g_ndev);
+    uint32_t h = 0, ne = 0;
+    std::vector<uint64_t> begin(ndev + 1);
+    TRY(mk::shard_plan(n, item_len, (uint32_t)ndev, &h, &ne, begin.data()));
+    auto stream_of = [&](int d) { return streams && streams[d] ? (hipStream_t)streams[d] : g_ctx[d]->stream; };
+    if (ne <= 1) {
+        TRY(bind_dev(0));
+        DevCtx* c = ctx();
+        Plan p;
+        TRY(mk::make_plan(n, item_len, false, 0, false, ((uintptr_t)d_shards[0] % 16) == 0, p));
+        TRY(grow(c->ws, p.small ? 256 : mk::plan_ws_bytes(p)));
+        return launch_plan(p, (const uint8_t*)d_shards[0], (uint8_t*)d_out32, (uint8_t*)c->ws.p, c->ws.cap,
+                           stream_of(0));
+    }
+    std::lock_guard<std::mutex> mlk(g_multi_mu);
+    const uint32_t k = multi_frontier(h);
+    const size_t block = (size_t)32 << k;
+    std::vector<int> devs(ndev);
+    for (int d = 0; d < ndev; ++d) devs[d] = d;
+    for (int d = 0; d < ndev; ++d) {  // every device: its shard to the frontier level, block d
+        TRY(bind_dev(d));
+        DevCtx* c = ctx();
+        TRY(grow(c->out, block * ndev + 32));
+        TRY(launch_shard((const uint8_t*)d_shards[d], begin[d + 1] - begin[d], item_len, h, k,
+                         (uint8_t*)c->out.p + block * d, c->ws, stream_of(d), true));
+    }
+    std::vector<ncclComm_t>* comms = nullptr;
+    TRY(comms_for(devs, comms));
+    if (ncclGroupStart() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupStart");
+    for (int d = 0; d < ndev; ++d) {
+        uint8_t* lvl = (uint8_t*)g_ctx[d]->out.p;
+        if (ncclAllGather(lvl + block * d, lvl, block, ncclUint8, (*comms)[d], stream_of(d)) != ncclSuccess) {
+            ncclGroupEnd();
+            return fail(MK_ECOMM, "ncclAllGather on device %d", d);
+        }
+    }
+    if (ncclGroupEnd() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupEnd");
+    TRY(bind_dev(0));
+    DevCtx* c0 = ctx();
+    const uint64_t last_nodes = k ? mk::frontier_nodes(begin[ne] - begin[ne - 1], item_len, h, k) : 1;
+    const uint64_t count = ((uint64_t)(ne - 1) << k) + last_nodes;
+    if (k) {
+        TRY(grow(c0->aux, finish_ws_bytes(count)));
+        return dev_finish_nodes(c0->out.p, count, n, d_out32, c0->aux.p, c0->aux.cap, stream_of(0));
+    }
+    return dev_finish(c0->out.p, ne, n, d_out32, stream_of(0));
+}
+
+}  // namespace
+
+// ---- deposit trie handle -----------------------------------------------------------------
+struct mk_trie {
+    std::mutex mu;
+    int dev = 0;
+    uint32_t depth = 32;
+    uint64_t cap = 0, count = 0;
+    DevBuf levels, root, in, offs, branch;
+};
+
+// =============================================================================
+extern "C" {
+
+const char* mk_version(void) { return "prysm_merkle 0.2 (gfx950)"; }
+
+const char* mk_strerror(int code) {
+    switch (code) {
+        case MK_OK: return "ok";
+        case MK_EINVAL: return "invalid argument";
+        case MK_ENODEV: return "no usable gfx950 device";
+        case MK_ENOMEM: return "out of memory";
+        case MK_EHIP: return "HIP runtime error";
+        case MK_ECOMM: return "RCCL error";
+        default: return "unknown error";
+    }
+}
+
+const char* mk_last_error(void) { return mk::last_error(); }
+
+int mk_device_count(void) { return probe_devices(); }
+
+int mk_init(int device) {
+    Scope S(nullptr);
+    return S.done(bind_dev(device < 0 ? 0 : device));
+}
+
+// ---- hashing ------------------------------------------------------------------
+int mk_dev_hash_batch(mk_call* call, const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    return S.done(rc ? rc : dev_hash_batch(d_in, n, msg_len, d_out, (hipStream_t)stream));
+}
+
+int mk_dev_hash_batch_var(mk_call* call, const void* d_in, const uint64_t* d_offs, uint64_t n, void* d_out,
+                          void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    return S.done(rc ? rc : dev_hash_var(d_in, d_offs, n, d_out, (hipStream_t)stream));
+}
+
+static int host_hash_batch(const uint8_t* in, uint64_t n, uint32_t msg_len, uint8_t* out) {
+    if (n && !in && msg_len) return fail(MK_EINVAL, "null input");
+    if (n && !out) return fail(MK_EINVAL, "null output");
+    TRY(bind_call());
+    if (n == 0) return MK_OK;
+    DevCtx* c = ctx();
+    std::lock_guard<std::mutex> lk(c->mu);
+    const size_t inb = n * (size_t)msg_len;
+    TRY(grow(c->in, inb));
+    TRY(grow(c->out, 32 * n));
+    hipStream_t st = c->stream;
+    if (inb) HIPCHK(hipMemcpyAsync(c->in.p, in, inb, hipMemcpyHostToDevice, st));
+    TRY(dev_hash_batch(c->in.p, n, msg_len, c->out.p, st));
+    HIPCHK(hipMemcpyAsync(out, c->out.p, 32 * n, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return MK_OK;
 }
 
-int mk_verify_merkle_branches(const uint8_t* leaves, const uint8_t* branches, const uint64_t* indices, uint64_t n,
-                              uint32_t depth, uint32_t tree_depth, const uint8_t* roots, uint8_t* ok) {
-    if (n && (!leaves || !indices || !roots || !ok || (depth && !branches))) return fail(MK_EINVAL, "null pointer");
-    Locked L;
-    TRY(lock_current(L));
+static int host_hash_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint8_t* out) {
+    if (n && (!offs || !out)) return fail(MK_EINVAL, "null pointer");
+    TRY(bind_call());
     if (n == 0) return MK_OK;
-    hipStream_t st = L.c->stream;
+    DevCtx* c = ctx();
+    std::lock_guard<std::mutex> lk(c->mu);
+    const size_t inb = offs[n] - offs[0];
+    TRY(grow(c->in, inb));
+    TRY(grow(c->aux, 8 * (n + 1)));
+    TRY(grow(c->out, 32 * n));
+    hipStream_t st = c->stream;
+    std::vector<uint64_t> rel(offs, offs + n + 1);
+    for (auto& o : rel) o -= offs[0];
+    if (inb) HIPCHK(hipMemcpyAsync(c->in.p, in + offs[0], inb, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->aux.p, rel.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
+    TRY(dev_hash_var(c->in.p, (const uint64_t*)c->aux.p, n, c->out.p, st));
+    HIPCHK(hipMemcpyAsync(out, c->out.p, 32 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+int mk_hash_batch(mk_call* call, const uint8_t* in, uint64_t n, uint32_t msg_len, uint8_t* out) {
+    Scope S(call);
+    return S.done(host_hash_batch(in, n, msg_len, out));
+}
+
+int mk_hash_batch_var(mk_call* call, const uint8_t* in, const uint64_t* offs, uint64_t n, uint8_t* out) {
+    Scope S(call);
+    return S.done(host_hash_var(in, offs, n, out));
+}
+
+int mk_hash(mk_call* call, const uint8_t* data, uint64_t len, uint8_t out[32]) {
+    Scope S(call);
+    if (len && !data) return S.done(fail(MK_EINVAL, "null input"));
+    if (len > UINT32_MAX) {
+        uint64_t offs[2] = {0, len};
+        return S.done(host_hash_var(data, offs, 1, out));
+    }
+    static const uint8_t empty = 0;
+    return S.done(host_hash_batch(len ? data : &empty, 1, (uint32_t)len, out));
+}
+
+// ---- merkleHash ---------------------------------------------------------------
+uint64_t mk_ssz_merkle_workspace_bytes(uint64_t n, uint32_t item_len) {
+    Scope S(nullptr, false);
+    Plan p;
+    if (mk::make_plan(n, item_len, false, 0, false, true, p) != MK_OK) return 0;
+    return p.small ? 256 : mk::plan_ws_bytes(p);
+}
+
+int mk_dev_ssz_merkle_hash(mk_call* call, const void* d_items, uint64_t n, uint32_t item_len, void* d_out32,
+                           void* d_ws, uint64_t ws_bytes, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    return S.done(rc ? rc : dev_merkle_hash(d_items, n, item_len, d_out32, d_ws, ws_bytes, (hipStream_t)stream));
+}
+
+int mk_ssz_merkle_hash(mk_call* call, const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t out[32]) {
+    Scope S(call);
+    return S.done(host_merkle_hash(items, n, item_len, out));
+}
+
+uint64_t mk_ssz_merkle_many_workspace_bytes(const uint64_t* n, const uint32_t* item_len, uint32_t nlists) {
+    Scope S(nullptr, false);
+    mk::ManyPlan mp;
+    std::vector<uint64_t> offs(nlists, 0);  // the layout does not depend on the offsets
+    if (mk::make_many_plan(offs.data(), n, item_len, nlists, UINT64_MAX, true, mp) != MK_OK) return 0;
+    return mp.ws_bytes;
+}
+
+int mk_dev_ssz_merkle_many(mk_call* call, const void* d_items, const uint64_t* offs, const uint64_t* n,
+                           const uint32_t* item_len, uint32_t nlists, void* d_roots, void* d_ws, uint64_t ws_bytes,
+                           void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    if (nlists && !offs) return S.done(fail(MK_EINVAL, "null offsets"));
+    mk::ManyPlan mp;
+    rc = mk::make_many_plan(offs, n, item_len, nlists, UINT64_MAX, ((uintptr_t)d_items % 16) == 0, mp);
+    if (rc) return S.done(rc);
+    return S.done(dev_merkle_many(d_items, mp, nlists, d_roots, d_ws, ws_bytes, (hipStream_t)stream));
+}
+
+static int host_merkle_many(const uint8_t* items, const uint64_t* offs, const uint64_t* n, const uint32_t* item_len,
+                            uint32_t nlists, uint8_t* roots) {
+    if (nlists == 0) return MK_OK;
+    if (!offs || !n || !item_len || !roots) return fail(MK_EINVAL, "null pointer");
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint32_t i = 0; i < nlists; ++i) {
+        const uint64_t b = n[i] * (uint64_t)item_len[i];
+        if (b) {
+            lo = std::min(lo, offs[i]);
+            hi = std::max(hi, offs[i] + b);
+        }
+    }
+    if (lo == UINT64_MAX) lo = hi = 0;
+    if (hi > lo && !items) return fail(MK_EINVAL, "null items");
+    // upload [lo, hi) of the caller's buffer; offsets shift by lo (rounded down to 16 keeps alignment)
+    lo &= ~15ull;
+    std::vector<uint64_t> rel(offs, offs + nlists);
+    for (uint32_t i = 0; i < nlists; ++i) rel[i] = n[i] * (uint64_t)item_len[i] ? offs[i] - lo : 0;
+    mk::ManyPlan mp;
+    TRY(mk::make_many_plan(rel.data(), n, item_len, nlists, hi - lo, ((uintptr_t)(items + lo) % 16) == 0, mp));
+    TRY(bind_call());
+    DevCtx* c = ctx();
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t st = c->stream;
+    TRY(grow(c->in, hi - lo));
+    TRY(grow(c->ws, mp.ws_bytes));
+    TRY(grow(c->out, 32 * (size_t)nlists));
+    if (hi > lo) HIPCHK(hipMemcpyAsync(c->in.p, items + lo, hi - lo, hipMemcpyHostToDevice, st));
+    TRY(dev_merkle_many(c->in.p, mp, nlists, c->out.p, c->ws.p, c->ws.cap, st));
+    HIPCHK(hipMemcpyAsync(roots, c->out.p, 32 * (size_t)nlists, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+int mk_ssz_merkle_many(mk_call* call, const uint8_t* items, const uint64_t* offs, const uint64_t* n,
+                       const uint32_t* item_len, uint32_t nlists, uint8_t* roots) {
+    Scope S(call);
+    return S.done(host_merkle_many(items, offs, n, item_len, nlists, roots));
+}
+
+// ---- sharding -------------------------------------------------------------------
+int mk_ssz_merkle_shard_plan(mk_call* call, uint64_t n, uint32_t item_len, uint32_t nshards, uint32_t* height,
+                             uint32_t* nonempty, uint64_t* item_begin) {
+    Scope S(call, false);
+    if (!height || !nonempty || !item_begin) return S.done(fail(MK_EINVAL, "null pointer"));
+    return S.done(mk::shard_plan(n, item_len, nshards, height, nonempty, item_begin));
+}
+
+int mk_dev_ssz_merkle_subtree(mk_call* call, const void* d_shard_items, uint64_t shard_n, uint32_t item_len,
+                              uint32_t height, int pad_at_one, void* d_out32, void* d_ws, uint64_t ws_bytes,
+                              void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    if (!d_out32 || (shard_n && !d_shard_items)) return S.done(fail(MK_EINVAL, "null pointer"));
+    Plan p;
+    rc = mk::make_plan(shard_n, item_len, true, height, pad_at_one != 0, ((uintptr_t)d_shard_items % 16) == 0, p);
+    if (rc) return S.done(rc);
+    return S.done(launch_plan(p, (const uint8_t*)d_shard_items, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes,
+                              (hipStream_t)stream));
+}
+
+int mk_dev_ssz_merkle_subtree_frontier(mk_call* call, const void* d_shard_items, uint64_t shard_n,
+                                       uint32_t item_len, uint32_t height, uint32_t frontier_log2, int pad_at_one,
+                                       void* d_out, uint64_t* nodes_out, void* d_ws, uint64_t ws_bytes,
+                                       void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    if (!d_out || (shard_n && !d_shard_items)) return S.done(fail(MK_EINVAL, "null pointer"));
+    Plan p;
+    rc = mk::make_plan(shard_n, item_len, true, height, pad_at_one != 0, ((uintptr_t)d_shard_items % 16) == 0, p,
+                       false, frontier_log2);
+    if (rc) return S.done(rc);
+    if (nodes_out) *nodes_out = p.out_nodes;
+    return S.done(launch_plan(p, (const uint8_t*)d_shard_items, (uint8_t*)d_out, (uint8_t*)d_ws, ws_bytes,
+                              (hipStream_t)stream));
+}
+
+uint64_t mk_ssz_merkle_node_frontier_workspace_bytes(uint64_t count, uint32_t height, uint32_t frontier_log2) {
+    Scope S(nullptr, false);
+    Plan p;
+    if (mk::make_plan(count, 32, true, height, true, true, p, true, frontier_log2) != MK_OK) return 0;
+    return std::max<uint64_t>(256, mk::plan_ws_bytes(p));
+}
+
+int mk_dev_ssz_merkle_node_frontier(mk_call* call, const void* d_nodes, uint64_t count, uint32_t height,
+                                    uint32_t frontier_log2, int pad_at_one, void* d_out, uint64_t* nodes_out,
+                                    void* d_ws, uint64_t ws_bytes, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    if (!d_out || !d_nodes || count == 0) return S.done(fail(MK_EINVAL, "null pointer or empty level"));
+    Plan p;
+    rc = mk::make_plan(count, 32, true, height, pad_at_one != 0, ((uintptr_t)d_nodes % 16) == 0, p, true,
+                       frontier_log2);
+    if (rc) return S.done(rc);
+    if (nodes_out) *nodes_out = frontier_log2 ? p.out_nodes : 1;
+    return S.done(launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out, (uint8_t*)d_ws, ws_bytes,
+                              (hipStream_t)stream));
+}
+
+uint64_t mk_ssz_merkle_finish_workspace_bytes(uint64_t count) {
+    Scope S(nullptr, false);
+    return finish_ws_bytes(count);
+}
+
+int mk_dev_ssz_merkle_finish_nodes(mk_call* call, const void* d_nodes, uint64_t count, uint64_t n_total,
+                                   void* d_out32, void* d_ws, uint64_t ws_bytes, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    return S.done(rc ? rc : dev_finish_nodes(d_nodes, count, n_total, d_out32, d_ws, ws_bytes, (hipStream_t)stream));
+}
+
+int mk_dev_ssz_merkle_finish(mk_call* call, const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32,
+                             void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    return S.done(rc ? rc : dev_finish(d_roots, nroots, n_total, d_out32, (hipStream_t)stream));
+}
+
+int mk_ssz_merkle_hash_multi(mk_call* call, const uint8_t* items, uint64_t n, uint32_t item_len, int nshards,
+                             const int* devs, uint8_t out[32]) {
+    Scope S(call);
+    return S.done(host_merkle_multi(items, n, item_len, nshards, devs, out));
+}
+
+int mk_dev_ssz_merkle_hash_multi(mk_call* call, const void* const* d_shards, uint64_t n, uint32_t item_len,
+                                 int ndev, void* d_out32, void* const* streams) {
+    Scope S(call);
+    return S.done(dev_merkle_multi(d_shards, n, item_len, ndev, d_out32, streams));
+}
+
+// ---- struct hashing ---------------------------------------------------------------
+uint64_t mk_ssz_struct_msg_len(const mk_field* fields, uint32_t nfields) {
+    Scope S(nullptr, false);
+    mk::StructSpec sp;
+    if (make_spec(fields, nfields, 0, sp) != MK_OK) return 0;
+    return sp.msg_len;
+}
+
+uint64_t mk_ssz_struct_list_workspace_bytes(uint64_t n, const mk_field* fields, uint32_t nfields) {
+    Scope S(nullptr, false);
+    mk::StructSpec sp;
+    if (make_spec(fields, nfields, 0, sp) != MK_OK) return 0;
+    return struct_list_ws(n, sp);
+}
+
+int mk_dev_ssz_struct_list_root(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
+                                const mk_field* fields, uint32_t nfields, void* d_out32, void* d_ws,
+                                uint64_t ws_bytes, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    mk::StructSpec sp;
+    rc = make_spec(fields, nfields, record_len, sp);
+    if (rc) return S.done(rc);
+    if (ws_bytes < struct_list_ws(n, sp)) return S.done(fail(MK_ENOMEM, "workspace too small"));
+    if (n && !d_records) return S.done(fail(MK_EINVAL, "null pointer"));
+    uint8_t* ws = (uint8_t*)d_ws;
+    uint8_t* msg = ws;
+    uint8_t* roots = ws + align256(n * sp.msg_len);
+    uint8_t* mws = roots + align256(32 * n);
+    hipStream_t st = (hipStream_t)stream;
+    rc = launch_struct_roots(d_records, n, sp, msg, roots, st);
+    if (rc) return S.done(rc);
+    return S.done(dev_merkle_hash(roots, n, 32, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), st));
+}
+
+int mk_dev_ssz_struct_roots(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
+                            const mk_field* fields, uint32_t nfields, void* d_roots, void* d_ws, uint64_t ws_bytes,
+                            void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    mk::StructSpec sp;
+    rc = make_spec(fields, nfields, record_len, sp);
+    if (rc) return S.done(rc);
+    if (n && (!d_records || !d_roots)) return S.done(fail(MK_EINVAL, "null pointer"));
+    if (ws_bytes < n * (uint64_t)sp.msg_len) return S.done(fail(MK_ENOMEM, "workspace too small"));
+    return S.done(launch_struct_roots(d_records, n, sp, d_ws, d_roots, (hipStream_t)stream));
+}
+
+static int host_struct_roots(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
+                             uint32_t nfields, uint8_t* roots) {
+    mk::StructSpec sp;
+    TRY(make_spec(fields, nfields, record_len, sp));
+    if (n && (!records || !roots)) return fail(MK_EINVAL, "null pointer");
+    TRY(bind_call());
+    if (n == 0) return MK_OK;
+    DevCtx* c = ctx();
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t st = c->stream;
+    TRY(grow(c->in, n * (size_t)record_len));
+    TRY(grow(c->ws, align256(n * sp.msg_len)));
+    TRY(grow(c->out, 32 * n));
+    HIPCHK(hipMemcpyAsync(c->in.p, records, n * (size_t)record_len, hipMemcpyHostToDevice, st));
+    TRY(launch_struct_roots(c->in.p, n, sp, c->ws.p, c->out.p, st));
+    HIPCHK(hipMemcpyAsync(roots, c->out.p, 32 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+int mk_ssz_struct_roots(mk_call* call, const uint8_t* records, uint64_t n, uint32_t record_len,
+                        const mk_field* fields, uint32_t nfields, uint8_t* roots) {
+    Scope S(call);
+    return S.done(host_struct_roots(records, n, record_len, fields, nfields, roots));
+}
+
+static int host_struct_list_root(const uint8_t* records, uint64_t n, uint32_t record_len, const mk_field* fields,
+                                 uint32_t nfields, uint8_t* out) {
+    mk::StructSpec sp;
+    TRY(make_spec(fields, nfields, record_len, sp));
+    if (!out || (n && !records)) return fail(MK_EINVAL, "null pointer");
+    TRY(bind_call());
+    DevCtx* c = ctx();
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t st = c->stream;
+    const uint64_t wsb = struct_list_ws(n, sp);
+    TRY(grow(c->in, n * (size_t)record_len));
+    TRY(grow(c->ws, wsb));
+    TRY(grow(c->out, 32));
+    // The records cross PCIe in chunks on the copy stream; the struct-roots
+    // kernel of chunk i runs on the compute stream while chunk i+1 is in
+    // flight, so only the last chunk's roots and the list merkleHash follow
+    // the copy.
+    uint8_t* ws = (uint8_t*)c->ws.p;
+    uint8_t* msg = ws;
+    uint8_t* roots = ws + align256(n * sp.msg_len);
+    uint8_t* mws = roots + align256(32 * n);
+    const uint8_t* din = (const uint8_t*)c->in.p;
+    uint64_t chunk = std::max<uint64_t>(kH2dMinChunk, ceil_div(n, kH2dChunks));
+    chunk = (chunk + 15) & ~15ull;  // chunk starts keep the records' 16-B alignment
+    for (uint64_t off = 0; off < n; off += chunk) {
+        const uint64_t cnt = std::min(chunk, n - off);
+        HIPCHK(hipMemcpyAsync((uint8_t*)c->in.p + off * record_len, records + off * record_len,
+                              cnt * (size_t)record_len, hipMemcpyHostToDevice, c->copy));
+        HIPCHK(hipEventRecord(c->h2d, c->copy));
+        HIPCHK(hipStreamWaitEvent(st, c->h2d, 0));
+        TRY(launch_struct_roots(din + off * record_len, cnt, sp, msg + off * sp.msg_len, roots + 32 * off, st));
+    }
+    TRY(dev_merkle_hash(roots, n, 32, c->out.p, mws, wsb - (uint64_t)(mws - ws), st));
+    HIPCHK(hipMemcpyAsync(out, c->out.p, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+int mk_ssz_struct_list_root(mk_call* call, const uint8_t* records, uint64_t n, uint32_t record_len,
+                            const mk_field* fields, uint32_t nfields, uint8_t out[32]) {
+    Scope S(call);
+    return S.done(host_struct_list_root(records, n, record_len, fields, nfields, out));
+}
+
+// ---- hashutil.MerkleRoot -----------------------------------------------------------
+uint64_t mk_merkle_root_workspace_bytes(uint64_t n) {
+    Scope S(nullptr, false);
+    return merkle_root_ws(n);
+}
+
+int mk_dev_merkle_root(mk_call* call, const void* d_data, const uint64_t* d_offs, uint64_t n, uint32_t fixed_len,
+                       void* d_heap, uint64_t heap_bytes, void* d_leaves32, void* d_out32, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    return S.done(rc ? rc
+                     : dev_merkle_root(d_data, d_offs, n, fixed_len, d_heap, heap_bytes, d_leaves32, d_out32,
+                                       (hipStream_t)stream));
+}
+
+static int host_merkle_root(const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_t* leaves_out,
+                            uint8_t* out) {
+    if (!out || (n && !offs)) return fail(MK_EINVAL, "null pointer");
+    if (n == 0) return fail(MK_EINVAL, "MerkleRoot of an empty list (reference: index out of range)");
+    TRY(bind_call());
+    DevCtx* c = ctx();
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t st = c->stream;
+    const size_t inb = offs[n] - offs[0];
+    const int64_t ulen = uniform_len(offs, n);
+    const uint64_t wsb = merkle_root_ws(n);
+    TRY(grow(c->in, inb + 16));
+    TRY(grow(c->aux, 8 * (n + 1)));
+    TRY(grow(c->ws, wsb));
+    TRY(grow(c->out, 32));
+    if (inb) HIPCHK(hipMemcpyAsync(c->in.p, data + offs[0], inb, hipMemcpyHostToDevice, st));
+    std::vector<uint64_t> rel;
+    if (ulen < 0) {
+        rel.assign(offs, offs + n + 1);
+        for (auto& o : rel) o -= offs[0];
+        HIPCHK(hipMemcpyAsync(c->aux.p, rel.data(), 8 * (n + 1), hipMemcpyHostToDevice, st));
+    }
+    TRY(dev_merkle_root(c->in.p, ulen < 0 ? (const uint64_t*)c->aux.p : nullptr, n, ulen < 0 ? 0 : (uint32_t)ulen,
+                        c->ws.p, wsb, nullptr, c->out.p, st));
+    HIPCHK(hipMemcpyAsync(out, c->out.p, 32, hipMemcpyDeviceToHost, st));
+    if (leaves_out) HIPCHK(hipMemcpyAsync(leaves_out, (uint8_t*)c->ws.p + 32 * n, 32 * n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));  // `rel` and the caller's buffers are released after this
+    return MK_OK;
+}
+
+int mk_merkle_root(mk_call* call, const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_t* leaves_out,
+                   uint8_t out[32]) {
+    Scope S(call);
+    return S.done(host_merkle_root(data, offs, n, leaves_out, out));
+}
+
+// ---- deposit trie -------------------------------------------------------------------
+uint64_t mk_deposit_trie_levels_bytes(uint64_t capacity, uint32_t depth) {
+    if (capacity == 0) return 0;
+    return 32 * mk::trie_levels_nodes(capacity, depth);
+}
+
+int mk_dev_deposit_trie_append(mk_call* call, void* d_levels, uint64_t capacity, uint64_t count, const void* d_data,
+                               const uint64_t* d_offs, uint64_t k, uint32_t fixed_len, uint32_t depth,
+                               void* d_root32, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    return S.done(rc ? rc
+                     : dev_trie_append(d_levels, capacity, count, d_data, d_offs, k, fixed_len, depth, d_root32,
+                                       (hipStream_t)stream));
+}
+
+int mk_dev_deposit_trie_branch(mk_call* call, const void* d_levels, uint64_t capacity, uint64_t count,
+                               uint32_t depth, uint64_t index, void* d_branch, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    return S.done(rc ? rc : dev_trie_branch(d_levels, capacity, count, depth, index, d_branch, (hipStream_t)stream));
+}
+
+// Uploads host deposits (data, offs[k+1]) for an append; fixed_len > 0 when uniform.
+static int upload_deposits(DevCtx* c, DevBuf& in, DevBuf& offs_buf, const uint8_t* data, const uint64_t* offs,
+                           uint64_t k, const uint64_t** d_offs, uint32_t* fixed_len, std::vector<uint64_t>& rel) {
+    const size_t inb = offs[k] - offs[0];
+    const int64_t ulen = uniform_len(offs, k);
+    TRY(grow(in, inb + 16));
+    if (inb) HIPCHK(hipMemcpyAsync(in.p, data + offs[0], inb, hipMemcpyHostToDevice, c->stream));
+    if (ulen >= 0) {
+        *d_offs = nullptr;
+        *fixed_len = (uint32_t)ulen;
+        return MK_OK;
+    }
+    rel.assign(offs, offs + k + 1);
+    for (auto& o : rel) o -= offs[0];
+    TRY(grow(offs_buf, 8 * (k + 1)));
+    HIPCHK(hipMemcpyAsync(offs_buf.p, rel.data(), 8 * (k + 1), hipMemcpyHostToDevice, c->stream));
+    *d_offs = (const uint64_t*)offs_buf.p;
+    *fixed_len = 0;
+    return MK_OK;
+}
+
+static int host_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
+                           uint8_t* levels_out, uint8_t* root) {
+    if (!root || (n && !offs)) return fail(MK_EINVAL, "null pointer");
+    TRY(check_trie(n, 0, n, depth));
+    if (n == 0) {
+        std::memset(root, 0, 32);
+        return MK_OK;
+    }
+    TRY(bind_call());
+    DevCtx* c = ctx();
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t st = c->stream;
+    const uint64_t lv_bytes = mk_deposit_trie_levels_bytes(n, depth);
+    TRY(grow(c->ws, lv_bytes));
+    TRY(grow(c->out, 32));
+    const uint64_t* d_offs = nullptr;
+    uint32_t fixed = 0;
+    std::vector<uint64_t> rel;
+    TRY(upload_deposits(c, c->in, c->aux, data, offs, n, &d_offs, &fixed, rel));
+    TRY(dev_trie_append(c->ws.p, n, 0, c->in.p, d_offs, n, fixed, depth, c->out.p, st));
+    HIPCHK(hipMemcpyAsync(root, c->out.p, 32, hipMemcpyDeviceToHost, st));
+    if (levels_out) HIPCHK(hipMemcpyAsync(levels_out, c->ws.p, lv_bytes, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+int mk_deposit_trie_build(mk_call* call, const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
+                          uint8_t* levels_out, uint8_t root[32]) {
+    Scope S(call);
+    return S.done(host_trie_build(data, offs, n, depth, levels_out, root));
+}
+
+int mk_deposit_trie_new(mk_call* call, uint32_t depth, uint64_t capacity, mk_trie** out) {
+    Scope S(call);
+    if (!out) return S.done(fail(MK_EINVAL, "null pointer"));
+    *out = nullptr;
+    if (depth == 0 || depth > 63) return S.done(fail(MK_EINVAL, "depth %u out of range (1..63)", depth));
+    int rc = bind_call();
+    if (rc) return S.done(rc);
+    auto* t = new (std::nothrow) mk_trie();
+    if (!t) return S.done(fail(MK_ENOMEM, "trie allocation failed"));
+    t->dev = t_bound;
+    t->depth = depth;
+    t->cap = std::max<uint64_t>(capacity, 1024);
+    if (depth < 63) t->cap = std::min<uint64_t>(t->cap, 1ull << depth);
+    rc = grow(t->levels, mk_deposit_trie_levels_bytes(t->cap, depth));
+    if (!rc) rc = grow(t->root, 32);
+    if (!rc) rc = grow(t->branch, 32 * (size_t)depth);
+    if (rc) {
+        mk_deposit_trie_free(t);
+        return S.done(rc);
+    }
+    *out = t;
+    return S.done(MK_OK);
+}
+
+void mk_deposit_trie_free(mk_trie* t) {
+    if (!t) return;
+    int saved = -1;
+    const bool restore = hipGetDevice(&saved) == hipSuccess;
+    (void)hipSetDevice(t->dev);
+    for (DevBuf* b : {&t->levels, &t->root, &t->in, &t->offs, &t->branch})
+        if (b->p) (void)hipFree(b->p);
+    if (restore) (void)hipSetDevice(saved);
+    delete t;
+}
+
+uint64_t mk_deposit_trie_count(const mk_trie* t) { return t ? t->count : 0; }
+
+static int trie_append(mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k) {
+    if (!t || (k && !offs)) return fail(MK_EINVAL, "null pointer");
+    std::lock_guard<std::mutex> tl(t->mu);
+    if (k == 0) return MK_OK;
+    TRY(check_trie(UINT64_MAX, t->count, k, t->depth));
+    TRY(bind_dev(t->dev));
+    DevCtx* c = ctx();
+    hipStream_t st = c->stream;
+    if (t->count + k > t->cap) {  // double the capacity, moving every level to its new slot
+        uint64_t ncap = std::max(2 * t->cap, t->count + k);
+        if (t->depth < 63) ncap = std::min<uint64_t>(ncap, 1ull << t->depth);
+        DevBuf nl;
+        TRY(grow(nl, mk_deposit_trie_levels_bytes(ncap, t->depth)));
+        for (uint32_t d = 0; d <= t->depth && t->count; ++d)
+            HIPCHK(hipMemcpyAsync(trie_level(nl.p, ncap, d), trie_level(t->levels.p, t->cap, d),
+                                  32 * mk::trie_count(t->count, d), hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+        (void)hipFree(t->levels.p);
+        t->levels = nl;
+        t->cap = ncap;
+    }
+    const uint64_t* d_offs = nullptr;
+    uint32_t fixed = 0;
+    std::vector<uint64_t> rel;
+    TRY(upload_deposits(c, t->in, t->offs, data, offs, k, &d_offs, &fixed, rel));
+    TRY(dev_trie_append(t->levels.p, t->cap, t->count, t->in.p, d_offs, k, fixed, t->depth, t->root.p, st));
+    HIPCHK(hipStreamSynchronize(st));  // the caller's buffers and `rel` are released after this
+    t->count += k;
+    return MK_OK;
+}
+
+int mk_deposit_trie_append(mk_call* call, mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k) {
+    Scope S(call);
+    return S.done(trie_append(t, data, offs, k));
+}
+
+static int trie_root(mk_trie* t, uint8_t* root) {
+    if (!t || !root) return fail(MK_EINVAL, "null pointer");
+    std::lock_guard<std::mutex> tl(t->mu);
+    if (t->count == 0) {
+        std::memset(root, 0, 32);
+        return MK_OK;
+    }
+    TRY(bind_dev(t->dev));
+    HIPCHK(hipMemcpyAsync(root, t->root.p, 32, hipMemcpyDeviceToHost, ctx()->stream));
+    HIPCHK(hipStreamSynchronize(ctx()->stream));
+    return MK_OK;
+}
+
+int mk_deposit_trie_root(mk_call* call, mk_trie* t, uint8_t root[32]) {
+    Scope S(call);
+    return S.done(trie_root(t, root));
+}
+
+static int trie_branch(mk_trie* t, uint64_t index, uint8_t* branch) {
+    if (!t || !branch) return fail(MK_EINVAL, "null pointer");
+    std::lock_guard<std::mutex> tl(t->mu);
+    if (t->count == 0) {
+        std::memset(branch, 0, 32 * (size_t)t->depth);
+        return MK_OK;
+    }
+    TRY(bind_dev(t->dev));
+    hipStream_t st = ctx()->stream;
+    TRY(dev_trie_branch(t->levels.p, t->cap, t->count, t->depth, index, t->branch.p, st));
+    HIPCHK(hipMemcpyAsync(branch, t->branch.p, 32 * (size_t)t->depth, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+int mk_deposit_trie_branch(mk_call* call, mk_trie* t, uint64_t index, uint8_t* branch) {
+    Scope S(call);
+    return S.done(trie_branch(t, index, branch));
+}
+
+static int trie_leaves(mk_trie* t, uint64_t first, uint64_t cnt, uint8_t* out) {
+    if (!t || (cnt && !out)) return fail(MK_EINVAL, "null pointer");
+    std::lock_guard<std::mutex> tl(t->mu);
+    if (first > t->count || cnt > t->count - first)
+        return fail(MK_EINVAL, "leaves [%llu, +%llu) beyond %llu deposits", (unsigned long long)first,
+                    (unsigned long long)cnt, (unsigned long long)t->count);
+    if (!cnt) return MK_OK;
+    TRY(bind_dev(t->dev));
+    hipStream_t st = ctx()->stream;
+    HIPCHK(hipMemcpyAsync(out, trie_level(t->levels.p, t->cap, 0) + 2 * first, 32 * cnt, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
+}
+
+int mk_deposit_trie_leaves(mk_call* call, mk_trie* t, uint64_t first, uint64_t cnt, uint8_t* out) {
+    Scope S(call);
+    return S.done(trie_leaves(t, first, cnt, out));
+}
+
+static int host_verify(const uint8_t* leaves, const uint8_t* branches, const uint64_t* indices, uint64_t n,
+                       uint32_t depth, uint32_t tree_depth, const uint8_t* roots, uint8_t* ok) {
+    if (n && (!leaves || !indices || !roots || !ok || (depth && !branches))) return fail(MK_EINVAL, "null pointer");
+    TRY(bind_call());
+    if (n == 0) return MK_OK;
+    DevCtx* c = ctx();
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t st = c->stream;
     const size_t bb = 32 * (size_t)depth * n;
-    TRY(grow(L.c->in, bb + 64 * n + 16));
-    TRY(grow(L.c->aux, 8 * n));
-    TRY(grow(L.c->out, n));
-    uint8_t* base = (uint8_t*)L.c->in.p;
+    TRY(grow(c->in, bb + 64 * n + 16));
+    TRY(grow(c->aux, 8 * n));
+    TRY(grow(c->out, n));
+    uint8_t* base = (uint8_t*)c->in.p;
     uint8_t* d_leaves = base;
     uint8_t* d_roots = base + 32 * n;
     uint8_t* d_br = base + 64 * n;
     HIPCHK(hipMemcpyAsync(d_leaves, leaves, 32 * n, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(d_roots, roots, 32 * n, hipMemcpyHostToDevice, st));
     if (bb) HIPCHK(hipMemcpyAsync(d_br, branches, bb, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(L.c->aux.p, indices, 8 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(c->aux.p, indices, 8 * n, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(mk::k_verify_branches, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint4*)d_leaves,
-                       (const uint4*)d_br, (const uint64_t*)L.c->aux.p, depth, tree_depth, (const uint4*)d_roots, n,
-                       (uint8_t*)L.c->out.p);
+                       (const uint4*)d_br, (const uint64_t*)c->aux.p, depth, tree_depth, (const uint4*)d_roots, n,
+                       (uint8_t*)c->out.p);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(ok, L.c->out.p, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ok, c->out.p, n, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return MK_OK;
 }
 
+int mk_verify_merkle_branches(mk_call* call, const uint8_t* leaves, const uint8_t* branches,
+                              const uint64_t* indices, uint64_t n, uint32_t depth, uint32_t tree_depth,
+                              const uint8_t* roots, uint8_t* ok) {
+    Scope S(call);
+    return S.done(host_verify(leaves, branches, indices, n, depth, tree_depth, roots, ok));
+}
+
 // ---- synthetic inputs -------------------------------------------------------------
-int mk_dev_synth_fill(void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t word0, void* stream) {
-    TRY(bind(-1));
-    if (nbytes % 8) return fail(MK_EINVAL, "nbytes %% 8 != 0");
-    if ((uintptr_t)d_dst % 8) return fail(MK_EINVAL, "destination not 8-byte aligned");
+int mk_dev_synth_fill(mk_call* call, void* d_dst, uint64_t nbytes, uint64_t seed, uint64_t word0, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    if (nbytes % 8) return S.done(fail(MK_EINVAL, "nbytes %% 8 != 0"));
+    if ((uintptr_t)d_dst % 8) return S.done(fail(MK_EINVAL, "destination not 8-byte aligned"));
     const uint64_t nwords = nbytes / 8;
-    if (!nwords) return MK_OK;
+    if (!nwords) return S.done(MK_OK);
     const uint64_t grid = std::min<uint64_t>(ceil_div(nwords, 256), 256 * 64);
     hipLaunchKernelGGL(mk::k_synth, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint64_t*)d_dst, nwords, seed,
                        word0);
-    HIPCHK(hipGetLastError());
-    return MK_OK;
+    hipError_t e = hipGetLastError();
+    return S.done(e == hipSuccess ? MK_OK : fail(MK_EHIP, "k_synth: %s", hipGetErrorString(e)));
 }
 
 // ---- measurement ----------------------------------------------------------------------
@@ -1278,7 +1729,7 @@ int mk_prof_enable(int on) {
     return MK_OK;
 }
 
-int mk_prof_read(double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms, double* leaf_hashes) {
+static int prof_read(double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms, double* leaf_hashes) {
     std::vector<ProfRec> recs;
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -1300,6 +1751,11 @@ int mk_prof_read(double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms, d
     if (leaf_perms) *leaf_perms = perms;
     if (leaf_hashes) *leaf_hashes = hashes;
     return MK_OK;
+}
+
+int mk_prof_read(mk_call* call, double* leaf_ms, uint64_t* leaf_launches, double* leaf_perms, double* leaf_hashes) {
+    Scope S(call);
+    return S.done(prof_read(leaf_ms, leaf_launches, leaf_perms, leaf_hashes));
 }
 
 }  // extern "C"

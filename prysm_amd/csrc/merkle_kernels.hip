@@ -962,7 +962,7 @@ __global__ __launch_bounds__(kWaveThreads) void k_trie_top2(const uint32_t* __re
 // workgroups; the last launch (one workgroup) runs to the top of the trie.
 template <uint32_t NT>
 __global__ __launch_bounds__(NT) void k_trie_top3(const uint32_t* __restrict__ in, uint64_t cin,
-                                                  uint32_t* __restrict__ lv_out, uint32_t levels) {
+                                                  uint32_t* __restrict__ lv_out, uint32_t levels, uint64_t capn) {
     constexpr uint32_t kPairs = NT / 2;
     __shared__ uint32_t lds[8 * kPairs];
     const uint32_t tid = threadIdx.x, k = tid >> 1, p = tid & 1u;
@@ -997,18 +997,19 @@ __global__ __launch_bounds__(NT) void k_trie_top3(const uint32_t* __restrict__ i
             store_node3(dst, lo / 2 + k, false, p, d);
         }
         __syncthreads();
-        dst += 8 * cn;
+        dst += 8 * capn;  // next level's slot of the level array (capacity layout)
+        capn = (capn + 1) / 2;
         c = cn;
         m = mn;
         lo /= 2;
     }
 }
 
-template __global__ void k_trie_top3<64>(const uint32_t*, uint64_t, uint32_t*, uint32_t);
-template __global__ void k_trie_top3<128>(const uint32_t*, uint64_t, uint32_t*, uint32_t);
-template __global__ void k_trie_top3<256>(const uint32_t*, uint64_t, uint32_t*, uint32_t);
-template __global__ void k_trie_top3<512>(const uint32_t*, uint64_t, uint32_t*, uint32_t);
-template __global__ void k_trie_top3<1024>(const uint32_t*, uint64_t, uint32_t*, uint32_t);
+template __global__ void k_trie_top3<64>(const uint32_t*, uint64_t, uint32_t*, uint32_t, uint64_t);
+template __global__ void k_trie_top3<128>(const uint32_t*, uint64_t, uint32_t*, uint32_t, uint64_t);
+template __global__ void k_trie_top3<256>(const uint32_t*, uint64_t, uint32_t*, uint32_t, uint64_t);
+template __global__ void k_trie_top3<512>(const uint32_t*, uint64_t, uint32_t*, uint32_t, uint64_t);
+template __global__ void k_trie_top3<1024>(const uint32_t*, uint64_t, uint32_t*, uint32_t, uint64_t);
 
 // ----------------------------------------------------------------------------
 // Final hash for trees with <= 1 chunk: K(bytes[0,total) || [0^128 if n==0] || lenc)
@@ -1578,6 +1579,180 @@ __global__ __launch_bounds__(256) void k_synth(uint64_t* __restrict__ dst, uint6
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nwords; k += stride)
         dst[k] = splitmix(seed, word0 + k);
+}
+
+
+// ----------------------------------------------------------------------------
+// Incremental deposit trie (UpdateDepositTrie, deposit_trie.go:29-40, for a
+// batch of appended leaves): level d0 of the level array already holds the
+// new nodes [lo, c) (c = count at d0 after the append).  For every level d0+1
+// .. depth the workgroup recomputes the right edge [lo/2, ceil(c/2)) with
+// node = K(left || right), a missing right child read as 0^32 (map miss).
+// The only child left of the changed range (index lo-1 when lo is odd) is
+// old and read from the level array; the changed children are carried from
+// level to level in LDS (bit-interleaved lane pairs, mk::ilv).  One
+// workgroup, one parent per lane pair: the host keeps c - lo <= NT - 4.
+// Level d starts at node trie_level_off(cap, d) = sum_{i<d} ceil(cap/2^i).
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void k_trie_append(uint32_t* __restrict__ levels, uint64_t cap, uint32_t d0,
+                                                    uint64_t lo, uint64_t c, uint32_t depth,
+                                                    uint32_t* __restrict__ root_out) {
+    constexpr uint32_t kPairs = NT / 2;
+    __shared__ uint32_t lds[2][8 * kPairs];
+    const uint32_t tid = threadIdx.x, k = tid >> 1, p = tid & 1u;
+    uint64_t off = 0, capd = cap;  // node offset and capacity of level d0
+    for (uint32_t i = 0; i < d0; ++i) {
+        off += capd;
+        capd = (capd + 1) / 2;
+    }
+    int buf = 0;
+    for (uint32_t d = d0; d < depth; ++d) {
+        const uint32_t* cur = levels + 8 * off;
+        uint32_t* nxt = levels + 8 * (off + capd);
+        const uint64_t plo = lo >> 1, cp = (c + 1) >> 1, np = cp - plo;
+        const uint64_t j = plo + k;
+        if (k < np) {
+            uint32_t a[4], b[4] = {0, 0, 0, 0};
+            const uint64_t il = 2 * j, ir = 2 * j + 1;
+            if (d == d0 || il < lo)
+                load_node3(cur, il, false, p, a);
+            else
+#pragma unroll
+                for (int w = 0; w < 4; ++w) a[w] = lds[buf][8 * (il - lo) + 2 * w + p];
+            if (ir < c) {
+                if (d == d0)
+                    load_node3(cur, ir, false, p, b);
+                else
+#pragma unroll
+                    for (int w = 0; w < 4; ++w) b[w] = lds[buf][8 * (ir - lo) + 2 * w + p];
+            }
+            uint32_t h[4];
+            hash_pair3(a, b, false, p, h);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) lds[buf ^ 1][8 * k + 2 * w + p] = h[w];
+            store_node3(nxt, j, false, p, h);
+            if (d + 1 == depth && k == 0) store_node3(root_out, 0, false, p, h);
+        }
+        __syncthreads();
+        buf ^= 1;
+        off += capd;
+        capd = (capd + 1) / 2;
+        lo = plo;
+        c = cp;
+    }
+}
+template __global__ void k_trie_append<64>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t*);
+template __global__ void k_trie_append<256>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t*);
+template __global__ void k_trie_append<1024>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t*);
+
+// GenerateMerkleBranch (deposit_trie.go:43-58): branch[d] = the sibling of
+// index's ancestor at level d, 0^32 when that node does not exist.
+__global__ void k_trie_branch(const uint4* __restrict__ levels, uint64_t cap, uint64_t count, uint32_t depth,
+                              uint64_t index, uint4* __restrict__ branch) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= depth) return;
+    uint64_t off = 0, capd = cap, cd = count;
+    for (uint32_t i = 0; i < d; ++i) {
+        off += capd;
+        capd = (capd + 1) / 2;
+        cd = (cd + 1) / 2;
+    }
+    const uint64_t sib = (index >> d) ^ 1ull;
+    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0;
+    if (sib < cd) {
+        v0 = levels[2 * (off + sib)];
+        v1 = levels[2 * (off + sib) + 1];
+    }
+    branch[2 * d] = v0;
+    branch[2 * d + 1] = v1;
+}
+
+// ----------------------------------------------------------------------------
+// Many lists (segmented merkleHash, hash.go:194-239 per list): one launch per
+// level for all lists with nodes at that level.  Thread t of the launch maps
+// to (list, node j) by binary search over the level's act table (exclusive
+// prefix sums of the per-list node counts).  LEAF: node j = K(window j of the
+// list's chunks) (256-B contiguous windows on the streaming path, the generic
+// sponge for odd item sizes and ragged / padded windows); NODE: K(n[2j] ||
+// n[2j+1]) or K(n[2j] || 0^128) on an odd count.
+__device__ __forceinline__ uint32_t many_find(const ManyAct* __restrict__ act, uint32_t cnt, uint64_t t) {
+    uint32_t lo = 0, hi = cnt;  // act[lo].out_first <= t < act[hi].out_first
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (act[mid].out_first <= t)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+template <bool LEAF>
+__global__ __launch_bounds__(256) void k_many_level(const uint8_t* __restrict__ items,
+                                                    const ManyList* __restrict__ lists,
+                                                    const ManyAct* __restrict__ act, uint32_t nact, uint64_t nodes,
+                                                    const uint4* __restrict__ in, uint4* __restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nodes) return;
+    const ManyAct A = act[many_find(act, nact, t)];
+    const ManyList L = lists[A.list];
+    const uint64_t j = t - A.out_first;
+    uint4 d0, d1;
+    if constexpr (LEAF) {
+        const uint8_t* base = items + L.items_off;
+        if (L.fast && j < L.total / 256) {
+            hash_window256(reinterpret_cast<const uint4*>(base) + j * 16, d0, d1);
+        } else {
+            const uint64_t lo = j * 2 * L.cb;
+            uint64_t la;
+            uint32_t lz;
+            if (2 * j + 1 < L.nchunks) {
+                la = (lo + 2 * L.cb < L.total ? lo + 2 * L.cb : L.total) - lo;
+                lz = 0;
+            } else {
+                la = L.total - lo;
+                lz = 128;
+            }
+            sponge_generic(base + lo, la, lz, false, 0, d0, d1);
+        }
+    } else {
+        const uint64_t cprev = (L.c1 + (1ull << (A.level - 2)) - 1) >> (A.level - 2);  // nodes at level - 1
+        const uint4* src = in + 2 * (A.in_first + 2 * j);
+        const bool padded = !(2 * j + 1 < cprev);
+        uint4 r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+        if (!padded) {
+            r0 = src[2];
+            r1 = src[3];
+        }
+        hash_pair(src[0], src[1], r0, r1, padded, d0, d1);
+    }
+    out[2 * (A.out_first + j)] = d0;
+    out[2 * (A.out_first + j) + 1] = d1;
+}
+template __global__ void k_many_level<true>(const uint8_t*, const ManyList*, const ManyAct*, uint32_t, uint64_t,
+                                            const uint4*, uint4*);
+template __global__ void k_many_level<false>(const uint8_t*, const ManyList*, const ManyAct*, uint32_t, uint64_t,
+                                             const uint4*, uint4*);
+
+// Root of every list that is not a big list: K(top || le64(n) || 0^24), or
+// for <= 1 chunk K(bytes || [0^128 if n == 0] || le64(n) || 0^24).
+__global__ __launch_bounds__(256) void k_many_final(const uint8_t* __restrict__ items,
+                                                    const ManyList* __restrict__ lists, uint32_t nlists,
+                                                    const uint4* __restrict__ buf0, const uint4* __restrict__ buf1,
+                                                    uint4* __restrict__ roots) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nlists) return;
+    const ManyList L = lists[i];
+    if (L.levels == 0xFFFFFFFFu) return;  // big list: its own plan wrote the root
+    uint4 d0, d1;
+    if (L.levels == 0) {
+        sponge_generic(items + L.items_off, L.total, L.n == 0 ? 128u : 0u, true, L.n, d0, d1);
+    } else {
+        const uint4* b = ((L.levels - 1) & 1) ? buf1 : buf0;
+        hash_final(b[2 * L.root_pos], b[2 * L.root_pos + 1], L.n, d0, d1);
+    }
+    roots[2 * i] = d0;
+    roots[2 * i + 1] = d1;
 }
 
 }  // namespace mk

@@ -3,36 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "plan_types.hpp"
+
 namespace mk {
-
-constexpr uint32_t kReduceThreads = 256;             // 4 waves
-constexpr uint64_t kReduceSpan1 = 4 * kReduceThreads;  // first-level nodes per workgroup
-constexpr uint64_t kReduceSpan2 = kReduceSpan1 / 2;    // level-2 nodes per workgroup (LDS)
-constexpr uint32_t kMaxPassLevels = 5;               // levels per non-final pass (1024 -> 64)
-constexpr uint32_t kWaveThreads = 64;                // latency pass: one wave per workgroup
-constexpr uint32_t kWaveLevels = 7;                  // first level + 6 in-wave levels (64 -> 1)
-constexpr uint64_t kWaveMaxC1 = 1ull << 16;          // use the latency pass at or below this width (A/B: 2^19 is slower)
-constexpr uint32_t kWave2Span = kWaveThreads / 2;    // two lanes per state: 32 nodes per wave
-constexpr uint32_t kWave2Levels = 6;                 // first level + 5 in-wave levels (32 -> 1)
-constexpr uint32_t kMidThreads = 1024;               // largest k_wave3: 16 waves, 512 lane pairs, 10 levels
-
-struct ReduceArgs {
-    const uint8_t* items;  // LEAF: item bytes; NODE: 32-B input nodes
-    uint64_t total;        // LEAF: item bytes in the tree (shard)
-    uint64_t cb;           // LEAF: chunk bytes
-    uint64_t nchunks;      // LEAF: chunks in the tree (shard)
-    uint64_t cin;          // NODE: input node count
-    uint64_t c1;           // first-level node count (windows / input pairs)
-    uint64_t c1_full;      // first-level nodes eligible for the fast path
-    uint8_t* out;          // output nodes (or the 32-B digest when finalize)
-    uint64_t n_items;      // length mix-in value (finalize)
-    uint32_t levels;       // hashing levels this pass performs
-    uint32_t finalize;     // reduce to the root and mix in the length
-    uint32_t pad_at_one;   // subtree mode: keep hashing (x || 0^128) at count 1
-    uint64_t wg_base;      // workgroup index offset of this launch
-    uint32_t in_ilv;       // k_wave3: input nodes are bit-interleaved lane pairs
-    uint32_t out_ilv;      // k_wave3: write bit-interleaved output nodes
-};
 
 constexpr uint32_t kMaxStructFields = 32;
 #ifndef MK_STRUCT_THREADS
@@ -80,11 +53,21 @@ constexpr uint32_t kRecGridMax = MK_REC_GRID;  // k_keccak_rec grid cap (A/B at 
 __global__ void k_trie_reduce(const uint4* in, uint64_t cin, uint4* lv_out, uint32_t levels);
 __global__ void k_trie_top2(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels);
 template <uint32_t NT>
-__global__ void k_trie_top3(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels);
+__global__ void k_trie_top3(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels, uint64_t capn);
 __global__ void k_trie_tail(uint4* node, uint32_t count, uint4* levels);
 __global__ void k_verify_branches(const uint4* leaves, const uint4* branches, const uint64_t* indices,
                                   uint32_t depth, uint32_t tree_depth, const uint4* roots, uint64_t n,
                                   uint8_t* ok);
+template <uint32_t NT>
+__global__ void k_trie_append(uint32_t* levels, uint64_t cap, uint32_t d0, uint64_t lo, uint64_t c, uint32_t depth,
+                              uint32_t* root_out);
+__global__ void k_trie_branch(const uint4* levels, uint64_t cap, uint64_t count, uint32_t depth, uint64_t index,
+                              uint4* branch);
+template <bool LEAF>
+__global__ void k_many_level(const uint8_t* items, const ManyList* lists, const ManyAct* act, uint32_t nact,
+                             uint64_t nodes, const uint4* in, uint4* out);
+__global__ void k_many_final(const uint8_t* items, const ManyList* lists, uint32_t nlists, const uint4* buf0,
+                             const uint4* buf1, uint4* roots);
 __global__ void k_synth(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t word0);
 
 }  // namespace mk

@@ -1,0 +1,62 @@
+// Types and shape constants shared by the HIP kernels and the host planner.
+// Plain C++ (no HIP headers), so the planner also builds host-only with
+// gcc -fsanitize=address,undefined (tests/c_abi/planner_fuzz.cpp).
+#pragma once
+#include <stdint.h>
+
+namespace mk {
+
+constexpr uint32_t kReduceThreads = 256;             // 4 waves
+constexpr uint64_t kReduceSpan1 = 4 * kReduceThreads;  // first-level nodes per workgroup
+constexpr uint64_t kReduceSpan2 = kReduceSpan1 / 2;    // level-2 nodes per workgroup (LDS)
+constexpr uint32_t kMaxPassLevels = 5;               // levels per non-final pass (1024 -> 64)
+constexpr uint32_t kWaveThreads = 64;                // latency pass: one wave per workgroup
+constexpr uint32_t kWaveLevels = 7;                  // first level + 6 in-wave levels (64 -> 1)
+constexpr uint64_t kWaveMaxC1 = 1ull << 16;          // use the latency pass at or below this width (A/B: 2^19 is slower)
+constexpr uint32_t kWave2Span = kWaveThreads / 2;    // two lanes per state: 32 nodes per wave
+constexpr uint32_t kWave2Levels = 6;                 // first level + 5 in-wave levels (32 -> 1)
+constexpr uint32_t kMidThreads = 1024;               // largest k_wave3: 16 waves, 512 lane pairs, 10 levels
+
+struct ReduceArgs {
+    const uint8_t* items;  // LEAF: item bytes; NODE: 32-B input nodes
+    uint64_t total;        // LEAF: item bytes in the tree (shard)
+    uint64_t cb;           // LEAF: chunk bytes
+    uint64_t nchunks;      // LEAF: chunks in the tree (shard)
+    uint64_t cin;          // NODE: input node count
+    uint64_t c1;           // first-level node count (windows / input pairs)
+    uint64_t c1_full;      // first-level nodes eligible for the fast path
+    uint8_t* out;          // output nodes (or the 32-B digest when finalize)
+    uint64_t n_items;      // length mix-in value (finalize)
+    uint32_t levels;       // hashing levels this pass performs
+    uint32_t finalize;     // reduce to the root and mix in the length
+    uint32_t pad_at_one;   // subtree mode: keep hashing (x || 0^128) at count 1
+    uint64_t wg_base;      // workgroup index offset of this launch
+    uint32_t in_ilv;       // k_wave3: input nodes are bit-interleaved lane pairs
+    uint32_t out_ilv;      // k_wave3: write bit-interleaved output nodes
+};
+
+// One list of a segmented (many-lists) merkleHash level: k_many_leaf /
+// k_many_level map a global thread index to (list, node) by binary search
+// over `first` (exclusive prefix sum of this level's node counts).
+struct ManyList {
+    uint64_t items_off;  // byte offset of the list's items in the input buffer
+    uint64_t total;      // item bytes
+    uint64_t cb;         // chunk bytes
+    uint64_t nchunks;    // chunks
+    uint64_t n;          // items (length mix-in)
+    uint64_t root_pos;   // node index of the list's top node in its last level's buffer
+    uint64_t c1;         // level-1 node count (0: the list has <= 1 chunk)
+    uint32_t levels;     // hashing levels above the chunks (0 for <= 1 chunk)
+    uint32_t fast;       // 256-B contiguous windows (item_len | 128, 16-B aligned)
+};
+
+// Entry of a level's act table: list `list` writes its nodes of this level at
+// [out_first, out_first + count) and reads the level below at in_first.
+struct ManyAct {
+    uint32_t list;
+    uint32_t level;     // 1 = windows (input: the list's item bytes)
+    uint64_t out_first;
+    uint64_t in_first;
+};
+
+}  // namespace mk

@@ -3,12 +3,14 @@
 torch provides device memory, the current HIP stream and torch.distributed;
 every hash is computed by the HIP kernels behind the C-ABI
 (``mk_dev_*`` in include/prysm_merkle.h).  Work is enqueued on torch's
-current stream of the tensor's device and is not synchronised here.
+current stream of the tensor's device and is not synchronised here.  Every
+call passes its device in its own ``mk_call`` context (``_lib.invoke``).
 """
 from __future__ import annotations
 
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -22,18 +24,22 @@ def _p(t: torch.Tensor):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def _bind(t: torch.Tensor):
+def _np(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _dev(t: torch.Tensor) -> int:
+    """Device index of a GPU tensor (passed in every call's context)."""
     if t.device.type != "cuda":
         raise _lib.MerkleError(_lib.MK_EINVAL, "device entry points need a GPU tensor")
-    _lib.init(t.device.index or 0)
+    return t.device.index if t.device.index is not None else torch.cuda.current_device()
 
 
 def synth_fill(dst: torch.Tensor, seed: int, word0: int = 0) -> torch.Tensor:
     """Fill ``dst`` (uint8, nbytes % 8 == 0) with bytes [8*word0, ...) of the
     SplitMix64 stream."""
-    _bind(dst)
-    _lib.check(_lib.load().mk_dev_synth_fill(_p(dst), dst.numel() * dst.element_size(), seed, word0,
-                                             _stream(dst.device)), "mk_dev_synth_fill")
+    _lib.invoke("mk_dev_synth_fill", _p(dst), dst.numel() * dst.element_size(), seed, word0, _stream(dst.device),
+                device=_dev(dst))
     return dst
 
 
@@ -44,7 +50,7 @@ def struct_roots(records: torch.Tensor, n: int, record_len: int, spec, out: torc
     registry.VALIDATOR_FIELDS).  Returns an (n*32,) uint8 device tensor."""
     from .registry import _fields
 
-    _bind(records)
+    dev = _dev(records)
     if records.numel() < n * record_len:
         raise ValueError("records tensor shorter than n*record_len")
     f = _fields(spec)
@@ -54,8 +60,25 @@ def struct_roots(records: torch.Tensor, n: int, record_len: int, spec, out: torc
     if ws is None:
         ws = torch.empty(max(256, n * L.mk_ssz_struct_msg_len(f, len(spec))), dtype=torch.uint8,
                          device=records.device)
-    _lib.check(L.mk_dev_ssz_struct_roots(_p(records), n, record_len, f, len(spec), _p(out), _p(ws), ws.numel(),
-                                         _stream(records.device)), "mk_dev_ssz_struct_roots")
+    _lib.invoke("mk_dev_ssz_struct_roots", _p(records), n, record_len, f, len(spec), _p(out), _p(ws), ws.numel(),
+                _stream(records.device), device=dev)
+    return out
+
+
+def struct_list_root(records: torch.Tensor, n: int, record_len: int, spec, out: torch.Tensor = None,
+                     ws: torch.Tensor = None) -> torch.Tensor:
+    """TreeHash of a list of n flat records (struct roots + merkleHash)."""
+    from .registry import _fields
+
+    dev = _dev(records)
+    f = _fields(spec)
+    if out is None:
+        out = torch.empty(32, dtype=torch.uint8, device=records.device)
+    if ws is None:
+        ws = torch.empty(_lib.load().mk_ssz_struct_list_workspace_bytes(n, f, len(spec)) + 256, dtype=torch.uint8,
+                         device=records.device)
+    _lib.invoke("mk_dev_ssz_struct_list_root", _p(records), n, record_len, f, len(spec), _p(out), _p(ws), ws.numel(),
+                _stream(records.device), device=dev)
     return out
 
 
@@ -68,16 +91,41 @@ def merkle_hash(items: torch.Tensor, n: int, item_len: int, out: torch.Tensor = 
                 ws: torch.Tensor = None) -> torch.Tensor:
     """ssz.merkleHash of n items of item_len bytes held in ``items`` (uint8,
     device).  Returns a (32,) uint8 device tensor."""
-    _bind(items)
+    dev = _dev(items)
     if items.numel() < n * item_len:
         raise ValueError("items tensor shorter than n*item_len")
     if out is None:
         out = torch.empty(32, dtype=torch.uint8, device=items.device)
     if ws is None:
         ws = merkle_workspace(n, item_len, items.device)
-    _lib.check(_lib.load().mk_dev_ssz_merkle_hash(_p(items), n, item_len, _p(out), _p(ws), ws.numel(),
-                                                  _stream(items.device)), "mk_dev_ssz_merkle_hash")
+    _lib.invoke("mk_dev_ssz_merkle_hash", _p(items), n, item_len, _p(out), _p(ws), ws.numel(), _stream(items.device),
+                device=dev)
     return out
+
+
+def merkle_many(items: torch.Tensor, offs, ns, item_lens, out: torch.Tensor = None,
+                ws: torch.Tensor = None) -> torch.Tensor:
+    """merkleHash of many lists in one call (list i = ns[i] items of
+    item_lens[i] bytes at byte offset offs[i] of ``items``): an (nlists*32,)
+    uint8 device tensor of roots."""
+    dev = _dev(items)
+    k = len(ns)
+    o = np.ascontiguousarray(offs, dtype=np.uint64)
+    n = np.ascontiguousarray(ns, dtype=np.uint64)
+    il = np.ascontiguousarray(item_lens, dtype=np.uint32)
+    if out is None:
+        out = torch.empty(max(32, 32 * k), dtype=torch.uint8, device=items.device)
+    if ws is None:
+        ws = torch.empty(max(256, many_workspace_bytes(n, il)), dtype=torch.uint8, device=items.device)
+    _lib.invoke("mk_dev_ssz_merkle_many", _p(items), _np(o), _np(n), _np(il), k, _p(out), _p(ws), ws.numel(),
+                _stream(items.device), device=dev)
+    return out[:32 * k]
+
+
+def many_workspace_bytes(ns, item_lens) -> int:
+    n = np.ascontiguousarray(ns, dtype=np.uint64)
+    il = np.ascontiguousarray(item_lens, dtype=np.uint32)
+    return _lib.load().mk_ssz_merkle_many_workspace_bytes(_np(n), _np(il), len(n))
 
 
 def shard_plan(n: int, item_len: int, nshards: int):
@@ -85,8 +133,7 @@ def shard_plan(n: int, item_len: int, nshards: int):
     h = ctypes.c_uint32()
     ne = ctypes.c_uint32()
     begin = (ctypes.c_uint64 * (nshards + 1))()
-    _lib.check(_lib.load().mk_ssz_merkle_shard_plan(n, item_len, nshards, ctypes.byref(h), ctypes.byref(ne),
-                                                    begin), "mk_ssz_merkle_shard_plan")
+    _lib.invoke("mk_ssz_merkle_shard_plan", n, item_len, nshards, ctypes.byref(h), ctypes.byref(ne), begin)
     return h.value, ne.value, list(begin)
 
 
@@ -99,14 +146,13 @@ def subtree_workspace(shard_n: int, item_len: int, device) -> torch.Tensor:
 def merkle_subtree(items: torch.Tensor, shard_n: int, item_len: int, height: int, pad_at_one: bool,
                    out: torch.Tensor = None, ws: torch.Tensor = None) -> torch.Tensor:
     """32-B root of one shard at `height` levels above its chunks."""
-    _bind(items)
+    dev = _dev(items)
     if out is None:
         out = torch.empty(32, dtype=torch.uint8, device=items.device)
     if ws is None:
         ws = subtree_workspace(shard_n, item_len, items.device)
-    _lib.check(_lib.load().mk_dev_ssz_merkle_subtree(_p(items), shard_n, item_len, height, int(pad_at_one), _p(out),
-                                                     _p(ws), ws.numel(), _stream(items.device)),
-               "mk_dev_ssz_merkle_subtree")
+    _lib.invoke("mk_dev_ssz_merkle_subtree", _p(items), shard_n, item_len, height, int(pad_at_one), _p(out), _p(ws),
+                ws.numel(), _stream(items.device), device=dev)
     return out
 
 
@@ -114,9 +160,9 @@ def merkle_subtree_frontier(items: torch.Tensor, shard_n: int, item_len: int, he
                             pad_at_one: bool, out: torch.Tensor = None, ws: torch.Tensor = None) -> torch.Tensor:
     """The shard's tree level `frontier_log2` levels below its root: a
     (nodes*32,) uint8 device tensor (nodes = parallel.frontier_count(...))."""
-    _bind(items)
     from .parallel import frontier_count
 
+    dev = _dev(items)
     nodes = frontier_count(shard_n, item_len, height, frontier_log2)
     if out is None:
         out = torch.empty(32 << frontier_log2, dtype=torch.uint8, device=items.device)
@@ -125,9 +171,8 @@ def merkle_subtree_frontier(items: torch.Tensor, shard_n: int, item_len: int, he
     if ws is None:
         ws = subtree_workspace(shard_n, item_len, items.device)
     got = ctypes.c_uint64()
-    _lib.check(_lib.load().mk_dev_ssz_merkle_subtree_frontier(
-        _p(items), shard_n, item_len, height, frontier_log2, int(pad_at_one), _p(out), ctypes.byref(got), _p(ws),
-        ws.numel(), _stream(items.device)), "mk_dev_ssz_merkle_subtree_frontier")
+    _lib.invoke("mk_dev_ssz_merkle_subtree_frontier", _p(items), shard_n, item_len, height, frontier_log2,
+                int(pad_at_one), _p(out), ctypes.byref(got), _p(ws), ws.numel(), _stream(items.device), device=dev)
     assert got.value == nodes, (got.value, nodes)
     return out[:32 * nodes]
 
@@ -137,7 +182,7 @@ def merkle_node_frontier(nodes: torch.Tensor, count: int, height: int, frontier_
     """A subtree continued from one of its node levels: `count` 32-B nodes
     reduced `height` levels (odd rule, hash.go:225-235), stopping
     `frontier_log2` levels below the top; returns the (nodes*32,) level."""
-    _bind(nodes)
+    dev = _dev(nodes)
     lib = _lib.load()
     want = max(1, -(-count // (1 << (height - frontier_log2)))) if frontier_log2 else 1
     if out is None:
@@ -148,9 +193,8 @@ def merkle_node_frontier(nodes: torch.Tensor, count: int, height: int, frontier_
         ws = torch.empty(max(256, lib.mk_ssz_merkle_node_frontier_workspace_bytes(count, height, frontier_log2)),
                          dtype=torch.uint8, device=nodes.device)
     got = ctypes.c_uint64()
-    _lib.check(lib.mk_dev_ssz_merkle_node_frontier(_p(nodes), count, height, frontier_log2, int(pad_at_one), _p(out),
-                                                   ctypes.byref(got), _p(ws), ws.numel(), _stream(nodes.device)),
-               "mk_dev_ssz_merkle_node_frontier")
+    _lib.invoke("mk_dev_ssz_merkle_node_frontier", _p(nodes), count, height, frontier_log2, int(pad_at_one), _p(out),
+                ctypes.byref(got), _p(ws), ws.numel(), _stream(nodes.device), device=dev)
     assert got.value == want, (got.value, want)
     return out[:32 * want]
 
@@ -164,33 +208,71 @@ def merkle_finish_nodes(nodes: torch.Tensor, count: int, n_total: int, out: torc
                         ws: torch.Tensor = None) -> torch.Tensor:
     """Reference level loop over one gathered tree level of `count` nodes +
     length mix-in (the finisher of the frontier sharding)."""
-    _bind(nodes)
+    dev = _dev(nodes)
     if out is None:
         out = torch.empty(32, dtype=torch.uint8, device=nodes.device)
     if ws is None:
         ws = finish_workspace(count, nodes.device)
-    _lib.check(_lib.load().mk_dev_ssz_merkle_finish_nodes(_p(nodes), count, n_total, _p(out), _p(ws), ws.numel(),
-                                                          _stream(nodes.device)), "mk_dev_ssz_merkle_finish_nodes")
+    _lib.invoke("mk_dev_ssz_merkle_finish_nodes", _p(nodes), count, n_total, _p(out), _p(ws), ws.numel(),
+                _stream(nodes.device), device=dev)
     return out
 
 
 def merkle_finish(roots: torch.Tensor, nroots: int, n_total: int, out: torch.Tensor = None) -> torch.Tensor:
     """Reference level loop over gathered shard roots + length mix-in."""
-    _bind(roots)
+    dev = _dev(roots)
     if out is None:
         out = torch.empty(32, dtype=torch.uint8, device=roots.device)
-    _lib.check(_lib.load().mk_dev_ssz_merkle_finish(_p(roots), nroots, n_total, _p(out), _stream(roots.device)),
-               "mk_dev_ssz_merkle_finish")
+    _lib.invoke("mk_dev_ssz_merkle_finish", _p(roots), nroots, n_total, _p(out), _stream(roots.device), device=dev)
+    return out
+
+
+def merkle_hash_multi(shards, n: int, item_len: int, out: torch.Tensor, streams=None) -> torch.Tensor:
+    """Single-process multi-device merkleHash (the cgo caller's form):
+    shards[d] on device d holds shard d of shard_plan(n, item_len,
+    len(shards)); RCCL all-gather of the frontiers, device 0 finishes into
+    ``out`` (a (32,) tensor on device 0)."""
+    k = len(shards)
+    ptrs = (ctypes.c_void_p * k)(*[s.data_ptr() for s in shards])
+    sts = (ctypes.c_void_p * k)(*[(streams[d] if streams else torch.cuda.current_stream(shards[d].device)).cuda_stream
+                                  for d in range(k)])
+    _lib.invoke("mk_dev_ssz_merkle_hash_multi", ptrs, n, item_len, k, _p(out), sts, device=0)
     return out
 
 
 def hash_batch(msgs: torch.Tensor, n: int, msg_len: int, out: torch.Tensor = None) -> torch.Tensor:
     """Batched Hash of n fixed-length messages resident on the device."""
-    _bind(msgs)
+    dev = _dev(msgs)
     if out is None:
         out = torch.empty(n * 32, dtype=torch.uint8, device=msgs.device)
-    _lib.check(_lib.load().mk_dev_hash_batch(_p(msgs), n, msg_len, _p(out), _stream(msgs.device)),
-               "mk_dev_hash_batch")
+    _lib.invoke("mk_dev_hash_batch", _p(msgs), n, msg_len, _p(out), _stream(msgs.device), device=dev)
+    return out
+
+
+def deposit_trie_levels_bytes(capacity: int, depth: int) -> int:
+    return _lib.load().mk_deposit_trie_levels_bytes(capacity, depth)
+
+
+def deposit_trie_append(levels: torch.Tensor, capacity: int, count: int, data: torch.Tensor, k: int,
+                        fixed_len: int, depth: int, root: torch.Tensor, offs: torch.Tensor = None) -> None:
+    """Append k deposits (fixed_len-byte records in ``data``, or variable
+    length with device ``offs``) to the device trie holding ``count``
+    deposits: UpdateDepositTrie (deposit_trie.go:29-40) batched, right edge
+    of every level only; count == 0 is the batch build."""
+    dev = _dev(levels)
+    _lib.invoke("mk_dev_deposit_trie_append", _p(levels), capacity, count, _p(data),
+                _p(offs) if offs is not None else None, k, fixed_len, depth, _p(root), _stream(levels.device),
+                device=dev)
+
+
+def deposit_trie_branch(levels: torch.Tensor, capacity: int, count: int, depth: int, index: int,
+                        out: torch.Tensor = None) -> torch.Tensor:
+    """GenerateMerkleBranch(index) of a device trie: (depth*32,) uint8."""
+    dev = _dev(levels)
+    if out is None:
+        out = torch.empty(32 * depth, dtype=torch.uint8, device=levels.device)
+    _lib.invoke("mk_dev_deposit_trie_branch", _p(levels), capacity, count, depth, index, _p(out),
+                _stream(levels.device), device=dev)
     return out
 
 
@@ -204,6 +286,5 @@ def prof_read():
     cnt = ctypes.c_uint64()
     perms = ctypes.c_double()
     hashes = ctypes.c_double()
-    _lib.check(_lib.load().mk_prof_read(ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(perms), ctypes.byref(hashes)),
-               "mk_prof_read")
+    _lib.invoke("mk_prof_read", ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(perms), ctypes.byref(hashes))
     return ms.value, cnt.value, perms.value, hashes.value

@@ -34,7 +34,7 @@ def Hash(data: bytes) -> bytes:
     data = bytes(data)
     out = ctypes.create_string_buffer(32)
     buf = ctypes.create_string_buffer(data, max(1, len(data)))
-    _lib.check(_lib.load().mk_hash(buf, len(data), out), "mk_hash")
+    _lib.invoke("mk_hash", buf, len(data), out)
     return out.raw
 
 
@@ -46,7 +46,7 @@ def hash_batch(msgs: np.ndarray, msg_len: int) -> np.ndarray:
         raise ValueError("msg_len must be > 0 (use hash_batch_var for empty messages)")
     n = a.size // msg_len
     out = np.empty((n, 32), dtype=np.uint8)
-    _lib.check(_lib.load().mk_hash_batch(_ptr(a), n, msg_len, _ptr(out)), "mk_hash_batch")
+    _lib.invoke("mk_hash_batch", _ptr(a), n, msg_len, _ptr(out))
     return out
 
 
@@ -56,8 +56,7 @@ def hash_batch_var(msgs: Sequence[bytes]) -> List[bytes]:
         return []
     data, offs = _flatten(msgs)
     out = np.empty((len(msgs), 32), dtype=np.uint8)
-    _lib.check(_lib.load().mk_hash_batch_var(_ptr(data), _ptr(offs), len(msgs), _ptr(out)),
-               "mk_hash_batch_var")
+    _lib.invoke("mk_hash_batch_var", _ptr(data), _ptr(offs), len(msgs), _ptr(out))
     return [bytes(r) for r in out]
 
 
@@ -76,7 +75,7 @@ def MerkleRoot(values: List[bytes]) -> bytes:
     data, offs = _flatten(values)
     leaves = np.empty((n, 32), dtype=np.uint8)
     out = ctypes.create_string_buffer(32)
-    _lib.check(_lib.load().mk_merkle_root(_ptr(data), _ptr(offs), n, _ptr(leaves), out), "mk_merkle_root")
+    _lib.invoke("mk_merkle_root", _ptr(data), _ptr(offs), n, _ptr(leaves), out)
     for i in range(n):
         values[i] = bytes(leaves[i])
     return out.raw

@@ -119,6 +119,10 @@ def sharded_merkle_hash(local_items: torch.Tensor, n_total: int, item_len: int, 
             fin = lambda: finish_fn(gather_buf, sp.nonempty, n_total)  # noqa: E731
         if finish_stream is not None:
             finish_stream.wait_stream(torch.cuda.current_stream(dev))
+            # the finisher reads gather_buf on finish_stream after this call
+            # returns: keep the caching allocator from handing its block to the
+            # next allocation on the current stream meanwhile
+            gather_buf.record_stream(finish_stream)
             with torch.cuda.stream(finish_stream):
                 return fin()
         return fin()

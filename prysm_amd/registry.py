@@ -62,8 +62,7 @@ def struct_roots(records: np.ndarray, spec=VALIDATOR_FIELDS) -> np.ndarray:
     raw = rec.view(np.uint8).reshape(-1)
     out = np.empty((n, 32), dtype=np.uint8)
     f = _fields(spec)
-    _lib.check(_lib.load().mk_ssz_struct_roots(_ptr(raw), n, rec.dtype.itemsize, f, len(spec), _ptr(out)),
-               "mk_ssz_struct_roots")
+    _lib.invoke("mk_ssz_struct_roots", _ptr(raw), n, rec.dtype.itemsize, f, len(spec), _ptr(out))
     return out
 
 
@@ -73,8 +72,8 @@ def struct_list_root(records: np.ndarray, spec=VALIDATOR_FIELDS) -> bytes:
     raw = rec.view(np.uint8).reshape(-1)
     out = ctypes.create_string_buffer(32)
     f = _fields(spec)
-    _lib.check(_lib.load().mk_ssz_struct_list_root(_ptr(raw) if raw.size else None, len(rec), rec.dtype.itemsize,
-                                                   f, len(spec), out), "mk_ssz_struct_list_root")
+    _lib.invoke("mk_ssz_struct_list_root", _ptr(raw) if raw.size else None, len(rec), rec.dtype.itemsize, f,
+                len(spec), out)
     return out.raw
 
 

@@ -15,10 +15,11 @@ Reference (file:line under the reference root):
 Go's reflection is replaced by explicit type descriptors (``Uint(16)``,
 ``Slice(T)``, ``Struct("ssz.simpleStruct", [("B", Uint(16)), ...])`` ...).
 Evaluation is breadth-first and batched: all elements of a list are hashed
-by one GPU launch per nesting level (bytes fields -> one variable-length
-Keccak batch, struct concatenations -> one batch, list roots -> the fused
-merkleHash kernels), instead of one Keccak call per field as in the
-reference's recursive hasher.  Errors carry the reference's exact text.
+by one library call per nesting level (bytes fields -> one variable-length
+Keccak batch, struct concatenations -> one batch, all lists of a nesting
+level -> one segmented merkleHash call, mk_ssz_merkle_many), instead of one
+Keccak call per field as in the reference's recursive hasher.  Errors carry
+the reference's exact text.
 """
 from __future__ import annotations
 
@@ -196,20 +197,20 @@ def _hash_many(t: SSZType, vals: Sequence, memo: dict) -> List[bytes]:
         concat = [b"".join(col[i] for col in cols) for i in range(n)]
         return hash_batch_var(concat)
     if isinstance(t, (Slice, Array)):
-        lens = [len(v) for v in vals]
+        # every list of this nesting level in one library call (mk_ssz_merkle_many)
         if isinstance(t.elem, (Bool, Uint)):
-            roots = []
-            for v in vals:
-                enc = _scalar_bytes(t.elem, v)
-                roots.append(merkle_hash_flat(enc, len(enc), enc.shape[1] if len(enc) else 1))
-            return roots
+            encs = [_scalar_bytes(t.elem, v) for v in vals]
+            size = 1 if isinstance(t.elem, Bool) else t.elem.bits // 8
+            return merkle_many([e.reshape(-1) for e in encs], [len(e) for e in encs], size)
+        lens = [len(v) for v in vals]
         flat = [e for v in vals for e in v]
         hs = _hash_many(t.elem, flat, memo)
-        out, pos = [], 0
+        size = len(hs[0]) if hs else 32
+        bufs, pos = [], 0
         for L in lens:
-            out.append(merkle_hash(hs[pos:pos + L]))
+            bufs.append(np.frombuffer(b"".join(hs[pos:pos + L]), dtype=np.uint8))
             pos += L
-        return out
+        return merkle_many(bufs, lens, size)
     raise HashError(f"type {t.go_name} is not hashable")
 
 
@@ -219,12 +220,37 @@ def merkle_hash_flat(items: np.ndarray, n: int, item_len: int) -> bytes:
     a = np.ascontiguousarray(items, dtype=np.uint8).reshape(-1)
     if a.size < n * item_len:
         raise ValueError("items buffer shorter than n*item_len")
-    out = ctypes.create_string_buffer(32)
-    rc = _lib.load().mk_ssz_merkle_hash(_ptr(a) if a.size else None, n, item_len, out)
-    if rc == _lib.MK_EINVAL and n and item_len == 0:
+    if n and item_len == 0:
         raise ZeroDivisionError("integer divide by zero")  # hash.go:207 panics
-    _lib.check(rc, "mk_ssz_merkle_hash")
+    out = ctypes.create_string_buffer(32)
+    _lib.invoke("mk_ssz_merkle_hash", _ptr(a) if a.size else None, n, item_len, out)
     return out.raw
+
+
+def merkle_many(lists: Sequence[np.ndarray], ns: Sequence[int], item_len: int) -> List[bytes]:
+    """merkleHash of every list (lists[i]: ns[i] items of item_len bytes) in
+    one library call: all lists' windows in one launch, one launch per level."""
+    k = len(lists)
+    if k == 0:
+        return []
+    if item_len == 0 and any(ns):
+        raise ZeroDivisionError("integer divide by zero")
+    offs = np.zeros(k, dtype=np.uint64)
+    parts, pos = [], 0
+    for i, a in enumerate(lists):
+        pad = (-pos) % 16  # 16-B aligned lists take the streaming window path
+        if pad:
+            parts.append(np.zeros(pad, np.uint8))
+            pos += pad
+        offs[i] = pos
+        parts.append(np.ascontiguousarray(a, dtype=np.uint8).reshape(-1))
+        pos += parts[-1].size
+    buf = np.concatenate(parts) if pos else np.zeros(16, np.uint8)
+    n = np.ascontiguousarray(ns, dtype=np.uint64)
+    il = np.full(k, max(item_len, 1), dtype=np.uint32)
+    out = np.empty((k, 32), dtype=np.uint8)
+    _lib.invoke("mk_ssz_merkle_many", _ptr(buf), _ptr(offs), _ptr(n), _ptr(il), k, _ptr(out))
+    return [bytes(r) for r in out]
 
 
 def merkle_hash(lst: Sequence[bytes]) -> bytes:

@@ -3,14 +3,18 @@ HIP engine.
 
 Reference: shared/trieutil/deposit_trie.go:13-81, depth 32 from
 shared/params/config.go:109.  ``DepositTrie`` keeps the reference's
-incremental API (UpdateDepositTrie / GenerateMerkleBranch / Root) but never
-hashes one deposit at a time: updates are queued and the trie is rebuilt by
-one batched GPU build (leaf Keccak batch + one launch per level) the next
-time it is read.  The batch build equals n incremental updates because every
-internal node's last recomputation happens when its rightmost leaf is
-inserted, at which point its subtree is final; tests check
-this against a literal dict restatement.  Empty nodes are 0^32 (Go map
-miss), the root of an empty trie is 0^32.
+incremental API (UpdateDepositTrie / GenerateMerkleBranch / Root) over a
+device-resident trie handle (``mk_deposit_trie_*``): every level stays in
+HBM, and the deposits queued by UpdateDepositTrie are appended at the next
+read by one library call that hashes the new leaves and recomputes only the
+right edge of each level (<= k/2^d + 2 nodes at level d for k new
+deposits).  The live caller, powchain's ``saveInTrie``
+(beacon-chain/powchain/service.go:379-386), reads Root() before every
+update, so each log costs one leaf hash plus ``depth`` node hashes — the
+reference's own O(depth) per deposit — instead of a rebuild.  A batch of
+updates followed by one read is the batch build (leaf batch + one launch per
+wide level).  Empty nodes are 0^32 (Go map miss); the root of an empty trie
+is 0^32.
 """
 from __future__ import annotations
 
@@ -32,13 +36,12 @@ def build_levels(deposits: Sequence[bytes], depth: int = DEPOSIT_CONTRACT_TREE_D
     n = len(deposits)
     root = ctypes.create_string_buffer(32)
     if n == 0:
-        _lib.check(_lib.load().mk_deposit_trie_build(None, None, 0, depth, None, root), "mk_deposit_trie_build")
+        _lib.invoke("mk_deposit_trie_build", None, None, 0, depth, None, root)
         return root.raw, []
     data, offs = _flatten(deposits)
     nbytes = _lib.load().mk_deposit_trie_levels_bytes(n, depth)
     lv = np.empty(nbytes, dtype=np.uint8)
-    _lib.check(_lib.load().mk_deposit_trie_build(_ptr(data), _ptr(offs), n, depth, _ptr(lv), root),
-               "mk_deposit_trie_build")
+    _lib.invoke("mk_deposit_trie_build", _ptr(data), _ptr(offs), n, depth, _ptr(lv), root)
     levels, pos, c = [], 0, n
     for _ in range(depth + 1):
         levels.append(lv[pos * 32:(pos + c) * 32].reshape(c, 32))
@@ -48,14 +51,23 @@ def build_levels(deposits: Sequence[bytes], depth: int = DEPOSIT_CONTRACT_TREE_D
 
 
 class DepositTrie:
-    """trieutil.DepositTrie (deposit_trie.go:13-16)."""
+    """trieutil.DepositTrie (deposit_trie.go:13-16) over a device trie handle."""
 
-    def __init__(self, depth: int = DEPOSIT_CONTRACT_TREE_DEPTH):
+    def __init__(self, depth: int = DEPOSIT_CONTRACT_TREE_DEPTH, capacity: int = 0, device: int = -1):
         self.depth = depth
         self.deposit_count = 0
-        self._deposits: List[bytes] = []
-        self._levels: Optional[list] = None
-        self._root = ZERO
+        self._queue: List[bytes] = []
+        self._handle: Optional[ctypes.c_void_p] = None
+        self._capacity = capacity
+        self._device = device
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None and _lib is not None:
+            try:
+                _lib.load().mk_deposit_trie_free(h)
+            except Exception:
+                pass
 
     # NewDepositTrie (deposit_trie.go:20-26)
     @classmethod
@@ -65,46 +77,63 @@ class DepositTrie:
     @classmethod
     def build(cls, deposits: Sequence[bytes], depth: int = DEPOSIT_CONTRACT_TREE_DEPTH) -> "DepositTrie":
         """Batch constructor: equals NewDepositTrie + UpdateDepositTrie for each."""
-        t = cls(depth)
-        t._deposits = [bytes(d) for d in deposits]
-        t.deposit_count = len(t._deposits)
+        t = cls(depth, capacity=len(deposits))
+        for d in deposits:
+            t.update_deposit_trie(d)
         return t
 
     def update_deposit_trie(self, deposit_data: bytes) -> None:
-        """UpdateDepositTrie (deposit_trie.go:29-40): deferred to one batch."""
-        self._deposits.append(bytes(deposit_data))
+        """UpdateDepositTrie (deposit_trie.go:29-40): queued, appended on the next read."""
+        self._queue.append(bytes(deposit_data))
         self.deposit_count += 1
-        self._levels = None
 
     UpdateDepositTrie = update_deposit_trie
 
-    def _sync(self):
-        if self._levels is None:
-            self._root, self._levels = build_levels(self._deposits, self.depth)
+    def _flush(self):
+        if not self._queue:
+            return
+        if self._handle is None:
+            h = ctypes.c_void_p()
+            _lib.invoke("mk_deposit_trie_new", self.depth, max(self._capacity, len(self._queue)), ctypes.byref(h),
+                        device=self._device)
+            self._handle = h
+        data, offs = _flatten(self._queue)
+        _lib.invoke("mk_deposit_trie_append", self._handle, _ptr(data), _ptr(offs), len(self._queue),
+                    device=self._device)
+        self._queue = []
 
     def generate_merkle_branch(self, index: int) -> List[bytes]:
         """GenerateMerkleBranch (deposit_trie.go:43-58): the sibling at each of
         the `depth` levels; missing nodes read as 0^32."""
-        self._sync()
-        out = []
-        for d in range(self.depth):
-            sib = (index >> d) ^ 1
-            lvl = self._levels[d] if d < len(self._levels) else None
-            out.append(bytes(lvl[sib]) if lvl is not None and sib < len(lvl) else ZERO)
-        return out
+        self._flush()
+        if self._handle is None:
+            return [ZERO] * self.depth
+        out = ctypes.create_string_buffer(32 * self.depth)
+        _lib.invoke("mk_deposit_trie_branch", self._handle, index, out, device=self._device)
+        raw = out.raw
+        return [raw[32 * d:32 * d + 32] for d in range(self.depth)]
 
     GenerateMerkleBranch = generate_merkle_branch
 
     def root(self) -> bytes:
         """Root (deposit_trie.go:61-63): node 1, 0^32 when empty."""
-        self._sync()
-        return self._root
+        self._flush()
+        if self._handle is None:
+            return ZERO
+        out = ctypes.create_string_buffer(32)
+        _lib.invoke("mk_deposit_trie_root", self._handle, out, device=self._device)
+        return out.raw
 
     Root = root
 
     def leaf(self, index: int) -> bytes:
-        self._sync()
-        return bytes(self._levels[0][index]) if self._levels and index < len(self._levels[0]) else ZERO
+        """Hash(deposit index) (the leaf the trie stores), 0^32 past the end."""
+        self._flush()
+        if self._handle is None or index >= self.deposit_count:
+            return ZERO
+        out = ctypes.create_string_buffer(32)
+        _lib.invoke("mk_deposit_trie_leaves", self._handle, index, 1, out, device=self._device)
+        return out.raw
 
 
 def verify_merkle_branches(leaves: Sequence[bytes], branches: Sequence[Sequence[bytes]], depth: int,
@@ -119,8 +148,7 @@ def verify_merkle_branches(leaves: Sequence[bytes], branches: Sequence[Sequence[
     br = np.frombuffer(b"".join(bytes(b[i]) for b in branches for i in range(depth)) or b"\0", dtype=np.uint8)
     idx = np.asarray(indices, dtype=np.uint64)
     ok = np.zeros(n, dtype=np.uint8)
-    _lib.check(_lib.load().mk_verify_merkle_branches(_ptr(lv), _ptr(br), _ptr(idx), n, depth, tree_depth,
-                                                     _ptr(rt), _ptr(ok)), "mk_verify_merkle_branches")
+    _lib.invoke("mk_verify_merkle_branches", _ptr(lv), _ptr(br), _ptr(idx), n, depth, tree_depth, _ptr(rt), _ptr(ok))
     return [bool(x) for x in ok]
 
 

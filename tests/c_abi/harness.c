@@ -1,0 +1,187 @@
+/*
+ * C-ABI harness: consumes include/prysm_merkle.h the way the cgo package
+ * gpu/merkle would (C99, no C++ or torch), links libprysm_merkle.so and calls
+ * the host-buffer entry points from NTHREADS pthreads at once.  Every thread
+ * checks its results against the committed fixture values passed on the
+ * command line (tests/golden/c_abi_fixture.json, made by
+ * tests/golden/make_c_abi_fixture.py with the CPU oracle), and checks that
+ * failures come back through the failing call's own mk_call context.
+ *
+ *   harness <threads> <rounds> <merkle_hex x8> <batch_hex x8> <trie_root_hex> <branch_hex> <many_hex x3>
+ *
+ * Inputs are SplitMix64 streams, identical to oracle/merkle_ref.c.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "prysm_merkle.h"
+
+#define NT_MAX 8
+#define SEED_BASE 0x5EED000000000700ull
+
+static uint64_t splitmix(uint64_t seed, uint64_t k) {
+    uint64_t z = seed + k * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* bytes [8*word0, 8*word0 + n) of the stream */
+static void fill(uint8_t* dst, size_t n, uint64_t seed, uint64_t word0) {
+    for (size_t i = 0; i < n; ++i) dst[i] = (uint8_t)(splitmix(seed, word0 + i / 8) >> (8 * (i % 8)));
+}
+
+static void hex(const uint8_t* b, char* out) {
+    for (int i = 0; i < 32; ++i) sprintf(out + 2 * i, "%02x", b[i]);
+}
+
+static const char* g_merkle[NT_MAX];
+static const char* g_batch[NT_MAX];
+static const char* g_trie_root;
+static const char* g_branch;
+static const char* g_many[3];
+static int g_rounds = 1;
+
+struct result {
+    int failures;
+    char msg[512];
+};
+
+#define CHECK(cond, ...)                                                     \
+    do {                                                                     \
+        if (!(cond)) {                                                       \
+            r->failures++;                                                   \
+            snprintf(r->msg, sizeof r->msg, __VA_ARGS__);                    \
+            return;                                                          \
+        }                                                                    \
+    } while (0)
+
+static int same(const uint8_t* got, const char* want) {
+    char h[65];
+    hex(got, h);
+    return strcmp(h, want) == 0;
+}
+
+static void run_once(int t, struct result* r) {
+    mk_call call;
+    uint8_t out[32];
+    call.device = -1;
+
+    /* ssz.merkleHash of 100003 + t items of 32 B */
+    const uint64_t n = 100003 + (uint64_t)t;
+    uint8_t* items = malloc(n * 32);
+    fill(items, n * 32, SEED_BASE + (uint64_t)t, 0);
+    int rc = mk_ssz_merkle_hash(&call, items, n, 32, out);
+    free(items);
+    CHECK(rc == MK_OK && call.code == MK_OK && call.err[0] == 0, "merkle rc %d: %s", rc, call.err);
+    CHECK(same(out, g_merkle[t]), "thread %d: merkle root mismatch", t);
+
+    /* hashutil.Hash batch of 1000 x 64 B, then Hash of the 32000 digest bytes */
+    uint8_t* msgs = malloc(1000 * 64);
+    uint8_t* dig = malloc(1000 * 32);
+    fill(msgs, 1000 * 64, SEED_BASE + 0x100 + (uint64_t)t, 0);
+    rc = mk_hash_batch(&call, msgs, 1000, 64, dig);
+    if (rc == MK_OK) rc = mk_hash(&call, dig, 1000 * 32, out);
+    free(msgs);
+    free(dig);
+    CHECK(rc == MK_OK, "hash rc %d: %s", rc, call.err);
+    CHECK(same(out, g_batch[t]), "thread %d: hash batch mismatch", t);
+
+    /* deposit trie handle: Root() before every UpdateDepositTrie (powchain saveInTrie) */
+    mk_trie* trie = NULL;
+    rc = mk_deposit_trie_new(&call, 32, 0, &trie);
+    CHECK(rc == MK_OK && trie, "trie_new rc %d: %s", rc, call.err);
+    uint8_t dep[280];
+    uint64_t offs[2] = {0, 280};
+    for (int i = 0; i < 300 && rc == MK_OK; ++i) {
+        rc = mk_deposit_trie_root(&call, trie, out);
+        fill(dep, 280, SEED_BASE + 0x200, 35 * (uint64_t)i);
+        if (rc == MK_OK) rc = mk_deposit_trie_append(&call, trie, dep, offs, 1);
+    }
+    uint8_t branch[32 * 32];
+    if (rc == MK_OK) rc = mk_deposit_trie_root(&call, trie, out);
+    int root_ok = rc == MK_OK && same(out, g_trie_root);
+    if (rc == MK_OK) rc = mk_deposit_trie_branch(&call, trie, 7, branch);
+    if (rc == MK_OK) rc = mk_hash(&call, branch, sizeof branch, out);
+    CHECK(mk_deposit_trie_count(trie) == 300, "trie count %llu", (unsigned long long)mk_deposit_trie_count(trie));
+    mk_deposit_trie_free(trie);
+    CHECK(rc == MK_OK, "trie rc %d: %s", rc, call.err);
+    CHECK(root_ok, "thread %d: trie root mismatch", t);
+    CHECK(same(out, g_branch), "thread %d: branch mismatch", t);
+
+    /* many lists in one call: 5 x 32 B, 1000 x 8 B, empty */
+    uint8_t* buf = malloc(160 + 8000);
+    fill(buf, 160 + 8000, SEED_BASE + 0x300, 0);
+    uint64_t moffs[3] = {0, 160, 0};
+    uint64_t mn[3] = {5, 1000, 0};
+    uint32_t mil[3] = {32, 8, 32};
+    uint8_t roots[3 * 32];
+    rc = mk_ssz_merkle_many(&call, buf, moffs, mn, mil, 3, roots);
+    free(buf);
+    CHECK(rc == MK_OK, "many rc %d: %s", rc, call.err);
+    for (int i = 0; i < 3; ++i) CHECK(same(roots + 32 * i, g_many[i]), "thread %d: many root %d mismatch", t, i);
+
+    /* failures travel with the call: item_len 0 (the reference's divide by zero) */
+    uint8_t one[64];
+    memset(one, 0, sizeof one);
+    rc = mk_ssz_merkle_hash(&call, one, 5, 0, out);
+    CHECK(rc == MK_EINVAL && call.code == MK_EINVAL && strstr(call.err, "divide by zero"),
+          "thread %d: item_len 0 gave rc %d '%s'", t, rc, call.err);
+    call.device = 1000 + t; /* a device that does not exist */
+    rc = mk_hash_batch(&call, one, 1, 64, out);
+    char want[64];
+    snprintf(want, sizeof want, "device %d out of range", 1000 + t);
+    CHECK(rc == MK_ENODEV && call.code == MK_ENODEV && strstr(call.err, want),
+          "thread %d: bad device gave rc %d '%s'", t, rc, call.err);
+    call.device = -1;
+    rc = mk_hash_batch(&call, one, 1, 64, out);
+    CHECK(rc == MK_OK && call.err[0] == 0, "thread %d: error detail leaked into the next call: '%s'", t, call.err);
+}
+
+struct arg {
+    int t;
+    struct result r;
+};
+
+static void* worker(void* p) {
+    struct arg* a = (struct arg*)p;
+    for (int k = 0; k < g_rounds && a->r.failures == 0; ++k) run_once(a->t, &a->r);
+    return NULL;
+}
+
+int main(int argc, char** argv) {
+    if (argc != 3 + NT_MAX + NT_MAX + 2 + 3) {
+        fprintf(stderr, "usage: %s threads rounds merkle x8 batch x8 trie_root branch many x3\n", argv[0]);
+        return 2;
+    }
+    int nt = atoi(argv[1]);
+    g_rounds = atoi(argv[2]);
+    if (nt < 1 || nt > NT_MAX) return 2;
+    for (int i = 0; i < NT_MAX; ++i) g_merkle[i] = argv[3 + i];
+    for (int i = 0; i < NT_MAX; ++i) g_batch[i] = argv[3 + NT_MAX + i];
+    g_trie_root = argv[3 + 2 * NT_MAX];
+    g_branch = argv[4 + 2 * NT_MAX];
+    for (int i = 0; i < 3; ++i) g_many[i] = argv[5 + 2 * NT_MAX + i];
+    printf("%s, %d visible gfx950 device(s)\n", mk_version(), mk_device_count());
+    pthread_t th[NT_MAX];
+    struct arg args[NT_MAX];
+    for (int t = 0; t < nt; ++t) {
+        args[t].t = t;
+        args[t].r.failures = 0;
+        args[t].r.msg[0] = 0;
+        if (pthread_create(&th[t], NULL, worker, &args[t]) != 0) return 3;
+    }
+    int bad = 0;
+    for (int t = 0; t < nt; ++t) {
+        pthread_join(th[t], NULL);
+        if (args[t].r.failures) {
+            fprintf(stderr, "thread %d FAILED: %s\n", t, args[t].r.msg);
+            bad = 1;
+        }
+    }
+    printf(bad ? "FAIL\n" : "ok: %d threads x %d rounds\n", nt, g_rounds);
+    return bad;
+}

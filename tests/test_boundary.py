@@ -46,7 +46,7 @@ def test_library_is_gfx950_code_object(lib):
 def _plan(lib, n, item_len, world):
     h, ne = ctypes.c_uint32(), ctypes.c_uint32()
     begin = (ctypes.c_uint64 * (world + 1))()
-    rc = lib.mk_ssz_merkle_shard_plan(n, item_len, world, ctypes.byref(h), ctypes.byref(ne), begin)
+    rc = lib.mk_ssz_merkle_shard_plan(None, n, item_len, world, ctypes.byref(h), ctypes.byref(ne), begin)
     return rc, h.value, ne.value, list(begin)
 
 
@@ -113,3 +113,31 @@ def test_oracle_is_not_imported_by_product():
                 txt = open(os.path.join(dp, f)).read()
                 assert "import oracle" not in txt and "from oracle" not in txt, f
                 assert "liboracle" not in txt, f
+
+
+def test_c99_harness_compiles_against_the_header(lib, tmp_path):
+    """The header is plain C99 (what cgo compiles): the pthread harness
+    builds with -std=c99 -Wall -Werror and links libprysm_merkle.so."""
+    import subprocess
+
+    src = os.path.join(ROOT, "tests", "c_abi", "harness.c")
+    libdir = os.path.join(ROOT, "prysm_amd", "lib")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-pedantic", "-I" + os.path.join(ROOT, "include"), src,
+                    "-L" + libdir, "-lprysm_merkle", "-lpthread", "-Wl,-rpath," + libdir,
+                    "-o", str(tmp_path / "harness")], check=True)
+
+
+def test_call_context_carries_errors_without_a_gpu(lib):
+    """Errors come back in the failing call's own mk_call (cgo may move a
+    goroutine between OS threads between two C calls)."""
+    call = _lib.Call(-1, 0, b"")
+    h, ne = ctypes.c_uint32(), ctypes.c_uint32()
+    begin = (ctypes.c_uint64 * 2)()
+    rc = lib.mk_ssz_merkle_shard_plan(ctypes.byref(call), 10, 32, 0, ctypes.byref(h), ctypes.byref(ne), begin)
+    assert rc == _lib.MK_EINVAL and call.code == rc and call.err == b"nshards == 0"
+    rc = lib.mk_ssz_merkle_shard_plan(ctypes.byref(call), 10, 32, 1, ctypes.byref(h), ctypes.byref(ne), begin)
+    assert rc == 0 and call.code == 0 and call.err == b""
+    if _lib.device_count() == 0:
+        out = ctypes.create_string_buffer(32)
+        rc = lib.mk_hash(ctypes.byref(call), b"abc", 3, out)
+        assert rc == _lib.MK_ENODEV and call.err == b"no gfx950 device visible"

@@ -173,7 +173,7 @@ def test_python_plan_matches_c_planner(n, item_len, world):
 
     h, ne = ctypes.c_uint32(), ctypes.c_uint32()
     begin = (ctypes.c_uint64 * (world + 1))()
-    assert _lib.load().mk_ssz_merkle_shard_plan(n, item_len, world, ctypes.byref(h), ctypes.byref(ne), begin) == 0
+    assert _lib.load().mk_ssz_merkle_shard_plan(None, n, item_len, world, ctypes.byref(h), ctypes.byref(ne), begin) == 0
     ph, pne, pbegin = _plan_cpu(n, item_len, world)
     assert (ne.value, list(begin)) == (pne, pbegin)
     if pne > 1:

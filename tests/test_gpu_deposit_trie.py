@@ -1,0 +1,154 @@
+"""GPU parity of the device-resident incremental deposit trie
+(mk_deposit_trie_* handle, mk_dev_deposit_trie_append/branch) against the
+literal dict restatement of shared/trieutil/deposit_trie.go:13-63
+(oracle.DictTrie) and the oracle's batch build."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED000000000000 + 500
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+
+    from prysm_amd import _lib
+
+    assert torch.cuda.is_available()
+    assert _lib.device_count() >= 1
+    return torch.device("cuda:0")
+
+
+def _deposit(i: int, ln: int = 280) -> bytes:
+    from oracle import oracle as O
+
+    return bytes(O.splitmix_bytes(ln, SEED, 35 * i))
+
+
+def test_read_root_then_update_2000(gpu):
+    """powchain saveInTrie (service.go:379-386): Root() before every
+    UpdateDepositTrie.  Each append recomputes the right edge only."""
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    t, ref = T.DepositTrie(), O.DictTrie()
+    rng = np.random.default_rng(5)
+    for i in range(2000):
+        assert t.Root() == ref.root(), i
+        d = _deposit(i)
+        t.UpdateDepositTrie(d)
+        ref.update(d)
+        if i % 173 == 0:
+            j = int(rng.integers(0, i + 1))
+            assert t.GenerateMerkleBranch(j) == ref.branch(j), (i, j)
+    assert t.Root() == ref.root()
+    assert t.deposit_count == 2000
+    for j in (0, 1, 1023, 1024, 1999):
+        br = t.GenerateMerkleBranch(j)
+        assert br == ref.branch(j)
+        assert T.VerifyMerkleBranch(O.keccak256(_deposit(j)), br, 32, j, t.Root())
+
+
+def test_variable_length_deposits_incremental(gpu):
+    """Deposits of different lengths (the var-length leaf kernel), appended in
+    uneven batches, past the initial capacity (1024) and a capacity doubling."""
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    t, ref = T.DepositTrie(), O.DictTrie()
+    i = 0
+    for batch in (1, 2, 5, 1, 100, 917, 1, 3000, 1):
+        for _ in range(batch):
+            d = _deposit(i, 1 + (i * 37) % 300)
+            t.UpdateDepositTrie(d)
+            ref.update(d)
+            i += 1
+        assert t.Root() == ref.root(), i
+    for j in (0, 7, 1024, i - 1):
+        assert t.GenerateMerkleBranch(j) == ref.branch(j)
+        assert t.leaf(j) == O.keccak256(_deposit(j, 1 + (j * 37) % 300))
+
+
+@pytest.mark.parametrize("batches", [(70_000,), (6_004, 70_000, 2), (1, 1, 1 << 17), ((1 << 17) + 5, 1023, 1024)])
+def test_append_batches_equal_batch_build(gpu, batches):
+    """Large appends take the wide-level path (k_trie_level on the right
+    edge) before the one-workgroup top; every state equals the batch build."""
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    t = T.DepositTrie()
+    deps = []
+    for b in batches:
+        new = [_deposit(len(deps) + k) for k in range(b)]
+        deps += new
+        for d in new:
+            t.UpdateDepositTrie(d)
+        root, levels = O.deposit_trie_levels(deps)
+        assert t.Root() == root, len(deps)
+        for j in sorted({0, len(deps) // 3, len(deps) - 1}):
+            want = [levels[d][(j >> d) ^ 1] if ((j >> d) ^ 1) < len(levels[d]) else bytes(32) for d in range(32)]
+            assert t.GenerateMerkleBranch(j) == want, (len(deps), j)
+
+
+@pytest.mark.parametrize("depth", [1, 2, 5, 20, 33, 63])
+def test_depths(gpu, depth):
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    n = min(1 << depth, 37)
+    t, ref = T.DepositTrie(depth), O.DictTrie(depth)
+    for i in range(n):
+        d = _deposit(i, 44)
+        t.UpdateDepositTrie(d)
+        ref.update(d)
+        if i % 5 == 0:
+            assert t.Root() == ref.root()
+    assert t.Root() == ref.root()
+    assert t.GenerateMerkleBranch(n - 1) == ref.branch(n - 1)
+
+
+def test_trie_full_is_an_error(gpu):
+    from prysm_amd import _lib
+    from prysm_amd import trieutil as T
+
+    t = T.DepositTrie(2)
+    for i in range(4):
+        t.UpdateDepositTrie(_deposit(i, 8))
+    assert len(t.Root()) == 32
+    t.UpdateDepositTrie(_deposit(4, 8))
+    with pytest.raises(_lib.MerkleError) as ei:
+        t.Root()
+    assert "do not fit a depth-2 trie" in str(ei.value)
+
+
+def test_dev_append_stream_of_blocks(gpu):
+    """mk_dev_deposit_trie_append on device-resident 280-B deposits (fixed
+    records, k_keccak_rec): blocks of deposits appended to one HBM trie;
+    root and branches after every block equal the batch build of the prefix."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    depth, cap, ln = 32, 1 << 16, 280
+    total = 40_000
+    data = torch.empty(total * ln, dtype=torch.uint8, device=gpu)
+    D.synth_fill(data, SEED + 7)
+    host = data.cpu().numpy()
+    levels = torch.zeros(D.deposit_trie_levels_bytes(cap, depth), dtype=torch.uint8, device=gpu)
+    root = torch.empty(32, dtype=torch.uint8, device=gpu)
+    count = 0
+    for k in (16, 1, 3000, 5, 1021, 1022, 17_000, 18_935):
+        D.deposit_trie_append(levels, cap, count, data[count * ln:(count + k) * ln], k, ln, depth, root)
+        count += k
+        deps = [bytes(host[i * ln:(i + 1) * ln]) for i in range(count)]
+        want_root, lv = O.deposit_trie_levels(deps)
+        br = D.deposit_trie_branch(levels, cap, count, depth, count - 1)
+        torch.cuda.synchronize()
+        assert bytes(root.cpu().numpy()) == want_root, count
+        want_br = b"".join(lv[d][((count - 1) >> d) ^ 1] if (((count - 1) >> d) ^ 1) < len(lv[d]) else bytes(32)
+                           for d in range(depth))
+        assert bytes(br.cpu().numpy()) == want_br, count
+    assert count == total

@@ -119,8 +119,8 @@ def test_c5_full_2p20_deposits(gpu):
     lv = torch.empty(L.mk_deposit_trie_levels_bytes(n, depth), dtype=torch.uint8, device=gpu)
     root = torch.empty(32, dtype=torch.uint8, device=gpu)
     st = ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream)
-    _lib.check(L.mk_dev_deposit_trie_build(ctypes.c_void_p(data.data_ptr()), None, n, dl, depth,
-                                           ctypes.c_void_p(lv.data_ptr()), ctypes.c_void_p(root.data_ptr()), st),
-               "mk_dev_deposit_trie_build")
+    _lib.check(L.mk_dev_deposit_trie_append(None, ctypes.c_void_p(lv.data_ptr()), n, 0, ctypes.c_void_p(data.data_ptr()),
+                                            None, n, dl, depth, ctypes.c_void_p(root.data_ptr()), st),
+               "mk_dev_deposit_trie_append")
     torch.cuda.synchronize()
     assert bytes(root.cpu().numpy()).hex() == g["root"]

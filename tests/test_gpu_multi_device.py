@@ -1,0 +1,163 @@
+"""GPU tests of the single-process multi-device entry points (the cgo
+caller's form) and of the per-call context (mk_call) the C
+ABI uses for device selection and error detail, plus the C99 pthread
+harness (tests/c_abi/harness.c) against committed fixtures."""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SEED = 0x5EED000000000000 + 650
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+
+    from prysm_amd import _lib
+
+    assert torch.cuda.is_available()
+    assert _lib.device_count() >= 1
+    return torch.device("cuda:0")
+
+
+def _multi_host(items: np.ndarray, n: int, item_len: int, devs):
+    from prysm_amd import _lib
+
+    out = ctypes.create_string_buffer(32)
+    arr = (ctypes.c_int * len(devs))(*devs)
+    _lib.invoke("mk_ssz_merkle_hash_multi", items.ctypes.data_as(ctypes.c_void_p), n, item_len, len(devs), arr, out)
+    return out.raw
+
+
+@pytest.mark.parametrize("n,nshards", [(12_345, 1), (1 << 20, 2), (1 << 20, 8), (999_999, 4), (5, 8),
+                                       ((1 << 22) + 7, 8), (100_003, 3)])
+def test_multi_shards_on_one_device(gpu, n, nshards):
+    """Every shard on device 0: per-device upload thread, pinned staging,
+    two alternating shard regions (upload of shard i+1 overlaps the passes of
+    shard i), frontier blocks gathered by copy, finisher on device 0."""
+    from oracle import oracle as O
+
+    items = O.splitmix_bytes(n * 32, SEED + nshards)
+    assert _multi_host(items, n, 32, [0] * nshards) == O.merkle_hash_flat(items, n, 32, nthreads=16)
+
+
+def test_multi_shards_item_sizes(gpu):
+    from oracle import oracle as O
+
+    for n, il, k in ((300_001, 8, 4), (77_777, 3, 2), (20_000, 200, 4)):
+        items = O.splitmix_bytes(n * il + 8, SEED + il)[:n * il]
+        assert _multi_host(items, n, il, [0] * k) == O.merkle_hash_flat(items, n, il, nthreads=16), (n, il)
+
+
+def test_multi_golden_2p26_eight_shards(gpu):
+    """2^26 x 32-B items (2 GiB host buffer) as 8 shards through the
+    host-buffer multi path; root vs the generator oracle."""
+    from oracle import oracle as O
+
+    n = 1 << 26
+    items = O.splitmix_bytes(n * 32, SEED + 26)
+    assert _multi_host(items, n, 32, [0] * 8) == O.merkle_hash_gen(n, 32, SEED + 26, nthreads=16)
+
+
+@pytest.mark.skipif("int(__import__('os').environ.get('MK_TEST_NDEV', '0')) < 2",
+                    reason="needs >= 2 GPUs (set MK_TEST_NDEV)")
+@pytest.mark.parametrize("ndev", [2, 4, 8])
+def test_multi_rccl_devices(gpu, ndev):
+    """One shard per device, RCCL all-gather of the frontiers (xGMI): the
+    golden-size C4 tree and a ragged n, host and device-resident forms."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import _lib
+    from prysm_amd import device as D
+
+    if _lib.device_count() < ndev:
+        pytest.skip(f"{_lib.device_count()} devices")
+    for n in (999_999, 1 << 24):
+        items = O.splitmix_bytes(n * 32, SEED + 77)
+        want = O.merkle_hash_flat(items, n, 32, nthreads=16)
+        assert _multi_host(items, n, 32, list(range(ndev))) == want
+        h, ne, begin = D.shard_plan(n, 32, ndev)
+        shards = [torch.from_numpy(items[begin[d] * 32:max(begin[d + 1], begin[d] + 1) * 32].copy()).to(f"cuda:{d}")
+                  for d in range(ndev)]
+        out = torch.empty(32, dtype=torch.uint8, device="cuda:0")
+        D.merkle_hash_multi(shards, n, 32, out)
+        for d in range(ndev):
+            torch.cuda.synchronize(d)
+        assert bytes(out.cpu().numpy()) == want
+
+
+def test_dev_multi_single_device(gpu):
+    """mk_dev_ssz_merkle_hash_multi with one device is the plain plan on the
+    caller's stream."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    n = 300_007
+    items = torch.empty(n * 32, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 5)
+    out = torch.empty(32, dtype=torch.uint8, device=gpu)
+    D.merkle_hash_multi([items], n, 32, out)
+    torch.cuda.synchronize()
+    assert bytes(out.cpu().numpy()) == O.merkle_hash_gen(n, 32, SEED + 5, nthreads=16)
+
+
+def test_call_context_errors_and_device_restore(gpu):
+    import torch
+
+    from prysm_amd import _lib
+
+    L = _lib.load()
+    call = _lib.Call(-1, 0, b"")
+    out = ctypes.create_string_buffer(32)
+    rc = L.mk_ssz_merkle_hash(ctypes.byref(call), None, 5, 0, out)
+    assert rc == _lib.MK_EINVAL and call.code == rc and b"divide by zero" in call.err
+    call = _lib.Call(77, 0, b"")
+    rc = L.mk_hash(ctypes.byref(call), b"abc", 3, out)
+    assert rc == _lib.MK_ENODEV and b"device 77 out of range" in call.err
+    # a device-resident call on a stream: the stream's device wins; a
+    # conflicting call->device is an error, not a silent retarget
+    if _lib.device_count() >= 2:
+        st = torch.cuda.Stream(device="cuda:1")
+        buf = torch.zeros(64, dtype=torch.uint8, device="cuda:1")
+        call = _lib.Call(0, 0, b"")
+        rc = L.mk_dev_hash_batch(ctypes.byref(call), buf.data_ptr(), 1, 64, buf.data_ptr(), st.cuda_stream)
+        assert rc == _lib.MK_EINVAL and b"stream belongs to device 1" in call.err
+    # the thread's current device is unchanged by a call that targets another one
+    cur = torch.cuda.current_device()
+    call = _lib.Call(_lib.device_count() - 1, 0, b"")
+    assert L.mk_hash(ctypes.byref(call), b"abc", 3, out) == 0
+    assert torch.cuda.current_device() == cur
+    assert out.raw.hex() == "4e03657aea45a94fc7d47ba826c8d667c0d1e6e33a64a036ec44f58fa12d6c45"
+
+
+def test_c_abi_harness_8_threads(gpu):
+    """tests/c_abi/harness.c (C99 against include/prysm_merkle.h, linked to
+    libprysm_merkle.so): 8 pthreads x 2 rounds of merkleHash, Hash batches,
+    the deposit-trie handle, many lists and per-call errors, vs fixtures."""
+    exe = _build_harness()
+    with open(os.path.join(ROOT, "tests", "golden", "c_abi_fixture.json")) as f:
+        fx = json.load(f)
+    args = [exe, "8", "2"] + fx["merkle"] + fx["batch"] + [fx["trie_root"], fx["branch"]] + fx["many"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok: 8 threads x 2 rounds" in r.stdout
+
+
+def _build_harness() -> str:
+    out = os.path.join(ROOT, "tests", "c_abi", "harness")
+    src = os.path.join(ROOT, "tests", "c_abi", "harness.c")
+    if not os.path.exists(out) or os.path.getmtime(out) < os.path.getmtime(src):
+        lib = os.path.join(ROOT, "prysm_amd", "lib")
+        subprocess.run(["gcc", "-std=c99", "-O2", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"), src,
+                        "-L" + lib, "-lprysm_merkle", "-lpthread", "-Wl,-rpath," + lib, "-o", out], check=True)
+    return out

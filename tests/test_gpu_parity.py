@@ -326,20 +326,6 @@ def test_finish_nodes_vs_reference_loop(gpu, count):
     assert bytes(got.cpu().numpy()) == want
 
 
-def test_multi_device_entry_single_gpu(gpu):
-    """mk_ssz_merkle_hash_multi with ndev=1 is the plain path."""
-    import ctypes
-
-    from oracle import oracle as O
-    from prysm_amd import _lib
-
-    n = 12345
-    items = O.splitmix_bytes(n * 32, SEED + 41)
-    out = ctypes.create_string_buffer(32)
-    _lib.check(_lib.load().mk_ssz_merkle_hash_multi(items.ctypes.data_as(ctypes.c_void_p), n, 32, 1, out))
-    assert out.raw == O.merkle_hash_flat(items, n, 32)
-
-
 # ------------------------------------------------------------------ TreeHash host mirror
 def test_tree_hash_reference_vectors(gpu, ref_vectors):
     from prysm_amd import ssz

@@ -115,30 +115,7 @@ def test_c_oracle_equals_pure_python_restatement():
         assert O.merkle_hash(lst) == _py_merkle_hash(lst)
 
 
-class _DictTrie:
-    """Literal restatement of shared/trieutil/deposit_trie.go:13-63."""
-
-    def __init__(self, depth=32):
-        self.depth, self.count, self.m = depth, 0, {}
-
-    def update(self, data):
-        idx = self.count + (1 << self.depth)
-        self.m[idx] = O.keccak256(data)
-        for _ in range(self.depth):
-            idx //= 2
-            self.m[idx] = O.keccak256(self.m.get(idx * 2, bytes(32)) + self.m.get(idx * 2 + 1, bytes(32)))
-        self.count += 1
-
-    def branch(self, index):
-        idx = index + (1 << self.depth)
-        out = []
-        for _ in range(self.depth):
-            out.append(self.m.get(idx - 1 if idx % 2 else idx + 1, bytes(32)))
-            idx //= 2
-        return out
-
-    def root(self):
-        return self.m.get(1, bytes(32))
+_DictTrie = O.DictTrie
 
 
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 5, 8, 13])

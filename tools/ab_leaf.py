@@ -60,7 +60,7 @@ def main():
     items = torch.empty(n * il, dtype=torch.uint8, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     first = libs[a.variants[0]]
-    assert first.mk_dev_synth_fill(ctypes.c_void_p(items.data_ptr()), n * il, 0x5EED000000000004, 0, st) == 0
+    assert first.mk_dev_synth_fill(None, ctypes.c_void_p(items.data_ptr()), n * il, 0x5EED000000000004, 0, st) == 0
     ws = torch.empty(max(L.mk_ssz_merkle_workspace_bytes(n, il) for L in libs.values()) + 4096, dtype=torch.uint8, device=dev)
     outs = {v: torch.empty(32, dtype=torch.uint8, device=dev) for v in a.variants}
     times = {v: [] for v in a.variants}
@@ -68,10 +68,10 @@ def main():
     for r in range(a.rounds + 1):
         for v, L in libs.items():
             L.mk_prof_enable(1)
-            L.mk_prof_read(None, None, None, None)
+            L.mk_prof_read(None, None, None, None, None)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            rc = L.mk_dev_ssz_merkle_hash(ctypes.c_void_p(items.data_ptr()), n, il,
+            rc = L.mk_dev_ssz_merkle_hash(None, ctypes.c_void_p(items.data_ptr()), n, il,
                                           ctypes.c_void_p(outs[v].data_ptr()), ctypes.c_void_p(ws.data_ptr()),
                                           ws.numel(), st)
             e1.record()
@@ -80,7 +80,7 @@ def main():
             ms = ctypes.c_double()
             cnt = ctypes.c_uint64()
             perms = ctypes.c_double()
-            L.mk_prof_read(ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(perms), None)
+            L.mk_prof_read(None, ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(perms), None)
             L.mk_prof_enable(0)
             if r:  # round 0 is warmup
                 times[v].append(e0.elapsed_time(e1))
@@ -102,7 +102,7 @@ def ab_trie(a, libs, dev):
     data = torch.empty(n * ln, dtype=torch.uint8, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     first = libs[a.variants[0]]
-    assert first.mk_dev_synth_fill(ctypes.c_void_p(data.data_ptr()), n * ln, 0x5EED000000000005, 0, st) == 0
+    assert first.mk_dev_synth_fill(None, ctypes.c_void_p(data.data_ptr()), n * ln, 0x5EED000000000005, 0, st) == 0
     lv = torch.empty(first.mk_deposit_trie_levels_bytes(n, depth), dtype=torch.uint8, device=dev)
     outs = {v: torch.empty(32, dtype=torch.uint8, device=dev) for v in a.variants}
     times = {v: [] for v in a.variants}
@@ -110,8 +110,9 @@ def ab_trie(a, libs, dev):
         for v, L in libs.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            rc = L.mk_dev_deposit_trie_build(ctypes.c_void_p(data.data_ptr()), None, n, ln, depth,
-                                             ctypes.c_void_p(lv.data_ptr()), ctypes.c_void_p(outs[v].data_ptr()), st)
+            rc = L.mk_dev_deposit_trie_append(None, ctypes.c_void_p(lv.data_ptr()), n, 0,
+                                              ctypes.c_void_p(data.data_ptr()), None, n, ln, depth,
+                                              ctypes.c_void_p(outs[v].data_ptr()), st)
             e1.record()
             torch.cuda.synchronize()
             assert rc == 0, (v, rc)
@@ -145,7 +146,7 @@ def ab_struct(a, libs, dev):
         for v, L in libs.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            rc = L.mk_dev_ssz_struct_list_root(ctypes.c_void_p(rec.data_ptr()), n, 160, spec, nf,
+            rc = L.mk_dev_ssz_struct_list_root(None, ctypes.c_void_p(rec.data_ptr()), n, 160, spec, nf,
                                                ctypes.c_void_p(outs[v].data_ptr()), ctypes.c_void_p(ws.data_ptr()),
                                                ws.numel(), st)
             e1.record()
@@ -169,14 +170,14 @@ def ab_c2(a, libs, dev):
     msgs = torch.empty(n * 64, dtype=torch.uint8, device=dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     first = libs[a.variants[0]]
-    assert first.mk_dev_synth_fill(ctypes.c_void_p(msgs.data_ptr()), n * 64, 0x5EED000000000002, 0, st) == 0
+    assert first.mk_dev_synth_fill(None, ctypes.c_void_p(msgs.data_ptr()), n * 64, 0x5EED000000000002, 0, st) == 0
     outs = {v: torch.empty(n * 32, dtype=torch.uint8, device=dev) for v in a.variants}
     times = {v: [] for v in a.variants}
     for r in range(a.rounds + 1):
         for v, L in libs.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            rc = L.mk_dev_hash_batch(ctypes.c_void_p(msgs.data_ptr()), n, 64, ctypes.c_void_p(outs[v].data_ptr()), st)
+            rc = L.mk_dev_hash_batch(None, ctypes.c_void_p(msgs.data_ptr()), n, 64, ctypes.c_void_p(outs[v].data_ptr()), st)
             e1.record()
             torch.cuda.synchronize()
             assert rc == 0, (v, rc)
@@ -209,7 +210,7 @@ def ab_host_struct(a, libs):
         for v, L in libs.items():
             out = ctypes.create_string_buffer(32)
             t0 = time.perf_counter()
-            rc = L.mk_ssz_struct_list_root(raw.ctypes.data_as(ctypes.c_void_p), n, rec.dtype.itemsize, f,
+            rc = L.mk_ssz_struct_list_root(None, raw.ctypes.data_as(ctypes.c_void_p), n, rec.dtype.itemsize, f,
                                            len(R.VALIDATOR_FIELDS), out)
             dt = time.perf_counter() - t0
             assert rc == 0, (v, rc)

@@ -113,7 +113,7 @@ def run_config(args):
         msgs = torch.empty(n * 64, dtype=torch.uint8, device=dev)
         D.synth_fill(msgs, seed + 2)
         out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
-        sec = _timeit(lambda: _lib.check(L.mk_dev_hash_batch(P(msgs), n, 64, P(out), st()), "c2"),
+        sec = _timeit(lambda: _lib.check(L.mk_dev_hash_batch(None, P(msgs), n, 64, P(out), st()), "c2"),
                       args.steps, args.warmup)
         cpu = None
         if not args.no_cpu_baseline:
@@ -156,10 +156,10 @@ def run_config(args):
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 D.merkle_hash(dbal, n, 8, out=roots[32:], ws=bws)
-            _lib.check(L.mk_dev_ssz_struct_list_root(P(rec), n, 160, spec, nf, P(roots), P(ws), ws.numel(), st()),
+            _lib.check(L.mk_dev_ssz_struct_list_root(None, P(rec), n, 160, spec, nf, P(roots), P(ws), ws.numel(), st()),
                        "registry")
             cur.wait_stream(side)
-            _lib.check(L.mk_dev_hash_batch(P(roots), 1, 64, P(out), st()), "state")
+            _lib.check(L.mk_dev_hash_batch(None, P(roots), 1, 64, P(out), st()), "state")
 
         sec = _timeit(step, args.steps, args.warmup)
         got = bytes(out.cpu().numpy())
@@ -191,8 +191,8 @@ def run_config(args):
         D.synth_fill(data, seed + 5)
         lv = torch.empty(L.mk_deposit_trie_levels_bytes(n, depth), dtype=torch.uint8, device=dev)
         root = torch.empty(32, dtype=torch.uint8, device=dev)
-        sec = _timeit(lambda: _lib.check(L.mk_dev_deposit_trie_build(P(data), None, n, dl, depth, P(lv), P(root),
-                                                                     st()), "c5"), args.steps, args.warmup)
+        sec = _timeit(lambda: _lib.check(L.mk_dev_deposit_trie_append(None, P(lv), n, 0, P(data), None, n, dl, depth,
+                                                                      P(root), st()), "c5"), args.steps, args.warmup)
         perms = 3 * n + (n - 1) + (depth - 20)
         hashes = n + (n - 1) + (depth - 20)
         cpu = None

@@ -56,14 +56,14 @@ def main():
     hi = torch.cuda.Stream(device=dev, priority=-1)
 
     def registry(cur):
-        _lib.check(L.mk_dev_ssz_struct_list_root(P(rec), n, 160, spec, nf, P(roots), P(ws), ws.numel(),
+        _lib.check(L.mk_dev_ssz_struct_list_root(None, P(rec), n, 160, spec, nf, P(roots), P(ws), ws.numel(),
                                                  ctypes.c_void_p(cur.cuda_stream)), "registry")
 
     def balances():
         D.merkle_hash(dbal, n, 8, out=roots[32:], ws=bws)
 
     def final(cur):
-        _lib.check(L.mk_dev_hash_batch(P(roots), 1, 64, P(out), ctypes.c_void_p(cur.cuda_stream)), "state")
+        _lib.check(L.mk_dev_hash_batch(None, P(roots), 1, 64, P(out), ctypes.c_void_p(cur.cuda_stream)), "state")
 
     def make(kind):
         side = hi if kind.startswith("hi") else lo
