@@ -479,6 +479,7 @@ int dev_merkle_many(const void* d_items, const mk::ManyPlan& mp, uint32_t nlists
     auto* lists = (mk::ManyList*)(ws + mp.off_lists);
     auto* act = (mk::ManyAct*)(ws + mp.off_act);
     uint4* buf[2] = {(uint4*)(ws + mp.off_buf0), (uint4*)(ws + mp.off_buf1)};
+    uint4* tops = (uint4*)(ws + mp.off_tops);
     DevCtx* c = ctx();
     TRY(upload_small(c, lists, mp.lists.data(), sizeof(mk::ManyList) * nlists, st));
     TRY(upload_small(c, act, mp.act.data(), sizeof(mk::ManyAct) * mp.act.size(), st));
@@ -490,14 +491,14 @@ int dev_merkle_many(const void* d_items, const mk::ManyPlan& mp, uint32_t nlists
         const mk::ManyAct* a = act + mp.lvl_begin[l];
         if (l == 0)
             hipLaunchKernelGGL((mk::k_many_level<true>), dim3(ceil_div(nodes, 256)), dim3(256), 0, st, items, lists, a,
-                               nact, nodes, (const uint4*)nullptr, buf[0]);
+                               nact, nodes, (const uint4*)nullptr, buf[0], tops);
         else
             hipLaunchKernelGGL((mk::k_many_level<false>), dim3(ceil_div(nodes, 256)), dim3(256), 0, st, items, lists,
-                               a, nact, nodes, (const uint4*)buf[(l - 1) % 2], buf[l % 2]);
+                               a, nact, nodes, (const uint4*)buf[(l - 1) % 2], buf[l % 2], tops);
         HIPCHK(hipGetLastError());
     }
     hipLaunchKernelGGL(mk::k_many_final, dim3(ceil_div(nlists, 256)), dim3(256), 0, st, items, lists, nlists,
-                       (const uint4*)buf[0], (const uint4*)buf[1], (uint4*)d_roots);
+                       (const uint4*)tops, (uint4*)d_roots);
     HIPCHK(hipGetLastError());
     for (size_t b = 0; b < mp.big.size(); ++b) {  // big lists: their own fused plans, one shared workspace
         const mk::ManyList& L = mp.lists[mp.big[b]];

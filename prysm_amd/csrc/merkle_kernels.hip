@@ -1691,7 +1691,8 @@ template <bool LEAF>
 __global__ __launch_bounds__(256) void k_many_level(const uint8_t* __restrict__ items,
                                                     const ManyList* __restrict__ lists,
                                                     const ManyAct* __restrict__ act, uint32_t nact, uint64_t nodes,
-                                                    const uint4* __restrict__ in, uint4* __restrict__ out) {
+                                                    const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                    uint4* __restrict__ tops) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nodes) return;
     const ManyAct A = act[many_find(act, nact, t)];
@@ -1726,20 +1727,24 @@ __global__ __launch_bounds__(256) void k_many_level(const uint8_t* __restrict__ 
         }
         hash_pair(src[0], src[1], r0, r1, padded, d0, d1);
     }
-    out[2 * (A.out_first + j)] = d0;
-    out[2 * (A.out_first + j) + 1] = d1;
+    if (A.level == L.levels) {  // the list's top node (its only node at this level)
+        tops[2 * A.list] = d0;
+        tops[2 * A.list + 1] = d1;
+    } else {
+        out[2 * (A.out_first + j)] = d0;
+        out[2 * (A.out_first + j) + 1] = d1;
+    }
 }
 template __global__ void k_many_level<true>(const uint8_t*, const ManyList*, const ManyAct*, uint32_t, uint64_t,
-                                            const uint4*, uint4*);
+                                            const uint4*, uint4*, uint4*);
 template __global__ void k_many_level<false>(const uint8_t*, const ManyList*, const ManyAct*, uint32_t, uint64_t,
-                                             const uint4*, uint4*);
+                                             const uint4*, uint4*, uint4*);
 
 // Root of every list that is not a big list: K(top || le64(n) || 0^24), or
 // for <= 1 chunk K(bytes || [0^128 if n == 0] || le64(n) || 0^24).
 __global__ __launch_bounds__(256) void k_many_final(const uint8_t* __restrict__ items,
                                                     const ManyList* __restrict__ lists, uint32_t nlists,
-                                                    const uint4* __restrict__ buf0, const uint4* __restrict__ buf1,
-                                                    uint4* __restrict__ roots) {
+                                                    const uint4* __restrict__ tops, uint4* __restrict__ roots) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nlists) return;
     const ManyList L = lists[i];
@@ -1748,8 +1753,7 @@ __global__ __launch_bounds__(256) void k_many_final(const uint8_t* __restrict__ 
     if (L.levels == 0) {
         sponge_generic(items + L.items_off, L.total, L.n == 0 ? 128u : 0u, true, L.n, d0, d1);
     } else {
-        const uint4* b = ((L.levels - 1) & 1) ? buf1 : buf0;
-        hash_final(b[2 * L.root_pos], b[2 * L.root_pos + 1], L.n, d0, d1);
+        hash_final(tops[2 * i], tops[2 * i + 1], L.n, d0, d1);
     }
     roots[2 * i] = d0;
     roots[2 * i + 1] = d1;

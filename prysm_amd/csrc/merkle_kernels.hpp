@@ -65,9 +65,9 @@ __global__ void k_trie_branch(const uint4* levels, uint64_t cap, uint64_t count,
                               uint4* branch);
 template <bool LEAF>
 __global__ void k_many_level(const uint8_t* items, const ManyList* lists, const ManyAct* act, uint32_t nact,
-                             uint64_t nodes, const uint4* in, uint4* out);
-__global__ void k_many_final(const uint8_t* items, const ManyList* lists, uint32_t nlists, const uint4* buf0,
-                             const uint4* buf1, uint4* roots);
+                             uint64_t nodes, const uint4* in, uint4* out, uint4* tops);
+__global__ void k_many_final(const uint8_t* items, const ManyList* lists, uint32_t nlists, const uint4* tops,
+                             uint4* roots);
 __global__ void k_synth(uint64_t* dst, uint64_t nwords, uint64_t seed, uint64_t word0);
 
 }  // namespace mk

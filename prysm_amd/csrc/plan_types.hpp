@@ -44,7 +44,6 @@ struct ManyList {
     uint64_t cb;         // chunk bytes
     uint64_t nchunks;    // chunks
     uint64_t n;          // items (length mix-in)
-    uint64_t root_pos;   // node index of the list's top node in its last level's buffer
     uint64_t c1;         // level-1 node count (0: the list has <= 1 chunk)
     uint32_t levels;     // hashing levels above the chunks (0 for <= 1 chunk)
     uint32_t fast;       // 256-B contiguous windows (item_len | 128, 16-B aligned)

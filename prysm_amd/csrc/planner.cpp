@@ -335,7 +335,6 @@ int make_many_plan(const uint64_t* offs, const uint64_t* n, const uint32_t* item
             if (L.levels == UINT32_MAX || L.levels == 0 || L.levels < l) continue;
             mp.act.push_back(ManyAct{i, l, first, prev_first[i]});
             prev_first[i] = first;
-            if (L.levels == l) L.root_pos = first;
             first += ceil_div(L.c1, 1ull << (l - 1));
         }
         mp.lvl_begin.push_back(mp.act.size());
@@ -347,6 +346,8 @@ int make_many_plan(const uint64_t* offs, const uint64_t* n, const uint32_t* item
     off += align256(sizeof(ManyList) * std::max<uint64_t>(1, nlists));
     mp.off_act = off;
     off += align256(sizeof(ManyAct) * std::max<size_t>(1, mp.act.size()));
+    mp.off_tops = off;
+    off += align256(32 * std::max<uint64_t>(1, nlists));
     mp.off_buf0 = off;
     off += align256(32 * std::max<uint64_t>(1, mp.buf_nodes[0]));
     mp.off_buf1 = off;

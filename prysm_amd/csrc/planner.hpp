@@ -90,14 +90,15 @@ struct ManyPlan {
     uint32_t nlevels = 0;                // node levels of the segmented part (level 1 = windows)
     // act table of level l+1 (l = 0: windows) = act[lvl_begin[l], lvl_begin[l+1]):
     // the lists with nodes there, out_first = exclusive prefix sum of their
-    // node counts; level l+1 is written to buffer l % 2
+    // node counts; level l+1 is written to buffer l % 2, and a list's top
+    // node (its last level) also to tops[list] (the buffers are reused)
     std::vector<ManyAct> act;
     std::vector<uint64_t> lvl_begin;     // nlevels + 1
     std::vector<uint64_t> lvl_nodes;     // nodes computed at each level
     uint64_t buf_nodes[2] = {0, 0};      // capacity of the two level buffers
     uint64_t big_ws = 0;                 // max plan_ws_bytes of the big lists
     // workspace layout (bytes from the workspace start, 256-aligned)
-    uint64_t off_lists = 0, off_act = 0, off_buf0 = 0, off_buf1 = 0, off_big = 0;
+    uint64_t off_lists = 0, off_act = 0, off_tops = 0, off_buf0 = 0, off_buf1 = 0, off_big = 0;
     uint64_t ws_bytes = 0;
     double perms = 0;                    // algorithmic permutations of the whole call
 };

@@ -260,6 +260,10 @@ def deposit_trie_append(levels: torch.Tensor, capacity: int, count: int, data: t
     deposits: UpdateDepositTrie (deposit_trie.go:29-40) batched, right edge
     of every level only; count == 0 is the batch build."""
     dev = _dev(levels)
+    if offs is None and data.numel() < k * fixed_len:
+        raise ValueError(f"deposit buffer holds {data.numel()} bytes < {k} x {fixed_len}")
+    if levels.numel() < deposit_trie_levels_bytes(capacity, depth):
+        raise ValueError("level buffer smaller than mk_deposit_trie_levels_bytes(capacity, depth)")
     _lib.invoke("mk_dev_deposit_trie_append", _p(levels), capacity, count, _p(data),
                 _p(offs) if offs is not None else None, k, fixed_len, depth, _p(root), _stream(levels.device),
                 device=dev)

@@ -132,10 +132,7 @@ int main(int argc, char** argv) {
             }
             REQUIRE(expect == mp.lvl_nodes[l] && expect <= mp.buf_nodes[l % 2]);
         }
-        for (uint32_t i = 0; i < nl; ++i) {
-            const ManyList& L = mp.lists[i];
-            if (L.levels && L.levels != UINT32_MAX) REQUIRE(L.root_pos < mp.buf_nodes[(L.levels - 1) % 2]);
-        }
+        REQUIRE(mp.off_tops + 32 * nl <= mp.off_buf0);
         REQUIRE(mp.off_big + 256 <= mp.ws_bytes);
         std::printf("M %u %u %llu\n", nl, mp.nlevels, (unsigned long long)mp.ws_bytes);
         // deposit-trie layout: levels are disjoint and in order

@@ -133,7 +133,7 @@ def test_dev_append_stream_of_blocks(gpu):
     from prysm_amd import device as D
 
     depth, cap, ln = 32, 1 << 16, 280
-    total = 40_000
+    total = 41_000
     data = torch.empty(total * ln, dtype=torch.uint8, device=gpu)
     D.synth_fill(data, SEED + 7)
     host = data.cpu().numpy()
