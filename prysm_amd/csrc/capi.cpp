@@ -1180,7 +1180,8 @@ static int host_merkle_many(const uint8_t* items, const uint64_t* offs, const ui
     std::vector<uint64_t> rel(offs, offs + nlists);
     for (uint32_t i = 0; i < nlists; ++i) rel[i] = n[i] * (uint64_t)item_len[i] ? offs[i] - lo : 0;
     mk::ManyPlan mp;
-    TRY(mk::make_many_plan(rel.data(), n, item_len, nlists, hi - lo, ((uintptr_t)(items + lo) % 16) == 0, mp));
+    // the device copy starts 256-B aligned: a list is 16-B aligned there iff its offset is
+    TRY(mk::make_many_plan(rel.data(), n, item_len, nlists, hi - lo, true, mp));
     TRY(bind_call());
     DevCtx* c = ctx();
     std::lock_guard<std::mutex> lk(c->mu);

@@ -121,27 +121,81 @@ def state_root(registry: ValidatorRegistry, balances: np.ndarray) -> bytes:
 
 
 FAR_FUTURE_EPOCH = (1 << 64) - 1  # shared/params/config.go:118
+_GAMMA = np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix_words(seed: int, word0: int, count: int) -> np.ndarray:
+    """Words [word0, word0 + count) of the counter-based SplitMix64 stream of
+    SURVEY.md §8d (x = seed + k * 0x9E3779B97F4A7C15, standard mix) —
+    the same stream the device kernel k_synth writes (mk_dev_synth_fill)."""
+    with np.errstate(over="ignore"):
+        k = np.arange(word0, word0 + count, dtype=np.uint64)
+        z = np.uint64(seed & 0xFFFFFFFFFFFFFFFF) + k * _GAMMA
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _fix_records(w: np.ndarray, first: int = 0) -> np.ndarray:
+    """Validator records from raw SplitMix64 words (n x 20 u64, record i =
+    stream words 20i .. 20i+19): bytes fields keep the stream; the epochs are
+    masked or FarFutureEpoch by index rule; StatusFlags = i % 4."""
+    n = w.shape[0]
+    i = np.arange(first, first + n, dtype=np.uint64)
+    far = np.uint64(FAR_FUTURE_EPOCH)
+    w[:, 14] &= np.uint64((1 << 20) - 1)                                          # RandaoLayers
+    w[:, 15] &= np.uint64((1 << 30) - 1)                                          # ActivationEpoch
+    w[:, 16] = np.where(i % 3 == 0, w[:, 16] & np.uint64((1 << 30) - 1), far)     # ExitEpoch
+    w[:, 17] = far                                                                # WithdrawalEpoch
+    w[:, 18] = np.where(i % 5 == 0, np.uint64(7), far)                            # PenalizedEpoch
+    w[:, 19] = i % np.uint64(4)                                                   # StatusFlags
+    return w
 
 
 def synthetic_registry(n: int, seed: int) -> ValidatorRegistry:
-    """SURVEY.md §8d synthetic registry: PRNG bytes fields; epochs PRNG or
-    FarFutureEpoch; StatusFlags 0..3."""
-    rng = np.random.default_rng(seed & ((1 << 63) - 1))
-    rec = np.zeros(n, dtype=VALIDATOR_DTYPE)
-    rec["pubkey"] = rng.integers(0, 256, (n, 48), dtype=np.uint8)
-    rec["withdrawal_credentials_hash32"] = rng.integers(0, 256, (n, 32), dtype=np.uint8)
-    rec["randao_commitment_hash32"] = rng.integers(0, 256, (n, 32), dtype=np.uint8)
-    rec["randao_layers"] = rng.integers(0, 1 << 20, n, dtype=np.uint64)
-    rec["activation_epoch"] = rng.integers(0, 1 << 30, n, dtype=np.uint64)
-    far = np.uint64(FAR_FUTURE_EPOCH)
-    rec["exit_epoch"] = np.where(np.arange(n) % 3 == 0, rng.integers(0, 1 << 30, n, dtype=np.uint64), far)
-    rec["withdrawal_epoch"] = far
-    rec["penalized_epoch"] = np.where(np.arange(n) % 5 == 0, np.uint64(7), far)
-    rec["status_flags"] = np.arange(n, dtype=np.uint64) % 4
-    return ValidatorRegistry(rec)
+    """SURVEY.md §8d synthetic registry from the SplitMix64 stream (record i
+    = words 20i..20i+19 of the stream with `seed`, 160 B), so the same
+    registry can be generated on the device (synthetic_registry_device):
+    PRNG bytes fields; epochs PRNG or FarFutureEpoch; StatusFlags 0..3."""
+    w = _fix_records(splitmix_words(seed, 0, 20 * n).reshape(n, 20))
+    return ValidatorRegistry(w.astype("<u8").view(VALIDATOR_DTYPE).reshape(n))
 
 
 def synthetic_balances(n: int, seed: int) -> np.ndarray:
-    """32e9 Gwei +- PRNG."""
-    rng = np.random.default_rng((seed + 1) & ((1 << 63) - 1))
-    return (np.uint64(32 * 10**9) + rng.integers(0, 10**9, n, dtype=np.uint64) - np.uint64(5 * 10**8)).astype("<u8")
+    """31.5e9 Gwei + (PRNG mod 1e9) (32 ETH +- 0.5 ETH), from
+    the SplitMix64 stream with seed + 1."""
+    w = splitmix_words(seed + 1, 0, n)
+    return (np.uint64(31_500_000_000) + (w & np.uint64((1 << 30) - 1)) % np.uint64(10**9)).astype("<u8")
+
+
+def synthetic_registry_device(n: int, seed: int, device):
+    """The same records as synthetic_registry, generated in HBM (k_synth +
+    the index rules as torch integer ops): an (n*160,) uint8 tensor."""
+    import torch
+
+    from . import device as D
+
+    raw = torch.empty(n * 160, dtype=torch.uint8, device=device)
+    D.synth_fill(raw, seed)
+    w = raw.view(torch.int64).view(n, 20)
+    i = torch.arange(n, dtype=torch.int64, device=device)
+    far = torch.full_like(i, -1)  # 2^64 - 1
+    w[:, 14] &= (1 << 20) - 1
+    w[:, 15] &= (1 << 30) - 1
+    w[:, 16] = torch.where(i % 3 == 0, w[:, 16] & ((1 << 30) - 1), far)
+    w[:, 17] = far
+    w[:, 18] = torch.where(i % 5 == 0, torch.full_like(i, 7), far)
+    w[:, 19] = i % 4
+    return raw
+
+
+def synthetic_balances_device(n: int, seed: int, device):
+    import torch
+
+    from . import device as D
+
+    raw = torch.empty(n * 8, dtype=torch.uint8, device=device)
+    D.synth_fill(raw, seed + 1)
+    w = raw.view(torch.int64)
+    w.copy_(31_500_000_000 + (w & ((1 << 30) - 1)) % 1_000_000_000)
+    return raw

@@ -30,7 +30,7 @@ from typing import Any, Callable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from .hashutil import _flatten, _ptr, hash_batch_var
+from .hashutil import _flatten, _ptr, hash_batch, hash_batch_var
 
 SSZ_CHUNK_SIZE = 128  # hash.go:15
 HASH_LENGTH = 32  # hash.go:14
@@ -134,16 +134,39 @@ def _check_serializable(t: SSZType) -> Optional[str]:
     return f"type {t.go_name} is not serializable"
 
 
+def _trivial(t: SSZType) -> bool:
+    """True when no value of type t can make the hasher fail or call a
+    Hashable hook (no pointers, no Hashable): validation can skip it."""
+    tr = getattr(t, "_trivial", None)
+    if tr is None:
+        if isinstance(t, (Ptr, Hashable)):
+            tr = False
+        elif isinstance(t, (Slice, Array)):
+            tr = _trivial(t.elem)
+        elif isinstance(t, Struct):
+            tr = all(_trivial(ft) for _, ft in t.hashed_fields())
+        else:
+            tr = True
+        t._trivial = tr
+    return tr
+
+
 def _validate(t: SSZType, v, memo: dict) -> None:
     """Depth-first pass in the reference's evaluation order that raises the
     first error the recursive Go hasher would hit (nil pointers, Hashable
     errors), with the same nesting of messages.  Hashable results are
-    memoised so TreeHashSSZ runs once."""
+    memoised so TreeHashSSZ runs once.  Subtrees that cannot fail are
+    skipped; a list of pointers to such a type only checks for nil."""
+    if _trivial(t):
+        return
     if isinstance(t, Hashable):
         memo[id(v)] = bytes(t.fn(v))
         return
     if isinstance(t, (Slice, Array)):
-        if isinstance(v, np.ndarray) and isinstance(t.elem, (Bool, Uint)):
+        if isinstance(t.elem, Ptr) and _trivial(t.elem.elem):
+            for e in v:
+                if e is None:
+                    raise HashError("failed to hash element of slice/array: nil is not supported")
             return
         for e in v:
             try:
@@ -174,43 +197,73 @@ def _scalar_bytes(t: SSZType, vals) -> np.ndarray:
     return a.reshape(-1).view(np.uint8).reshape(-1, t.bits // 8)
 
 
-def _hash_many(t: SSZType, vals: Sequence, memo: dict) -> List[bytes]:
-    """Hash of every value in ``vals`` (all of type t), batched on the GPU."""
+def _hash_size(t: SSZType) -> int:
+    """Length of the hasher's output for type t (hash.go:56-82)."""
+    if isinstance(t, Bool):
+        return 1
+    if isinstance(t, Uint):
+        return t.bits // 8
+    if isinstance(t, Ptr):
+        return _hash_size(t.elem)
+    return 32
+
+
+def _column(vals: Sequence, name: str) -> list:
+    if vals and isinstance(vals[0], dict):
+        return [v[name] for v in vals]
+    return [_field(v, name) for v in vals]
+
+
+def _hash_bytes_values(vals: Sequence) -> np.ndarray:
+    """hashedEncoding of every value: Keccak(le32(len) || bytes) (hash.go:100-107,
+    encode.go:148-159), one batched call; equal lengths take the fixed-length
+    kernels."""
+    bs = [bytes(v) for v in vals]
+    L0 = len(bs[0])
+    if all(len(b) == L0 for b in bs):
+        msgs = np.empty((len(bs), 4 + L0), dtype=np.uint8)
+        msgs[:, :4] = np.frombuffer(_st.pack("<I", L0), dtype=np.uint8)
+        if L0:
+            msgs[:, 4:] = np.frombuffer(b"".join(bs), dtype=np.uint8).reshape(len(bs), L0)
+        return hash_batch(msgs, 4 + L0)
+    return np.frombuffer(b"".join(hash_batch_var([_st.pack("<I", len(b)) + b for b in bs])),
+                         dtype=np.uint8).reshape(len(bs), 32)
+
+
+def _hash_many(t: SSZType, vals: Sequence, memo: dict) -> np.ndarray:
+    """Hasher output of every value in ``vals`` (all of type t) as an
+    (n, size) uint8 matrix, batched on the GPU: one library call per
+    nesting level (bytes fields, struct messages, all lists of a level)."""
     n = len(vals)
+    size = _hash_size(t)
     if n == 0:
-        return []
+        return np.zeros((0, size), dtype=np.uint8)
     if isinstance(t, Hashable):
-        return [memo[id(v)] for v in vals]
+        return np.frombuffer(b"".join(memo[id(v)] for v in vals), dtype=np.uint8).reshape(n, 32)
     if isinstance(t, (Bool, Uint)):
-        enc = _scalar_bytes(t, vals)
-        return [bytes(r) for r in enc]
+        return _scalar_bytes(t, vals)
     if isinstance(t, (Bytes, ByteArray)):
-        msgs = []
-        for v in vals:
-            b = bytes(v)
-            msgs.append(_st.pack("<I", len(b)) + b)  # le32 length prefix (encode.go:148-159)
-        return hash_batch_var(msgs)
+        return _hash_bytes_values(vals)
     if isinstance(t, Ptr):
         return _hash_many(t.elem, vals, memo)
     if isinstance(t, Struct):
-        cols = [_hash_many(ft, [_field(v, name) for v in vals], memo) for name, ft in t.hashed_fields()]
-        concat = [b"".join(col[i] for col in cols) for i in range(n)]
-        return hash_batch_var(concat)
+        cols = [_hash_many(ft, _column(vals, name), memo) for name, ft in t.hashed_fields()]
+        if not cols:  # Keccak of the empty concatenation
+            return np.frombuffer(b"".join(hash_batch_var([b""] * n)), dtype=np.uint8).reshape(n, 32)
+        return hash_batch(np.ascontiguousarray(np.concatenate(cols, axis=1)), sum(c.shape[1] for c in cols))
     if isinstance(t, (Slice, Array)):
         # every list of this nesting level in one library call (mk_ssz_merkle_many)
         if isinstance(t.elem, (Bool, Uint)):
             encs = [_scalar_bytes(t.elem, v) for v in vals]
-            size = 1 if isinstance(t.elem, Bool) else t.elem.bits // 8
-            return merkle_many([e.reshape(-1) for e in encs], [len(e) for e in encs], size)
-        lens = [len(v) for v in vals]
-        flat = [e for v in vals for e in v]
-        hs = _hash_many(t.elem, flat, memo)
-        size = len(hs[0]) if hs else 32
-        bufs, pos = [], 0
-        for L in lens:
-            bufs.append(np.frombuffer(b"".join(hs[pos:pos + L]), dtype=np.uint8))
-            pos += L
-        return merkle_many(bufs, lens, size)
+            roots = merkle_many([e.reshape(-1) for e in encs], [len(e) for e in encs], _hash_size(t.elem))
+        else:
+            lens = [len(v) for v in vals]
+            flat = [e for v in vals for e in v]
+            hs = _hash_many(t.elem, flat, memo)  # the inner lists are consecutive rows
+            size = _hash_size(t.elem)
+            offs = np.cumsum([0] + lens[:-1], dtype=np.uint64) * np.uint64(size)
+            return merkle_many_flat(hs, offs, lens, size)
+        return np.frombuffer(b"".join(roots), dtype=np.uint8).reshape(n, 32)
     raise HashError(f"type {t.go_name} is not hashable")
 
 
@@ -246,11 +299,25 @@ def merkle_many(lists: Sequence[np.ndarray], ns: Sequence[int], item_len: int) -
         parts.append(np.ascontiguousarray(a, dtype=np.uint8).reshape(-1))
         pos += parts[-1].size
     buf = np.concatenate(parts) if pos else np.zeros(16, np.uint8)
+    return [bytes(r) for r in merkle_many_flat(buf, offs, ns, item_len)]
+
+
+def merkle_many_flat(buf: np.ndarray, offs, ns, item_len: int) -> np.ndarray:
+    """merkleHash of list i = ns[i] items of item_len bytes at byte offset
+    offs[i] of ``buf`` (one mk_ssz_merkle_many call): (k, 32) roots."""
+    k = len(ns)
+    if item_len == 0 and any(ns):
+        raise ZeroDivisionError("integer divide by zero")
+    buf = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    if buf.size == 0:
+        buf = np.zeros(16, np.uint8)
+    o = np.ascontiguousarray(offs, dtype=np.uint64)
     n = np.ascontiguousarray(ns, dtype=np.uint64)
     il = np.full(k, max(item_len, 1), dtype=np.uint32)
     out = np.empty((k, 32), dtype=np.uint8)
-    _lib.invoke("mk_ssz_merkle_many", _ptr(buf), _ptr(offs), _ptr(n), _ptr(il), k, _ptr(out))
-    return [bytes(r) for r in out]
+    if k:
+        _lib.invoke("mk_ssz_merkle_many", _ptr(buf), _ptr(o), _ptr(n), _ptr(il), k, _ptr(out))
+    return out
 
 
 def merkle_hash(lst: Sequence[bytes]) -> bytes:
@@ -297,5 +364,5 @@ def tree_hash(val: Any, typ: Optional[SSZType]) -> bytes:
         _validate(typ, val, memo)
     except HashError as err:
         raise HashError(f"hash error: {err} for input type {typ.go_name}")
-    out = _hash_many(typ, [val], memo)[0]
+    out = bytes(_hash_many(typ, [val], memo)[0])
     return (out + bytes(32))[:32]  # bytesutil.ToBytes32

@@ -9,9 +9,13 @@ restatement_vectors.json; the oracle is pinned by reference_vectors.json).
   c3: TreeHash of State{1,000,000 synthetic validators, balances}
   c4: merkleHash of 2^28 x 32-B SplitMix64 items (the headline tree)
   c5: depth-32 deposit trie root of 2^20 x 280-B SplitMix64 deposits
+  c3_state: TreeHash of the synthetic pb.BeaconState of prysm_amd/state.py
+      with 1,000,000 validators (oracle/ssz_ref.py's reflective restatement,
+      the registry root from the C oracle's struct roots + merkleHash)
 
-Run:  python tests/golden/make_full_size.py   (C oracle, all host cores;
-about a minute on 8 cores).
+Run:  python tests/golden/make_full_size.py [c2,c3,c3_state,c4,c5]
+(C oracle, all host cores; about a minute on 8 cores; named configs are
+recomputed and merged into the existing file).
 """
 from __future__ import annotations
 
@@ -31,43 +35,84 @@ from oracle import oracle as O  # noqa: E402
 SEED = 0x5EED000000000000  # seed = 0x5EED.. + config id
 
 
-def main():
+def c3_state(nt):
+    from oracle import ssz_ref as OS
+    from prysm_amd import registry as R
+    from prysm_amd import state as ST
+    from tests.ssz_types import to_ref_type
+
+    n, seed = 1_000_000, SEED + 3
+    st = ST.synthetic_state(n, seed)
+    roots = O.struct_roots(st.registry.records.view(np.uint8).reshape(-1), n, 160, R.VALIDATOR_FIELDS, nthreads=nt)
+    reg_root = O.merkle_hash_flat(roots.reshape(-1), n, 32, nthreads=nt)
+    small = ST.synthetic_state(0, seed)  # everything but the 1M-entry lists, as a reflective value
+    small.balances = st.balances
+    small.attestations, small.scalars = st.attestations, st.scalars
+    for f in ("randao_mixes", "seeds", "crosslink_epochs", "crosslink_roots", "latest_block_roots",
+              "batched_block_roots", "penalized_balances", "index_roots", "eth1_data", "eth1_votes",
+              "eth1_vote_counts", "fork"):
+        setattr(small, f, getattr(st, f))
+    val = small.as_value()
+    val["ValidatorRegistry"] = "precomputed"
+    t = to_ref_type(ST.STATE_SSZ)
+    fields = [(name, ("hashable", "ValidatorRegistry", lambda _v: reg_root) if name == "ValidatorRegistry" else ft)
+              for name, ft in t[2]]
+    root = OS.tree_hash(("struct", t[1], fields), val)
+    return {"n": n, "seed": seed, "registry_root": reg_root.hex(), "state_root": root.hex(),
+            "shape": "prysm_amd/state.py synthetic_state defaults (8192-entry arrays, 1024 crosslinks, "
+                     "128 attestations, 16 batched roots, 4 eth1 votes)"}
+
+
+def main(only=None):
     nt = os.cpu_count() or 1
+    path = os.path.join(HERE, "full_size_roots.json")
     out = {"_generated_by": "tests/golden/make_full_size.py", "_oracle": "oracle/*.c (CPU restatement)"}
+    if only and os.path.exists(path):
+        with open(path) as f:
+            out = json.load(f)
+    want = lambda c: not only or c in only  # noqa: E731
     t0 = time.time()
 
-    n = 1 << 24
-    msgs = O.splitmix_bytes(n * 64, SEED + 2)
-    dig = O.keccak256_batch(msgs, 64, nthreads=nt)
-    out["c2"] = {"n": n, "msg_len": 64, "seed": SEED + 2, "digest_of_digests": O.keccak256(dig.tobytes()).hex()}
-    del msgs, dig
+    if want("c2"):
+        n = 1 << 24
+        msgs = O.splitmix_bytes(n * 64, SEED + 2)
+        dig = O.keccak256_batch(msgs, 64, nthreads=nt)
+        out["c2"] = {"n": n, "msg_len": 64, "seed": SEED + 2, "digest_of_digests": O.keccak256(dig.tobytes()).hex()}
+        del msgs, dig
 
-    from prysm_amd import registry as R
+    if want("c3"):
+        from prysm_amd import registry as R
 
-    n = 1_000_000
-    reg = R.synthetic_registry(n, SEED + 3)
-    bal = R.synthetic_balances(n, SEED + 3)
-    roots = O.struct_roots(reg.records.view(np.uint8).reshape(-1), n, 160, R.VALIDATOR_FIELDS, nthreads=nt)
-    reg_root = O.merkle_hash_flat(roots.reshape(-1), n, 32, nthreads=nt)
-    bal_root = O.merkle_hash_flat(bal.view(np.uint8), n, 8, nthreads=nt)
-    out["c3"] = {"n": n, "seed": SEED + 3, "registry_root": reg_root.hex(), "balances_root": bal_root.hex(),
-                 "state_root": O.keccak256(reg_root + bal_root).hex()}
+        n = 1_000_000
+        reg = R.synthetic_registry(n, SEED + 3)
+        bal = R.synthetic_balances(n, SEED + 3)
+        roots = O.struct_roots(reg.records.view(np.uint8).reshape(-1), n, 160, R.VALIDATOR_FIELDS, nthreads=nt)
+        reg_root = O.merkle_hash_flat(roots.reshape(-1), n, 32, nthreads=nt)
+        bal_root = O.merkle_hash_flat(bal.view(np.uint8), n, 8, nthreads=nt)
+        out["c3"] = {"n": n, "seed": SEED + 3, "registry_root": reg_root.hex(), "balances_root": bal_root.hex(),
+                     "state_root": O.keccak256(reg_root + bal_root).hex(),
+                     "generator": "registry.synthetic_registry / synthetic_balances (SplitMix64 stream)"}
 
-    n = 1 << 28
-    out["c4"] = {"n": n, "item_len": 32, "seed": SEED + 4,
-                 "root": O.merkle_hash_gen(n, 32, SEED + 4, nthreads=nt).hex()}
+    if want("c3_state"):
+        out["c3_state"] = c3_state(nt)
 
-    n, dl = 1 << 20, 280
-    host = O.splitmix_bytes(n * dl, SEED + 5)
-    deps = [host[i * dl:(i + 1) * dl].tobytes() for i in range(n)]
-    root, _ = O.deposit_trie_levels(deps)
-    out["c5"] = {"n": n, "deposit_len": dl, "seed": SEED + 5, "depth": 32, "root": bytes(root).hex()}
+    if want("c4"):
+        n = 1 << 28
+        out["c4"] = {"n": n, "item_len": 32, "seed": SEED + 4,
+                     "root": O.merkle_hash_gen(n, 32, SEED + 4, nthreads=nt).hex()}
 
-    with open(os.path.join(HERE, "full_size_roots.json"), "w") as f:
+    if want("c5"):
+        n, dl = 1 << 20, 280
+        host = O.splitmix_bytes(n * dl, SEED + 5)
+        deps = [host[i * dl:(i + 1) * dl].tobytes() for i in range(n)]
+        root, _ = O.deposit_trie_levels(deps)
+        out["c5"] = {"n": n, "deposit_len": dl, "seed": SEED + 5, "depth": 32, "root": bytes(root).hex()}
+
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
         f.write("\n")
     print(f"wrote full_size_roots.json in {time.time() - t0:.0f} s")
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1].split(",") if len(sys.argv) > 1 else None)

@@ -81,3 +81,26 @@ def validator_registry(n, seed):
     ssz_fields = [(n, S.Bytes() if k == "bytes" else S.Uint(64)) for n, k in VALIDATOR_FIELDS]
     t_ssz = S.Slice(S.Ptr(S.Struct("ssz.ValidatorRecord", ssz_fields)))
     return t_ref, t_ssz, vals
+
+
+def to_ref_type(t):
+    """prysm_amd.ssz descriptor -> oracle/ssz_ref type tuple (inverse of to_ssz_type)."""
+    if isinstance(t, S.Bool):
+        return ("bool",)
+    if isinstance(t, S.Uint):
+        return ("uint", t.bits)
+    if isinstance(t, S.Bytes):
+        return ("bytes",)
+    if isinstance(t, S.ByteArray):
+        return ("bytearray", t.n)
+    if isinstance(t, S.Slice):
+        return ("slice", to_ref_type(t.elem))
+    if isinstance(t, S.Array):
+        return ("array", to_ref_type(t.elem), t.n)
+    if isinstance(t, S.Struct):
+        return ("struct", t.go_name, [(n, to_ref_type(ft)) for n, ft in t.fields])
+    if isinstance(t, S.Ptr):
+        return ("ptr", to_ref_type(t.elem))
+    if isinstance(t, S.Hashable):
+        return ("hashable", t.go_name, t.fn)
+    return ("string",)
