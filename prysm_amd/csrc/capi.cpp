@@ -38,6 +38,10 @@ constexpr bool kRecKernel = MK_REC_KERNEL != 0;  // k_keccak_rec<35> for 280-B d
 #define MK_STRUCT_FUSED 1
 #endif
 constexpr bool kStructFused = MK_STRUCT_FUSED != 0;  // k_struct_fused instead of fields + message kernels
+#ifndef MK_STRUCT_REG
+#define MK_STRUCT_REG 1
+#endif
+constexpr bool kStructReg = MK_STRUCT_REG != 0;  // k_struct_reg<NB, NRAW> for bytes-then-u64 layouts
 #ifndef MK_TRIE_TOP_MAX_LOG2
 #define MK_TRIE_TOP_MAX_LOG2 17
 #endif
@@ -555,6 +559,26 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
         } else if (sp.len[f] % 4 || sp.off[f] % 4) {
             fused = false;
         }
+    }
+    // compile-time message layout: NB dword-granular bytes fields (<= 64 B)
+    // first, then NRAW 8-byte scalars, at 4-byte aligned record offsets
+    uint32_t nb = 0;
+    while (nb < sp.nfields && sp.kind[nb] == MK_FIELD_BYTES) ++nb;
+    bool layout = fused && nb > 0;
+    for (uint32_t f = nb; f < sp.nfields; ++f)
+        if (sp.kind[f] != MK_FIELD_RAW || sp.len[f] != 8) layout = false;
+    const uint32_t nraw = sp.nfields - nb;
+    if (kStructReg && layout && nb == 3 && nraw == 6) {
+        hipLaunchKernelGGL((mk::k_struct_reg<3, 6>), dim3(ceil_div(n, mk::kStructThreads)), dim3(mk::kStructThreads),
+                           0, st, (const uint8_t*)d_rec, n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);
+        HIPCHK(hipGetLastError());
+        return MK_OK;
+    }
+    if (kStructReg && layout && nb == 2 && nraw == 0) {
+        hipLaunchKernelGGL((mk::k_struct_reg<2, 0>), dim3(ceil_div(n, mk::kStructThreads)), dim3(mk::kStructThreads),
+                           0, st, (const uint8_t*)d_rec, n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);
+        HIPCHK(hipGetLastError());
+        return MK_OK;
     }
     if (fused) {
         hipLaunchKernelGGL(mk::k_struct_fused, dim3(ceil_div(n, mk::kStructThreads)), dim3(mk::kStructThreads),

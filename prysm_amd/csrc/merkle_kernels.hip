@@ -1314,6 +1314,92 @@ __global__ __launch_bounds__(kStructThreads) void k_struct_fused(const uint8_t* 
     }
 }
 
+// Struct roots for the "bytes fields first, then 8-byte scalars" layout
+// (pb.Validator: 3 bytes fields + 6 uint64) with the message
+// layout known at compile time: the NB field digests go to this thread's
+// LDS column (24 KB per workgroup for NB = 3, against 36 KB for the whole
+// message in k_struct_fused), the NRAW scalars are re-read from the record
+// at absorb time, and the absorb loop is unrolled over compile-time message
+// dwords.  No barrier: a thread only touches its own LDS column.
+#ifndef MK_STRUCT_REG_WAVES
+#define MK_STRUCT_REG_WAVES 6
+#endif
+template <int NB, int NRAW>
+__global__ __launch_bounds__(kStructThreads, MK_STRUCT_REG_WAVES) void k_struct_reg(const uint8_t* __restrict__ rec,
+                                                                                  uint64_t n, StructSpec sp,
+                                                                                  uint32_t vec16,
+                                                                                  uint4* __restrict__ roots) {
+    __shared__ uint32_t dg[NB * 8 * kStructThreads];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * kStructThreads + tid;
+    if (i >= n) return;
+    const uint8_t* r = rec + i * sp.rec_len;
+    uint32_t nxt[16];
+    load_field16(r + sp.off[0], sp.len[0], vec16, nxt);
+#pragma unroll 1
+    for (uint32_t f = 0; f < (uint32_t)NB; ++f) {  // Keccak(le32(len) || bytes), one block
+        const uint32_t len = sp.len[f];
+        uint32_t a[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) a[k] = nxt[k];
+        if (f + 1 < (uint32_t)NB) load_field16(r + sp.off[f + 1], sp.len[f + 1], vec16, nxt);
+        const uint32_t nd = len / 4 + 1;
+        State s;
+        zero(s);
+#pragma unroll
+        for (int q = 0; q < 18; ++q) {
+            uint32_t v = q == 0 ? len : ((uint32_t)q < nd ? a[q - 1] : 0u);
+            if ((uint32_t)q == nd) v ^= 1u;
+            if (q & 1)
+                s.hi[q / 2] ^= v;
+            else
+                s.lo[q / 2] ^= v;
+        }
+        s.hi[16] ^= 0x80000000u;
+        keccak_f_digest(s);
+        uint4 d0, d1;
+        digest(s, d0, d1);
+        const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int w = 0; w < 8; ++w) dg[(8 * f + w) * kStructThreads + tid] = dw[w];
+    }
+    uint32_t raw[2 * NRAW > 0 ? 2 * NRAW : 1];
+#pragma unroll
+    for (int k = 0; k < NRAW; ++k) {
+        const uint32_t* A32 = reinterpret_cast<const uint32_t*>(r + sp.off[NB + k]);
+        raw[2 * k] = A32[0];
+        raw[2 * k + 1] = A32[1];
+    }
+    constexpr int MW = 8 * NB + 2 * NRAW;  // message dwords
+    constexpr int NBLK = 4 * MW / 136 + 1;
+    State s;
+    zero(s);
+#pragma unroll
+    for (int b = 0; b < NBLK; ++b) {
+#pragma unroll
+        for (int w = 0; w < 34; ++w) {
+            const int q = 34 * b + w;
+            uint32_t v = q < 8 * NB ? dg[q * kStructThreads + tid] : (q < MW ? raw[q - 8 * NB] : 0u);
+            if (q == MW) v ^= 1u;
+            if (b == NBLK - 1 && w == 33) v ^= 0x80000000u;
+            if (w & 1)
+                s.hi[w / 2] ^= v;
+            else
+                s.lo[w / 2] ^= v;
+        }
+        if (b + 1 < NBLK)
+            keccak_f(s);
+        else
+            keccak_f_digest(s);
+    }
+    uint4 d0, d1;
+    digest(s, d0, d1);
+    roots[2 * i] = d0;
+    roots[2 * i + 1] = d1;
+}
+template __global__ void k_struct_reg<3, 6>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
+template __global__ void k_struct_reg<2, 0>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
+
 // ----------------------------------------------------------------------------
 // n messages of msg_len bytes, msg_len % 8 == 0, 8-byte aligned: whole-word
 // loads only (deposit leaves: 280 B = 35 words = 3 blocks).

@@ -27,6 +27,8 @@ __global__ void k_reduce(ReduceArgs a);
 template <bool FAST>
 __global__ void k_struct_fields(const uint8_t* rec, uint64_t n, StructSpec sp, uint8_t* msg);
 __global__ void k_struct_fused(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
+template <int NB, int NRAW>
+__global__ void k_struct_reg(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
 template <bool LEAF>
 __global__ void k_wave(ReduceArgs a);
 template <bool LEAF>
