@@ -254,6 +254,12 @@ int mk_deposit_trie_build(mk_call* call, const uint8_t* data, const uint64_t* of
 int mk_dev_deposit_trie_append(mk_call* call, void* d_levels, uint64_t capacity, uint64_t count, const void* d_data,
                                const uint64_t* d_offs, uint64_t k, uint32_t fixed_len, uint32_t depth,
                                void* d_root32, void* stream);
+/* Levels d_from+1 .. d_to of the batch build of a `count`-deposit trie whose
+ * level d_from is complete (the root to d_root32 when d_to == depth): lets a
+ * caller hash the leaves and the wide levels of trie i+1 on one stream while
+ * the narrow, latency-bound top of trie i runs on another. */
+int mk_dev_deposit_trie_levels(mk_call* call, void* d_levels, uint64_t capacity, uint64_t count, uint32_t d_from,
+                               uint32_t d_to, uint32_t depth, void* d_root32, void* stream);
 /* GenerateMerkleBranch (deposit_trie.go:43-58) from a device level array:
  * d_branch[d] = sibling of `index`'s ancestor at level d (0^32 if absent). */
 int mk_dev_deposit_trie_branch(mk_call* call, const void* d_levels, uint64_t capacity, uint64_t count,

@@ -295,6 +295,38 @@ int or_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n,
     return 0;
 }
 
+/* The reference's own incremental algorithm, one deposit at a time
+ * (UpdateDepositTrie, deposit_trie.go:29-40): leaf = Hash(deposit), then all
+ * `depth` ancestors recomputed from their two children, where a node not
+ * written yet reads as 0^32 (Go map miss).  The map is replaced by one
+ * zero-initialised array per level.  1 + depth hashes per deposit (35
+ * permutations for a 280-B deposit at depth 32) -- the CPU baseline of the
+ * reference's cost; or_deposit_trie_build is the batch form (same root). */
+int or_deposit_trie_incremental(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
+                                uint8_t root[32]) {
+    memset(root, 0, HASHLEN);
+    if (n == 0) return 0;
+    uint8_t** lv = (uint8_t**)calloc(depth + 1, sizeof(uint8_t*));
+    uint64_t cap = n;
+    for (uint32_t d = 0; d <= depth; ++d) {
+        lv[d] = (uint8_t*)calloc(cap + 1, HASHLEN);  /* + 1: the right sibling slot of the last node */
+        cap = (cap + 1) / 2;
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t idx = i;
+        or_keccak256(data + offs[i], offs[i + 1] - offs[i], lv[0] + idx * HASHLEN);
+        for (uint32_t d = 0; d < depth; ++d) {
+            const uint64_t p = idx / 2;
+            or_keccak256(lv[d] + 2 * p * HASHLEN, 2 * HASHLEN, lv[d + 1] + p * HASHLEN);
+            idx = p;
+        }
+    }
+    memcpy(root, lv[depth], HASHLEN);
+    for (uint32_t d = 0; d <= depth; ++d) free(lv[d]);
+    free(lv);
+    return 0;
+}
+
 /* deposit_trie.go:68-81; tree_depth = params DepositContractTreeDepth */
 int or_verify_merkle_branch(const uint8_t leaf[32], const uint8_t* branch, uint32_t depth,
                             uint64_t index, uint32_t tree_depth, const uint8_t root[32]) {

@@ -22,6 +22,8 @@ int or_merkle_subtree_gen(uint64_t n, uint32_t item_len, uint64_t seed, uint64_t
 
 int or_deposit_trie_build(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
                           uint8_t* levels_out, uint8_t root[32]);
+int or_deposit_trie_incremental(const uint8_t* data, const uint64_t* offs, uint64_t n, uint32_t depth,
+                                uint8_t root[32]);
 int or_verify_merkle_branch(const uint8_t leaf[32], const uint8_t* branch, uint32_t depth,
                             uint64_t index, uint32_t tree_depth, const uint8_t root[32]);
 int or_merkle_root(const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_t out[32]);

@@ -54,13 +54,15 @@ def lib():
         L.or_merkle_subtree_gen.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                             ctypes.c_uint64, ctypes.c_uint32, u8p, ctypes.c_int]
         L.or_deposit_trie_build.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint32, u8p, u8p]
+        L.or_deposit_trie_incremental.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint32, u8p]
         L.or_verify_merkle_branch.argtypes = [u8p, u8p, ctypes.c_uint32, ctypes.c_uint64,
                                               ctypes.c_uint32, u8p]
         L.or_merkle_root.argtypes = [u8p, u8p, ctypes.c_uint64, u8p]
         L.or_struct_roots.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint32,
                                       u8p, ctypes.c_int]
         for name in ("or_merkle_hash", "or_merkle_hash_var", "or_merkle_hash_gen",
-                     "or_merkle_subtree_gen", "or_deposit_trie_build", "or_verify_merkle_branch",
+                     "or_merkle_subtree_gen", "or_deposit_trie_build", "or_deposit_trie_incremental",
+                     "or_verify_merkle_branch",
                      "or_merkle_root"):
             getattr(L, name).restype = ctypes.c_int
         _lib = L
@@ -176,6 +178,15 @@ def deposit_trie_levels(deposits, depth: int = DEPOSIT_TREE_DEPTH):
             levels.append([bytes(lv[(pos + i) * 32:(pos + i + 1) * 32]) for i in range(c)])
             pos += c
     return root.raw, levels
+
+
+def deposit_trie_incremental_root(deposits, depth: int = DEPOSIT_TREE_DEPTH) -> bytes:
+    """Root after n calls of the reference's UpdateDepositTrie (C restatement,
+    1 + depth hashes per deposit)."""
+    data, offs = _flat(deposits)
+    root = ctypes.create_string_buffer(32)
+    lib().or_deposit_trie_incremental(_ptr(data), _ptr(offs), len(deposits), depth, root)
+    return root.raw
 
 
 class DictTrie:

@@ -688,15 +688,17 @@ int check_trie(uint64_t cap, uint64_t count, uint64_t k, uint32_t depth) {
     return MK_OK;
 }
 
-// Batch build of levels 1..depth over the `n` leaf hashes already in level 0.
-int trie_levels_build(void* d_levels, uint64_t cap, uint64_t n, uint32_t depth, void* d_root32, hipStream_t st) {
+// Levels d_from+1 .. d_to of the batch build over `n` deposits, level d_from
+// complete; the root (level depth node 0) to d_root32 when d_to == depth.
+int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from, uint32_t d_to, uint32_t depth,
+                      void* d_root32, hipStream_t st) {
     // Wide levels: one launch per level (every lane busy); the narrow top
     // (<= 2^17 nodes) plus the zero-sibling tail: k_trie_top3 (bit-interleaved
     // lane pairs), log2(NT) levels per workgroup of NT inputs, the last
     // launch to the top.
-    uint64_t c = n;
-    uint32_t d = 0;
-    while (d < depth && c > kTrieTopMax) {
+    uint64_t c = mk::trie_count(n, d_from);
+    uint32_t d = d_from;
+    while (d < d_to && c > kTrieTopMax) {
         const uint64_t cn = (c + 1) / 2;
         hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(cn, 256)), dim3(256), 0, st,
                            (const uint4*)trie_level(d_levels, cap, d), c, trie_level(d_levels, cap, d + 1));
@@ -704,12 +706,12 @@ int trie_levels_build(void* d_levels, uint64_t cap, uint64_t n, uint32_t depth, 
         c = cn;
         ++d;
     }
-    while (d < depth) {
+    while (d < d_to) {
         uint32_t nt = mk::kWaveThreads;
         while (nt < mk::kMidThreads && ceil_div(c, nt) > kTrieTopWgs) nt *= 2;
         while (nt < mk::kMidThreads && c <= mk::kMidThreads && c > nt) nt *= 2;  // the last <= 1024 nodes in one WG
         const uint64_t nwg = ceil_div(c, nt);
-        const uint32_t k = nwg == 1 ? depth - d : std::min<uint32_t>(ilog2(nt), depth - d);
+        const uint32_t k = nwg == 1 ? d_to - d : std::min<uint32_t>(ilog2(nt), d_to - d);
         const uint32_t* src = (const uint32_t*)trie_level(d_levels, cap, d);
         uint32_t* dst = (uint32_t*)trie_level(d_levels, cap, d + 1);
         const uint64_t capn = mk::trie_count(cap, d + 1);
@@ -724,8 +726,13 @@ int trie_levels_build(void* d_levels, uint64_t cap, uint64_t n, uint32_t depth, 
         for (uint32_t i = 0; i < k; ++i) c = (c + 1) / 2;
         d += k;
     }
-    HIPCHK(hipMemcpyAsync(d_root32, trie_level(d_levels, cap, depth), 32, hipMemcpyDeviceToDevice, st));
+    if (d_to == depth && d_root32)
+        HIPCHK(hipMemcpyAsync(d_root32, trie_level(d_levels, cap, depth), 32, hipMemcpyDeviceToDevice, st));
     return MK_OK;
+}
+
+int trie_levels_build(void* d_levels, uint64_t cap, uint64_t n, uint32_t depth, void* d_root32, hipStream_t st) {
+    return trie_levels_range(d_levels, cap, n, 0, depth, depth, d_root32, st);
 }
 
 int dev_trie_append(void* d_levels, uint64_t cap, uint64_t count, const void* d_data, const uint64_t* d_offs,
@@ -1504,6 +1511,19 @@ int mk_dev_deposit_trie_append(mk_call* call, void* d_levels, uint64_t capacity,
     return S.done(rc ? rc
                      : dev_trie_append(d_levels, capacity, count, d_data, d_offs, k, fixed_len, depth, d_root32,
                                        (hipStream_t)stream));
+}
+
+int mk_dev_deposit_trie_levels(mk_call* call, void* d_levels, uint64_t capacity, uint64_t count, uint32_t d_from,
+                               uint32_t d_to, uint32_t depth, void* d_root32, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    rc = check_trie(capacity, count, 0, depth);
+    if (rc) return S.done(rc);
+    if (d_from > d_to || d_to > depth) return S.done(fail(MK_EINVAL, "levels %u..%u out of range", d_from, d_to));
+    if (!d_levels || count == 0 || (d_to == depth && !d_root32))
+        return S.done(fail(MK_EINVAL, "null pointer or empty trie"));
+    return S.done(trie_levels_range(d_levels, capacity, count, d_from, d_to, depth, d_root32, (hipStream_t)stream));
 }
 
 int mk_dev_deposit_trie_branch(mk_call* call, const void* d_levels, uint64_t capacity, uint64_t count,

@@ -269,6 +269,15 @@ def deposit_trie_append(levels: torch.Tensor, capacity: int, count: int, data: t
                 device=dev)
 
 
+def deposit_trie_levels(levels: torch.Tensor, capacity: int, count: int, d_from: int, d_to: int, depth: int,
+                        root: torch.Tensor = None) -> None:
+    """Levels d_from+1 .. d_to of the batch build (level d_from complete);
+    the root to ``root`` when d_to == depth."""
+    dev = _dev(levels)
+    _lib.invoke("mk_dev_deposit_trie_levels", _p(levels), capacity, count, d_from, d_to, depth,
+                _p(root) if root is not None else None, _stream(levels.device), device=dev)
+
+
 def deposit_trie_branch(levels: torch.Tensor, capacity: int, count: int, depth: int, index: int,
                         out: torch.Tensor = None) -> torch.Tensor:
     """GenerateMerkleBranch(index) of a device trie: (depth*32,) uint8."""

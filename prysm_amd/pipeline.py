@@ -78,3 +78,56 @@ class MerklePipeline:
             ev.record(self.side)
         self._done[slot] = ev
         return root
+
+
+class TriePipeline:
+    """Batch builds of a stream of deposit tries (one trie per ``submit``,
+    trieutil.DepositTrie semantics, deposit_trie.go:29-63) with each trie's
+    narrow top off the main stream.
+
+    Per trie, on the caller's current stream: the leaf hashes
+    (Hash(deposit), one launch) and the wide levels, down to the first level
+    of at most 2^17 nodes (one launch per level, every lane busy).  On a
+    high-priority side stream, overlapping the next trie's leaves: the
+    latency-bound top (k_trie_top3 launches) plus the zero-sibling levels
+    up to ``depth`` and the root.  Level arrays and roots are double-buffered
+    like MerklePipeline: a submit waits for the top of the trie two submits
+    back; a returned root stays valid until the submit after next."""
+
+    TOP_MAX = 1 << 17  # capi.cpp kTrieTopMax: levels at or below this width run k_trie_top3
+
+    def __init__(self, n: int, deposit_len: int, depth: int, device):
+        self.n, self.dl, self.depth = n, deposit_len, depth
+        self.device = torch.device(device)
+        split = 0
+        while split < depth and -(-n // (1 << split)) > self.TOP_MAX:
+            split += 1
+        self.split = split
+        nbytes = D.deposit_trie_levels_bytes(n, depth)
+        self.levels = [torch.empty(nbytes, dtype=torch.uint8, device=self.device) for _ in range(2)]
+        self.roots = [torch.empty(32, dtype=torch.uint8, device=self.device) for _ in range(2)]
+        self.side = torch.cuda.Stream(device=self.device, priority=-1)  # its own hardware queue
+        self._done = [None, None]
+        self._i = 0
+
+    def submit(self, deposits: torch.Tensor) -> torch.Tensor:
+        """Enqueue the trie of n fixed-length deposits held in ``deposits``;
+        returns its (32,) root tensor, produced on ``self.side``."""
+        if deposits.numel() < self.n * self.dl:
+            raise ValueError("deposit buffer shorter than n * deposit_len")
+        slot = self._i & 1
+        self._i += 1
+        cur = torch.cuda.current_stream(self.device)
+        if self._done[slot] is not None:
+            cur.wait_event(self._done[slot])
+        lv, root = self.levels[slot], self.roots[slot]
+        D.hash_batch(deposits, self.n, self.dl, out=lv[:32 * self.n])
+        if self.split:
+            D.deposit_trie_levels(lv, self.n, self.n, 0, self.split, self.depth)
+        self.side.wait_stream(cur)
+        with torch.cuda.stream(self.side):
+            D.deposit_trie_levels(lv, self.n, self.n, self.split, self.depth, self.depth, root)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+        self._done[slot] = ev
+        return root

@@ -152,3 +152,33 @@ def test_dev_append_stream_of_blocks(gpu):
                            for d in range(depth))
         assert bytes(br.cpu().numpy()) == want_br, count
     assert count == total
+
+
+@pytest.mark.parametrize("n", [1, 5, 1000, (1 << 17) + 3, (1 << 19) + 7])
+def test_trie_pipeline_stream_of_tries(gpu, n):
+    """TriePipeline: leaves + wide levels on the current stream, the top on a
+    side stream overlapping the next trie; 4 consecutive tries, each root and
+    a branch against the oracle's batch build."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+    from prysm_amd.pipeline import TriePipeline
+
+    ln, depth = 280, 32
+    pipe = TriePipeline(n, ln, depth, gpu)
+    datas = []
+    for t in range(4):
+        d = torch.empty(n * ln, dtype=torch.uint8, device=gpu)
+        D.synth_fill(d, SEED + 900 + t)
+        datas.append(d)
+    roots = []
+    for t, d in enumerate(datas):
+        roots.append(pipe.submit(d))
+        if t % 2 == 1:
+            torch.cuda.synchronize()
+            roots = [r if isinstance(r, bytes) else bytes(r.cpu().numpy()) for r in roots]
+    for t, d in enumerate(datas):
+        host = d.cpu().numpy()
+        want = O.deposit_trie_levels([bytes(host[i * ln:(i + 1) * ln]) for i in range(n)])[0]
+        assert roots[t] == want, (t, pipe.split)

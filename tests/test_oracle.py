@@ -133,6 +133,17 @@ def test_deposit_trie_batch_equals_incremental(n):
         assert not O.verify_merkle_branch(O.keccak256(deps[i] + b"x"), br, 32, i, root)
 
 
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 7, 100, 1025])
+def test_incremental_c_restatement_equals_dict_and_batch(n):
+    """or_deposit_trie_incremental (the reference's per-deposit algorithm in C,
+    the C5 CPU baseline) against the dict restatement and the batch build."""
+    deps = [bytes([i % 251]) * (1 + (i * 37) % 300) for i in range(n)]
+    t = _DictTrie()
+    for d in deps:
+        t.update(d)
+    assert O.deposit_trie_incremental_root(deps) == t.root() == O.deposit_trie_levels(deps)[0]
+
+
 def test_restatement_fixtures_reproduce(res_vectors):
     for c in res_vectors["merkle_flat"][::17]:
         items = O.splitmix_bytes(c["n"] * c["item_len"], c["seed"])

@@ -25,6 +25,17 @@ OPS_PER_PERM = 4320
 OPS_SAVED_PER_HASH = 122
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def _timeit(fn, steps, warmup):
     import torch
 
@@ -101,7 +112,7 @@ def run_config(args):
                 rr = O.struct_roots(raw, n, 160, R.VALIDATOR_FIELDS, nthreads=1)
                 O.merkle_hash_flat(rr.reshape(-1), n, 32)
             dt = (time.perf_counter() - t0) / 10
-            cpu = {"value": n / dt, "unit": "validators/s", "cores": 1, "kind": "port",
+            cpu = {"value": n / dt, "unit": "validators/s", "cores": 1, "kind": "port", "cpu_model": _cpu_model(),
                    "sample": f"oracle struct_roots + merkleHash, the same 16,384 validators, 1 thread, {dt * 1e3:.1f} ms"}
         _line("ssz.TreeHash of a 16,384-entry []ValidatorRecord (host buffers)", n / sec, "validators/s", args, sec,
               perms, hashes, {"workload": "C1: TreeHash([]*ValidatorRecord), 16,384 synthetic validators, host records",
@@ -124,7 +135,7 @@ def run_config(args):
             t0 = time.perf_counter()
             O.keccak256_batch(host, 64, nthreads=1)
             dt = time.perf_counter() - t0
-            cpu = {"value": m / dt, "unit": "hashes/s", "cores": 1, "kind": "port",
+            cpu = {"value": m / dt, "unit": "hashes/s", "cores": 1, "kind": "port", "cpu_model": _cpu_model(),
                    "sample": f"oracle keccak256_batch, 2^21 x 64-B messages, 1 thread, {dt:.1f} s"}
         _line("hashutil.Hash throughput, 2^24 x 64-B messages", n / sec, "hashes/s", args, sec, n, n,
               {"workload": "C2: batched Keccak-256 of 2^24 x 64-B messages (1 GiB)", "n": n, "msg_len": 64},
@@ -178,7 +189,7 @@ def run_config(args):
             O.merkle_hash_flat(rr.reshape(-1), m, 32)
             O.merkle_hash_flat(bal[:m].view(np.uint8), m, 8)
             dt = time.perf_counter() - t0
-            cpu = {"value": m / dt, "unit": "validators/s", "cores": 1, "kind": "port",
+            cpu = {"value": m / dt, "unit": "validators/s", "cores": 1, "kind": "port", "cpu_model": _cpu_model(),
                    "sample": f"oracle struct_roots + merkleHash, 2^17 validators + balances, 1 thread, {dt:.1f} s"}
         _line("TreeHash of a 1M-validator State (registry + balances)", n / sec, "validators/s", args, sec, perms, hashes,
               {"workload": "C3: synthetic State{[]*ValidatorRecord, []uint64}, 1,000,000 validators",
@@ -191,27 +202,51 @@ def run_config(args):
         D.synth_fill(data, seed + 5)
         lv = torch.empty(L.mk_deposit_trie_levels_bytes(n, depth), dtype=torch.uint8, device=dev)
         root = torch.empty(32, dtype=torch.uint8, device=dev)
-        sec = _timeit(lambda: _lib.check(L.mk_dev_deposit_trie_append(None, P(lv), n, 0, P(data), None, n, dl, depth,
-                                                                      P(root), st()), "c5"), args.steps, args.warmup)
+        one = lambda: _lib.check(L.mk_dev_deposit_trie_append(None, P(lv), n, 0, P(data), None, n, dl, depth,  # noqa
+                                                               P(root), st()), "c5")
+        sec_one = _timeit(one, args.steps, args.warmup)  # one trie: leaves, levels, top, in order
+        one_root = bytes(root.cpu().numpy())
+        # a stream of tries (TriePipeline): trie i's latency-bound top on a
+        # high-priority side stream overlaps trie i+1's leaves and wide levels
+        from prysm_amd.pipeline import TriePipeline
+
+        pipe = TriePipeline(n, dl, depth, dev)
+        got = pipe.submit(data)
+        torch.cuda.synchronize()
+        if bytes(got.cpu().numpy()) != one_root:
+            raise SystemExit("c5: pipelined root differs from the one-call root")
+        sec = _timeit(lambda: pipe.submit(data), args.steps, args.warmup)
         perms = 3 * n + (n - 1) + (depth - 20)
         hashes = n + (n - 1) + (depth - 20)
         cpu = None
         if not args.no_cpu_baseline:
             from oracle import oracle as O
 
+            # SURVEY 8d / BASELINE.md 3: both CPU algorithms on 2^17 deposits,
+            # the reference's incremental UpdateDepositTrie (1 + 32 hashes per
+            # deposit) and the batch form (1 + ~1 per deposit)
             m = 1 << 17
             host = O.splitmix_bytes(m * dl, seed + 5)
             deps = [bytes(host[i * dl:(i + 1) * dl]) for i in range(m)]
             t0 = time.perf_counter()
-            O.deposit_trie_levels(deps)
+            r_inc = O.deposit_trie_incremental_root(deps)
+            dt_inc = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            r_bat, _ = O.deposit_trie_levels(deps)
             dt = time.perf_counter() - t0
-            cpu = {"value": m / dt, "unit": "deposits/s", "cores": 1, "kind": "port",
-                   "sample": f"oracle batch deposit trie, 2^17 x 280-B deposits, 1 thread, {dt:.1f} s "
-                             "(the reference's incremental UpdateDepositTrie does 35 perms/deposit, "
-                             "this batch form 4)"}
+            assert r_inc == r_bat
+            cpu = {"value": m / dt_inc, "unit": "deposits/s", "cores": 1, "kind": "port",
+                   "cpu_model": _cpu_model(),
+                   "sample": f"oracle or_deposit_trie_incremental (the reference's UpdateDepositTrie loop, "
+                             f"35 perms/deposit), 2^17 x 280-B deposits, 1 thread, {dt_inc:.1f} s",
+                   "batch_form": {"value": m / dt, "unit": "deposits/s", "cores": 1,
+                                  "sample": f"oracle or_deposit_trie_build (batch, ~4 perms/deposit), the same "
+                                            f"2^17 deposits, 1 thread, {dt:.2f} s"}}
         _line("deposit trie build, 2^20 x 280-B deposits, depth 32", n / sec, "deposits/s", args, sec, perms, hashes,
-              {"workload": "C5: trieutil deposit trie, 2^20 synthetic 280-B deposits", "n": n,
-               "root": bytes(root.cpu().numpy()).hex()}, cpu)
+              {"workload": "C5: trieutil deposit trie, 2^20 synthetic 280-B deposits (stream of tries, "
+                           "each trie's top overlapping the next trie's leaves)", "n": n,
+               "root": one_root.hex(), "pipelined": True, "split_level": pipe.split,
+               "single_trie_ms": sec_one * 1e3}, cpu)
         return
 
 
