@@ -139,7 +139,8 @@ def ab_struct(a, libs, dev):
     nf = len(R.VALIDATOR_FIELDS)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     first = libs[a.variants[0]]
-    ws = torch.empty(first.mk_ssz_struct_list_workspace_bytes(n, spec, nf) + 4096, dtype=torch.uint8, device=dev)
+    ws = torch.empty(max(L.mk_ssz_struct_list_workspace_bytes(n, spec, nf) for L in libs.values()) + 4096,
+                     dtype=torch.uint8, device=dev)
     outs = {v: torch.empty(32, dtype=torch.uint8, device=dev) for v in a.variants}
     times = {v: [] for v in a.variants}
     for r in range(a.rounds + 1):

@@ -9,6 +9,9 @@ serialised.  Variants:
   side_after  struct kernel first, balances on the side stream after it
   hi_first    side_first with a high-priority side stream
   hi_after    side_after with a high-priority side stream
+  hi_split    struct roots on the current stream; then the balances tree on a
+              high-priority side stream beside the registry merkleHash (the
+              latency-bound top leaves CUs idle that the balances can use)
 
   python tools/c3_streams.py [--rounds 5] [--steps 20]
 """
@@ -59,6 +62,17 @@ def main():
         _lib.check(L.mk_dev_ssz_struct_list_root(None, P(rec), n, 160, spec, nf, P(roots), P(ws), ws.numel(),
                                                  ctypes.c_void_p(cur.cuda_stream)), "registry")
 
+    sroots = torch.empty(32 * n, dtype=torch.uint8, device=dev)
+    sws = torch.empty(n * 144 + 256, dtype=torch.uint8, device=dev)
+    mws = D.merkle_workspace(n, 32, dev)
+
+    def split(cur, side):
+        D.struct_roots(rec, n, 160, R.VALIDATOR_FIELDS, out=sroots, ws=sws)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            balances()
+        D.merkle_hash(sroots, n, 32, out=roots[:32], ws=mws)
+
     def balances():
         D.merkle_hash(dbal, n, 8, out=roots[32:], ws=bws)
 
@@ -73,6 +87,8 @@ def main():
             if kind == "serial":
                 registry(cur)
                 balances()
+            elif kind == "hi_split":
+                split(cur, side)
             elif kind.endswith("first"):
                 side.wait_stream(cur)
                 with torch.cuda.stream(side):
@@ -88,7 +104,7 @@ def main():
             final(cur)
         return step
 
-    kinds = ["serial", "side_first", "side_after", "hi_first", "hi_after"]
+    kinds = ["serial", "hi_first", "hi_split"]
     steps = {k: make(k) for k in kinds}
     times = {k: [] for k in kinds}
     want = R.state_root(reg, bal)

@@ -23,7 +23,9 @@ def counters(d):
 
 
 def main(d):
-    res = {"dir": d}
+    import socket
+
+    res = {"dir": d, "box": f"GPU box {socket.gethostname()}"}
     stats = glob.glob(os.path.join(d, "stats", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         res["kernel_stats"] = [
