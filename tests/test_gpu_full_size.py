@@ -90,6 +90,34 @@ def test_c2_full_2p24(gpu):
 
 
 @pytest.mark.gpu
+def test_c3_2p20_validators_device_generated(gpu):
+    """SURVEY.md §8d's second C3 size, N = 2^20: the registry and balances
+    generated in HBM (synthetic_registry_device: k_synth + the index rules),
+    equal to the host generator, and the device-resident State root equal to
+    the oracle's (C restatement, computed here on the host cores)."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+    from prysm_amd import registry as R
+
+    n, seed = 1 << 20, GOLD["c3"]["seed"]
+    reg = R.synthetic_registry(n, seed)
+    bal = R.synthetic_balances(n, seed)
+    drec = R.synthetic_registry_device(n, seed, gpu)
+    dbal = R.synthetic_balances_device(n, seed, gpu)
+    torch.cuda.synchronize()
+    assert np.array_equal(drec.cpu().numpy(), reg.records.view(np.uint8).reshape(-1))
+    assert np.array_equal(dbal.cpu().numpy(), bal.view(np.uint8))
+    reg_root = D.struct_list_root(drec, n, 160, R.VALIDATOR_FIELDS)
+    bal_root = D.merkle_hash(dbal, n, 8)
+    torch.cuda.synchronize()
+    roots = O.struct_roots(reg.records.view(np.uint8).reshape(-1), n, 160, R.VALIDATOR_FIELDS, nthreads=16)
+    assert bytes(reg_root.cpu().numpy()) == O.merkle_hash_flat(roots.reshape(-1), n, 32, nthreads=16)
+    assert bytes(bal_root.cpu().numpy()) == O.merkle_hash_flat(bal.view(np.uint8), n, 8, nthreads=16)
+
+
+@pytest.mark.gpu
 def test_c3_full_1m_validators(gpu):
     from prysm_amd import registry as R
     from prysm_amd import ssz as S
