@@ -688,6 +688,37 @@ int check_trie(uint64_t cap, uint64_t count, uint64_t k, uint32_t depth) {
     return MK_OK;
 }
 
+// Most parents any level d .. d_end-1 has when the nodes [lo, c) of level d
+// changed (the right edge of an append; lo = 0 for a batch top).
+uint64_t edge_max_parents(uint64_t lo, uint64_t c, uint32_t d, uint32_t d_end) {
+    uint64_t m = 0;
+    for (; d < d_end; ++d) {
+        const uint64_t plo = lo >> 1, cp = (c + 1) >> 1;
+        m = std::max(m, cp - plo);
+        lo = plo;
+        c = cp;
+    }
+    return m;
+}
+
+// k_trie_spread over levels d .. d_end-1 (one wave per parent, <= 4 parents)
+int launch_trie_spread(void* d_levels, uint64_t cap, uint32_t d, uint64_t lo, uint64_t c, uint32_t d_end,
+                       uint32_t depth, void* d_root32, hipStream_t st) {
+    const uint64_t m = edge_max_parents(lo, c, d, d_end);
+    uint32_t* lv = (uint32_t*)d_levels;
+    uint32_t* root = (uint32_t*)d_root32;
+    if (m <= 1)
+        hipLaunchKernelGGL(mk::k_trie_spread<1>, dim3(1), dim3(64), 0, st, lv, cap, d, lo, c, d_end, depth, root);
+    else if (m <= 2)
+        hipLaunchKernelGGL(mk::k_trie_spread<2>, dim3(1), dim3(128), 0, st, lv, cap, d, lo, c, d_end, depth, root);
+    else if (m <= mk::kSpreadWavesMax)
+        hipLaunchKernelGGL(mk::k_trie_spread<4>, dim3(1), dim3(256), 0, st, lv, cap, d, lo, c, d_end, depth, root);
+    else
+        return fail(MK_EINVAL, "internal: trie edge of %llu parents for the spread kernel", (unsigned long long)m);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
 // Levels d_from+1 .. d_to of the batch build over `n` deposits, level d_from
 // complete; the root (level depth node 0) to d_root32 when d_to == depth.
 int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from, uint32_t d_to, uint32_t depth,
@@ -706,12 +737,29 @@ int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from,
         c = cn;
         ++d;
     }
+    bool root_done = false;
     while (d < d_to) {
+        if (MK_TRIE_SPREAD && c <= 2 * mk::kSpreadWavesMax) {  // the last <= 3 levels + zero-sibling tail
+            void* root = d_to == depth ? d_root32 : nullptr;
+            TRY(launch_trie_spread(d_levels, cap, d, 0, c, d_to, depth, root, st));
+            root_done = root != nullptr;
+            d = d_to;
+            break;
+        }
         uint32_t nt = mk::kWaveThreads;
         while (nt < mk::kMidThreads && ceil_div(c, nt) > kTrieTopWgs) nt *= 2;
         while (nt < mk::kMidThreads && c <= mk::kMidThreads && c > nt) nt *= 2;  // the last <= 1024 nodes in one WG
         const uint64_t nwg = ceil_div(c, nt);
-        const uint32_t k = nwg == 1 ? d_to - d : std::min<uint32_t>(ilog2(nt), d_to - d);
+        uint32_t k = nwg == 1 ? d_to - d : std::min<uint32_t>(ilog2(nt), d_to - d);
+        if (MK_TRIE_SPREAD && nwg == 1) {  // stop where k_trie_spread takes over
+            uint64_t cc = c;
+            uint32_t kk = 0;
+            while (kk < k && cc > 2 * mk::kSpreadWavesMax) {
+                cc = (cc + 1) / 2;
+                ++kk;
+            }
+            k = kk;
+        }
         const uint32_t* src = (const uint32_t*)trie_level(d_levels, cap, d);
         uint32_t* dst = (uint32_t*)trie_level(d_levels, cap, d + 1);
         const uint64_t capn = mk::trie_count(cap, d + 1);
@@ -726,7 +774,7 @@ int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from,
         for (uint32_t i = 0; i < k; ++i) c = (c + 1) / 2;
         d += k;
     }
-    if (d_to == depth && d_root32)
+    if (d_to == depth && d_root32 && !root_done)
         HIPCHK(hipMemcpyAsync(d_root32, trie_level(d_levels, cap, depth), 32, hipMemcpyDeviceToDevice, st));
     return MK_OK;
 }
@@ -764,18 +812,30 @@ int dev_trie_append(void* d_levels, uint64_t cap, uint64_t count, const void* d_
         HIPCHK(hipMemcpyAsync(d_root32, trie_level(d_levels, cap, depth), 32, hipMemcpyDeviceToDevice, st));
         return MK_OK;
     }
+    // lane pairs (k_trie_append) while a level has more than kSpreadWavesMax
+    // changed parents, then one state per wave (k_trie_spread) to the root
+    uint32_t d_stop = d;
+    uint64_t slo = lo, sc = c;
+    while (d_stop < depth && (!MK_TRIE_SPREAD || edge_max_parents(slo, sc, d_stop, depth) > mk::kSpreadWavesMax)) {
+        slo >>= 1;
+        sc = (sc + 1) >> 1;
+        ++d_stop;
+    }
     const uint64_t r = c - lo;
     uint32_t* lv = (uint32_t*)d_levels;
-    if (r <= 60)
-        hipLaunchKernelGGL(mk::k_trie_append<64>, dim3(1), dim3(64), 0, st, lv, cap, d, lo, c, depth,
-                           (uint32_t*)d_root32);
-    else if (r <= 252)
-        hipLaunchKernelGGL(mk::k_trie_append<256>, dim3(1), dim3(256), 0, st, lv, cap, d, lo, c, depth,
-                           (uint32_t*)d_root32);
-    else
-        hipLaunchKernelGGL(mk::k_trie_append<1024>, dim3(1), dim3(1024), 0, st, lv, cap, d, lo, c, depth,
-                           (uint32_t*)d_root32);
-    HIPCHK(hipGetLastError());
+    uint32_t* root = (uint32_t*)d_root32;
+    if (d_stop > d) {
+        if (r <= 60)
+            hipLaunchKernelGGL(mk::k_trie_append<64>, dim3(1), dim3(64), 0, st, lv, cap, d, lo, c, d_stop, depth, root);
+        else if (r <= 252)
+            hipLaunchKernelGGL(mk::k_trie_append<256>, dim3(1), dim3(256), 0, st, lv, cap, d, lo, c, d_stop, depth,
+                               root);
+        else
+            hipLaunchKernelGGL(mk::k_trie_append<1024>, dim3(1), dim3(1024), 0, st, lv, cap, d, lo, c, d_stop, depth,
+                               root);
+        HIPCHK(hipGetLastError());
+    }
+    if (d_stop < depth) TRY(launch_trie_spread(d_levels, cap, d_stop, slo, sc, depth, depth, d_root32, st));
     return MK_OK;
 }
 

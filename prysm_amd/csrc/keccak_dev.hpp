@@ -564,3 +564,174 @@ __device__ __forceinline__ uint32_t from_ilv(uint32_t own, uint32_t p) {
 
 }  // namespace ilv
 }  // namespace mk
+
+// ============================================================================
+// One state spread over a whole wave (latency form, v3).  GPU lane L = 8g + q
+// holds, bit-interleaved (ilv words: e = even bits, o = odd bits), the Keccak
+// lane (x, y) = (q mod 5, min(g, 4)): group g < 5 is row y = g, positions
+// 0..4 are the canonical x = 0..4 and positions 5..7 repeat x = 0..2, and
+// groups 5..7 mirror row 4.  Per round and lane: theta's column parity is an
+// all-reduce over the groups (row_ror:8 DPP with rows {0,1,3} enabled, then
+// v_permlane16_swap and v_permlane32_swap: the mirrors make rows 2/3 hold
+// row 4 twice and 0 after the first two steps), its x-1 / x+1 neighbours are
+// row_shr:1 / row_shl:1 DPP moves (row_shl:4 for x-1 at position 0), rho is
+// a per-lane rotation with shift amounts in VGPRs, pi is one ds_bpermute per
+// word from the canonical source lane (which also refreshes the repeats and
+// mirrors), and chi reads x+1 / x+2 with row_shl:1 / row_shl:2.  ~36 VALU
+// instructions and 2 bpermutes per round instead of 107 per lane for the
+// lane pair: the narrow top of a tree, where one permutation's latency on a
+// lone wave is the cost of a whole level.  Canonical positions are correct
+// after every round; positions 6/7 are scratch between pi and the next pi.
+namespace mk {
+namespace spread {
+
+struct Lane {
+    uint32_t i;      // Keccak lane index x + 5y of this GPU lane
+    uint32_t sh1;    // rho: alignbit shift rotating the even word
+    uint32_t sh2;    // rho: alignbit shift rotating the odd word
+    uint32_t swap;   // rho: all-ones when the offset is odd (the parities trade places)
+    uint32_t src;    // pi: ds_bpermute byte address of the source lane
+    uint32_t wrap;   // theta: all-ones at position 0 (x - 1 = 4 sits at position 4)
+    uint32_t iota;   // all-ones on the two GPU lanes holding Keccak lane 0
+};
+
+__device__ __forceinline__ Lane lane_consts(uint32_t L) {
+    const uint32_t g = (L >> 3) & 7u, q = L & 7u;
+    const uint32_t x = q % 5u, y = g < 4u ? g : 4u;
+    Lane c;
+    c.i = x + 5u * y;
+    const uint32_t r = MK_RHO(c.i);
+    const uint32_t m = r >> 1;
+    // rotl by k == alignbit(v, v, (32 - k) & 31)
+    c.swap = (r & 1u) ? 0xFFFFFFFFu : 0u;
+    c.sh1 = (32u - m) & 31u;                   // even word rotated by m
+    c.sh2 = (32u - (m + (r & 1u))) & 31u;      // odd word by m (+1 if r odd)
+    // pi: destination (X, Y) = (y', 2x' + 3y') of source (x', y'):
+    // y' = X, x' = 3 (Y - 3X) mod 5
+    const uint32_t xs = (3u * ((y + 15u - 3u * x) % 5u)) % 5u, ys = x;
+    c.src = 4u * (8u * ys + xs);
+    c.wrap = q == 0u ? 0xFFFFFFFFu : 0u;
+    c.iota = c.i == 0u ? 0xFFFFFFFFu : 0u;
+    return c;
+}
+
+// lanes whose source is outside the 16-lane row read 0 (never used).  Every
+// lane must be written (bound_ctrl): with an undefined old value the DPP
+// combiner may fold the move into its user (e.g. a v_cndmask) and leave
+// such lanes unwritten, which corrupted the x-1 select at positions 0/1.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+constexpr int kShl1 = 0x101, kShl2 = 0x102, kShl4 = 0x104, kShr1 = 0x111, kRor8 = 0x128;
+
+// column parity of this lane's x (valid at positions 0..5 of every group)
+__device__ __forceinline__ uint32_t colsum(uint32_t v) {
+    // rows 0, 1: g0^g1, g2^g3; row 2 kept (g4 | g5 = g4); row 3: g6^g7 = 0
+    const uint32_t t = v ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRor8, 0xB, 0xF, false);
+    const auto a = __builtin_amdgcn_permlane16_swap(t, t, false, false);
+    const uint32_t s = a[0] ^ a[1];  // rows 0, 1: g0^..^g3; rows 2, 3: g4
+    const auto b = __builtin_amdgcn_permlane32_swap(s, s, false, false);
+    return b[0] ^ b[1];
+}
+
+// m ? a : b per bit (LUT 0xCA).  Lane selects must not be written as ?: on a
+// DPP result: the compiler turns that into exec-masked DPP moves, and a DPP
+// read of a lane that is off in EXEC returns 0.
+__device__ __forceinline__ uint32_t sel(uint32_t m, uint32_t a, uint32_t b) {
+    return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);
+}
+
+// column parities of both words at once: the first swap pairs the even
+// word's rows with the odd word's, so rows 0/2 carry even sums and rows 1/3
+// odd sums until the last swap spreads each over the wave
+__device__ __forceinline__ void colsum2(uint32_t e, uint32_t o, uint32_t& ce, uint32_t& co) {
+    const uint32_t te = e ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, kRor8, 0xB, 0xF, false);
+    const uint32_t to = o ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)o, kRor8, 0xB, 0xF, false);
+    const auto a = __builtin_amdgcn_permlane16_swap(te, to, false, false);
+    const uint32_t r = a[0] ^ a[1];  // rows: e(0^1), o(0^1), e(2^3), o(2^3)
+    const auto b = __builtin_amdgcn_permlane32_swap(r, r, false, false);
+    const uint32_t s = b[0] ^ b[1];  // rows: Ce, Co, Ce, Co
+    const auto d = __builtin_amdgcn_permlane16_swap(s, s, false, false);
+    ce = d[0];
+    co = d[1];
+}
+
+__device__ __forceinline__ void round_fn(uint32_t& e, uint32_t& o, const Lane& c, uint32_t rce, uint32_t rco) {
+    uint32_t ce, co;
+    colsum2(e, o, ce, co);
+    const uint32_t me = sel(c.wrap, dpp<kShl4>(ce), dpp<kShr1>(ce));
+    const uint32_t mo = sel(c.wrap, dpp<kShl4>(co), dpp<kShr1>(co));
+    // D = C[x-1] ^ rotl64(C[x+1], 1): even word rotl32(odd, 1), odd word = even
+    e = xor3(e, me, __builtin_amdgcn_alignbit(dpp<kShl1>(co), dpp<kShl1>(co), 31u));
+    o = xor3(o, mo, dpp<kShl1>(ce));
+    const uint32_t t1 = __builtin_amdgcn_alignbit(e, e, c.sh1);
+    const uint32_t t2 = __builtin_amdgcn_alignbit(o, o, c.sh2);
+    const uint32_t re = sel(c.swap, t2, t1), ro = sel(c.swap, t1, t2);
+    const uint32_t be = (uint32_t)__builtin_amdgcn_ds_bpermute((int)c.src, (int)re);
+    const uint32_t bo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)c.src, (int)ro);
+    // iota: v ^ (iota & rc), LUT 0x78
+    e = __builtin_amdgcn_bitop3_b32(chi3(be, dpp<kShl1>(be), dpp<kShl2>(be)), c.iota, rce, 0x78);
+    o = __builtin_amdgcn_bitop3_b32(chi3(bo, dpp<kShl1>(bo), dpp<kShl2>(bo)), c.iota, rco, 0x78);
+}
+
+// ---- the same permutation on (lo, hi) halves instead of parity words ----------
+// One more alignbit per round (theta's rotl 1 needs both halves), but nodes
+// go in and out as plain 64-bit words: for one permutation per tree level
+// that is cheaper than the bit (de)interleave.  rho: rotl64 by r = 32s + t
+// takes (a, b) = (hi, lo) or, for r >= 32, (lo, hi) and shifts by 32 - t;
+// r = 0 is run as r = 64 (shift 0 returns the second operand).
+struct LaneLH {
+    uint32_t swap;   // all-ones when r >= 32 or r == 0
+    uint32_t sh;     // (32 - r mod 32) mod 32
+    uint32_t src;    // pi: ds_bpermute byte address of the source lane
+    uint32_t wrap;   // theta: all-ones at position 0
+    uint32_t iota;   // all-ones on the lanes holding Keccak lane 0
+    uint32_t i;      // Keccak lane index of this GPU lane
+};
+
+__device__ __forceinline__ LaneLH lane_consts_lh(uint32_t L) {
+    const Lane c = lane_consts(L);
+    const uint32_t r = MK_RHO(c.i);
+    LaneLH h;
+    h.swap = (r >= 32u || r == 0u) ? 0xFFFFFFFFu : 0u;
+    h.sh = (32u - (r & 31u)) & 31u;
+    h.src = c.src;
+    h.wrap = c.wrap;
+    h.iota = c.iota;
+    h.i = c.i;
+    return h;
+}
+
+__device__ __forceinline__ void round_lh(uint32_t& lo, uint32_t& hi, const LaneLH& c, uint32_t rcl, uint32_t rch) {
+    uint32_t cl, ch;
+    colsum2(lo, hi, cl, ch);
+    const uint32_t ml = sel(c.wrap, dpp<kShl4>(cl), dpp<kShr1>(cl));
+    const uint32_t mh = sel(c.wrap, dpp<kShl4>(ch), dpp<kShr1>(ch));
+    const uint32_t pl = dpp<kShl1>(cl), ph = dpp<kShl1>(ch);
+    lo = xor3(lo, ml, __builtin_amdgcn_alignbit(pl, ph, 31u));
+    hi = xor3(hi, mh, __builtin_amdgcn_alignbit(ph, pl, 31u));
+    const uint32_t a = sel(c.swap, lo, hi), b = sel(c.swap, hi, lo);
+    const uint32_t th = __builtin_amdgcn_alignbit(a, b, c.sh);
+    const uint32_t tl = __builtin_amdgcn_alignbit(b, a, c.sh);
+    const uint32_t bl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)c.src, (int)tl);
+    const uint32_t bh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)c.src, (int)th);
+    lo = __builtin_amdgcn_bitop3_b32(chi3(bl, dpp<kShl1>(bl), dpp<kShl2>(bl)), c.iota, rcl, 0x78);
+    hi = __builtin_amdgcn_bitop3_b32(chi3(bh, dpp<kShl1>(bh), dpp<kShl2>(bh)), c.iota, rch, 0x78);
+}
+
+#ifndef MK_SPREAD_UNROLL
+#define MK_SPREAD_UNROLL 24
+#endif
+__device__ __forceinline__ void keccak_f(uint32_t& e, uint32_t& o, const Lane& c) {
+#pragma unroll MK_SPREAD_UNROLL
+    for (int r = 0; r < 24; ++r) round_fn(e, o, c, ilv::kRcE[r], ilv::kRcO[r]);
+}
+
+__device__ __forceinline__ void keccak_f_lh(uint32_t& lo, uint32_t& hi, const LaneLH& c) {
+#pragma unroll MK_SPREAD_UNROLL
+    for (int r = 0; r < 24; ++r) round_lh(lo, hi, c, kRcLo[r], kRcHi[r]);
+}
+
+}  // namespace spread
+}  // namespace mk

@@ -249,6 +249,70 @@ __device__ __forceinline__ void hash_window256_staged(const uint4* __restrict__ 
     digest(s, d0, d1);
 }
 
+// MK_LEAF_SPLIT=1: the window without a staging buffer.  Block 1 (bytes
+// 0..135) is loaded straight into the state registers, block 2 only after
+// the first permutation, in two halves, so at most 16 data VGPRs are live
+// beside the state; the thread's held digests live in its own LDS level
+// slots (k_reduce), so the kernel fits MK_LEAF_SPLIT_WAVES waves per SIMD
+// with 16 KB of LDS per workgroup.  The 128-B line shared by both blocks is
+// fetched twice when it leaves L2 in between (infinity-cache hit).
+#ifndef MK_LEAF_SPLIT
+#define MK_LEAF_SPLIT 0
+#endif
+#ifndef MK_LEAF_SPLIT_WAVES
+#define MK_LEAF_SPLIT_WAVES 6
+#endif
+__device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w, uint4& d0, uint4& d1) {
+    State s;
+    uint4 v[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) v[k] = ld_nt(w + k);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        s.lo[2 * k] = v[k].x;
+        s.hi[2 * k] = v[k].y;
+        s.lo[2 * k + 1] = v[k].z;
+        s.hi[2 * k + 1] = v[k].w;
+    }
+    s.lo[16] = v[8].x;
+    s.hi[16] = v[8].y;
+    const uint32_t t0 = v[8].z, t1 = v[8].w;
+#pragma unroll
+    for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+    keccak_f(s);
+    asm volatile("" ::: "memory");  // block 2 loads stay after the permutation
+    s.lo[0] ^= t0;
+    s.hi[0] ^= t1;
+    {
+        uint4 u[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = ld_nt(w + 9 + k);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s.lo[1 + 2 * k] ^= u[k].x;
+            s.hi[1 + 2 * k] ^= u[k].y;
+            s.lo[2 + 2 * k] ^= u[k].z;
+            s.hi[2 + 2 * k] ^= u[k].w;
+        }
+    }
+    {
+        uint4 u[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) u[k] = ld_nt(w + 13 + k);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            s.lo[9 + 2 * k] ^= u[k].x;
+            s.hi[9 + 2 * k] ^= u[k].y;
+            s.lo[10 + 2 * k] ^= u[k].z;
+            s.hi[10 + 2 * k] ^= u[k].w;
+        }
+    }
+    s.lo[15] ^= 1u;  // byte 256 = byte 120 of block 1
+    s.hi[16] ^= 0x80000000u;
+    keccak_f_digest(s);
+    digest(s, d0, d1);
+}
+
 // ----------------------------------------------------------------------------
 // First-level node j of a reduce pass.
 //   LEAF: window j of the item buffer.
@@ -297,11 +361,13 @@ __device__ __forceinline__ void first_level_generic(const ReduceArgs& a, uint64_
 // Non-final passes write 512 >> (levels-2) nodes per workgroup; the final
 // pass (one workgroup) reduces to the root and applies the length mix-in.
 template <bool LEAF, bool FAST, int NI>
-__global__ __launch_bounds__(kReduceThreads, (MK_STAGE_LDS && LEAF && FAST) ? MK_STAGE_WAVES : MK_MIN_WAVES) void k_reduce(
+__global__ __launch_bounds__(kReduceThreads, (MK_LEAF_SPLIT && LEAF && FAST) ? MK_LEAF_SPLIT_WAVES
+                                             : (MK_STAGE_LDS && LEAF && FAST) ? MK_STAGE_WAVES : MK_MIN_WAVES) void k_reduce(
     ReduceArgs a) {
     constexpr uint64_t kSpan1 = 2 * NI * kReduceThreads;  // first-level nodes per workgroup
     constexpr uint64_t kSpan2 = kSpan1 / 2;
-    constexpr bool kStaged = MK_STAGE_LDS && LEAF && FAST;
+    constexpr bool kSplit = MK_LEAF_SPLIT && LEAF && FAST;
+    constexpr bool kStaged = !kSplit && MK_STAGE_LDS && LEAF && FAST;
     constexpr uint64_t kLdsU4 = kStaged && 8 * kReduceThreads > 2 * kSpan2 ? 8 * kReduceThreads : 2 * kSpan2;
     __shared__ uint4 lds[kLdsU4];
     const uint32_t tid = threadIdx.x;
@@ -314,7 +380,25 @@ __global__ __launch_bounds__(kReduceThreads, (MK_STAGE_LDS && LEAF && FAST) ? MK
     const uint64_t m2 = pair ? (m1 + 1) / 2 : m1;
 
     // ---- phase A: first level (+ pair level) from global memory ----------
-    if constexpr (kStaged) {
+    if constexpr (kSplit) {
+        // the left window's digest waits in the thread's own level slot (the
+        // pair node overwrites it), so no digest is held across a window
+#pragma unroll 1
+        for (int i = 0; i < NI; ++i) {
+            const uint32_t q = i * kReduceThreads + tid;
+            const uint4* w = reinterpret_cast<const uint4*>(a.items) + (lo1 + 2 * (uint64_t)q) * 16;
+            uint4 l0, l1, r0, r1, d0, d1;
+            hash_window256_split(w, d0, d1);
+            lds[2 * q] = d0;
+            lds[2 * q + 1] = d1;
+            hash_window256_split(w + 16, r0, r1);
+            l0 = lds[2 * q];
+            l1 = lds[2 * q + 1];
+            hash_pair(l0, l1, r0, r1, false, d0, d1);
+            lds[2 * q] = d0;
+            lds[2 * q + 1] = d1;
+        }
+    } else if constexpr (kStaged) {
         // The staging slots alias the level buffer: every pair node stays in
         // registers until all threads are done with their slots.
         static_assert(NI == 1 || NI == 2, "staged leaf pass holds at most 2 pair nodes");
@@ -1681,7 +1765,7 @@ __global__ __launch_bounds__(256) void k_synth(uint64_t* __restrict__ dst, uint6
 // Level d starts at node trie_level_off(cap, d) = sum_{i<d} ceil(cap/2^i).
 template <uint32_t NT>
 __global__ __launch_bounds__(NT) void k_trie_append(uint32_t* __restrict__ levels, uint64_t cap, uint32_t d0,
-                                                    uint64_t lo, uint64_t c, uint32_t depth,
+                                                    uint64_t lo, uint64_t c, uint32_t d_end, uint32_t depth,
                                                     uint32_t* __restrict__ root_out) {
     constexpr uint32_t kPairs = NT / 2;
     __shared__ uint32_t lds[2][8 * kPairs];
@@ -1692,7 +1776,7 @@ __global__ __launch_bounds__(NT) void k_trie_append(uint32_t* __restrict__ level
         capd = (capd + 1) / 2;
     }
     int buf = 0;
-    for (uint32_t d = d0; d < depth; ++d) {
+    for (uint32_t d = d0; d < d_end; ++d) {
         const uint32_t* cur = levels + 8 * off;
         uint32_t* nxt = levels + 8 * (off + capd);
         const uint64_t plo = lo >> 1, cp = (c + 1) >> 1, np = cp - plo;
@@ -1727,9 +1811,77 @@ __global__ __launch_bounds__(NT) void k_trie_append(uint32_t* __restrict__ level
         c = cp;
     }
 }
-template __global__ void k_trie_append<64>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t*);
-template __global__ void k_trie_append<256>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t*);
-template __global__ void k_trie_append<1024>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t*);
+template __global__ void k_trie_append<64>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
+                                           uint32_t*);
+template __global__ void k_trie_append<256>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
+                                            uint32_t*);
+template __global__ void k_trie_append<1024>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
+                                             uint32_t*);
+
+// The narrow right edge / top of the deposit trie with ONE STATE PER WAVE
+// (mk::spread, lo/hi form: ~6.3 k cycles per permutation on a lone wave
+// against ~12.8 k for a lane pair, profiles/r02d/lat_probe_spread.json).
+// Wave w hashes parent plo + w of every level d0 .. d_end-1 (the host
+// guarantees at most NW parents per level); level d0 and the untouched left
+// neighbours come from the level array, later children from LDS.  A missing
+// right child is 0^32 (deposit_trie.go:33-38), so once the count is 1 the
+// levels above are the zero-sibling tail.  GPU lane L holds Keccak lane i
+// (mk::spread::lane_consts): lanes i < 8 load the message words (left node
+// words 0-3, right node 4-7), i = 8 / 16 carry the 0x01 / 0x80 padding, and
+// lanes 0..3 hold the digest.
+template <uint32_t NW>
+__global__ __launch_bounds__(64 * NW) void k_trie_spread(uint32_t* __restrict__ levels, uint64_t cap, uint32_t d0,
+                                                         uint64_t lo, uint64_t c, uint32_t d_end, uint32_t depth,
+                                                         uint32_t* __restrict__ root_out) {
+    __shared__ uint2 lds[2][4 * NW];
+    const uint32_t w = threadIdx.x >> 6, L = threadIdx.x & 63u;
+    const spread::LaneLH cst = spread::lane_consts_lh(L);
+    const uint32_t i = cst.i;
+    uint64_t off = 0, capd = cap;  // node offset and capacity of level d0
+    for (uint32_t k = 0; k < d0; ++k) {
+        off += capd;
+        capd = (capd + 1) / 2;
+    }
+    int buf = 0;
+    for (uint32_t d = d0; d < d_end; ++d) {
+        const uint2* cur = reinterpret_cast<const uint2*>(levels) + 4 * off;
+        uint2* nxt = reinterpret_cast<uint2*>(levels) + 4 * (off + capd);
+        const uint64_t plo = lo >> 1, cp = (c + 1) >> 1;
+        if (w < cp - plo) {  // wave-uniform: the permutation needs every lane
+            const uint64_t j = plo + w;
+            uint32_t slo = 0u, shi = 0u;
+            if (i < 8u) {
+                const uint64_t ch = 2 * j + (i >> 2);
+                if (ch < c) {
+                    const uint2 v = (d == d0 || ch < lo) ? cur[4 * ch + (i & 3u)] : lds[buf][4 * (ch - lo) + (i & 3u)];
+                    slo = v.x;
+                    shi = v.y;
+                }
+            }
+            if (i == 8u) slo = 1u;
+            if (i == 16u) shi = 0x80000000u;
+            spread::keccak_f_lh(slo, shi, cst);
+            if (L < 4u) {
+                const uint2 h = make_uint2(slo, shi);
+                lds[buf ^ 1][4 * w + L] = h;
+                nxt[4 * j + L] = h;
+                if (d + 1 == depth && root_out) reinterpret_cast<uint2*>(root_out)[L] = h;
+            }
+        }
+        __syncthreads();
+        buf ^= 1;
+        off += capd;
+        capd = (capd + 1) / 2;
+        lo = plo;
+        c = cp;
+    }
+}
+template __global__ void k_trie_spread<1>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
+                                          uint32_t*);
+template __global__ void k_trie_spread<2>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
+                                          uint32_t*);
+template __global__ void k_trie_spread<4>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
+                                          uint32_t*);
 
 // GenerateMerkleBranch (deposit_trie.go:43-58): branch[d] = the sibling of
 // index's ancestor at level d, 0^32 when that node does not exist.

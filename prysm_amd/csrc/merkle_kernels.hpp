@@ -61,8 +61,15 @@ __global__ void k_verify_branches(const uint4* leaves, const uint4* branches, co
                                   uint32_t depth, uint32_t tree_depth, const uint4* roots, uint64_t n,
                                   uint8_t* ok);
 template <uint32_t NT>
-__global__ void k_trie_append(uint32_t* levels, uint64_t cap, uint32_t d0, uint64_t lo, uint64_t c, uint32_t depth,
-                              uint32_t* root_out);
+__global__ void k_trie_append(uint32_t* levels, uint64_t cap, uint32_t d0, uint64_t lo, uint64_t c, uint32_t d_end,
+                              uint32_t depth, uint32_t* root_out);
+#ifndef MK_TRIE_SPREAD
+#define MK_TRIE_SPREAD 1
+#endif
+constexpr uint32_t kSpreadWavesMax = 4;  // k_trie_spread: one state per wave, one wave per SIMD
+template <uint32_t NW>
+__global__ void k_trie_spread(uint32_t* levels, uint64_t cap, uint32_t d0, uint64_t lo, uint64_t c, uint32_t d_end,
+                              uint32_t depth, uint32_t* root_out);
 __global__ void k_trie_branch(const uint4* levels, uint64_t cap, uint64_t count, uint32_t depth, uint64_t index,
                               uint4* branch);
 template <bool LEAF>

@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--c2", action="store_true", help="A/B the batched Keccak of 2^log2n x 64-B messages")
     ap.add_argument("--host-struct", type=int, default=0,
                     help="A/B mk_ssz_struct_list_root from host records (this many validators)")
+    ap.add_argument("--append", type=int, default=0,
+                    help="A/B this many single-deposit appends on a 2^log2n-capacity trie (Root after each)")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -48,6 +50,8 @@ def main():
             os.path.join(ROOT, "prysm_amd", "lib", "variants", f"libprysm_merkle_{v}.so")
         libs[v] = load(p)
         assert libs[v].mk_init(0) == 0
+    if a.append:
+        return ab_append(a, libs, dev)
     if a.trie:
         return ab_trie(a, libs, dev)
     if a.struct:
@@ -123,6 +127,46 @@ def ab_trie(a, libs, dev):
     for v in a.variants:
         print(json.dumps({"variant": v, "trie_log2n": a.log2n, "median_ms": statistics.median(times[v]),
                           "min_ms": min(times[v])}))
+    print(json.dumps({"root": next(iter(roots.values()), None)}))
+
+
+def ab_append(a, libs, dev):
+    """UpdateDepositTrie + Root() latency: each variant owns a trie holding
+    2^log2n - append deposits, then appends one deposit at a time."""
+    import torch
+
+    cap, ln, depth, k = 1 << a.log2n, 280, 32, a.append
+    data = torch.empty(cap * ln, dtype=torch.uint8, device=dev)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    first = libs[a.variants[0]]
+    assert first.mk_dev_synth_fill(None, ctypes.c_void_p(data.data_ptr()), cap * ln, 0x5EED000000000005, 0, st) == 0
+    nb = first.mk_deposit_trie_levels_bytes(cap, depth)
+    lvs = {v: torch.empty(nb, dtype=torch.uint8, device=dev) for v in a.variants}
+    outs = {v: torch.empty(32, dtype=torch.uint8, device=dev) for v in a.variants}
+    base = cap - k
+    for v, L in libs.items():
+        assert L.mk_dev_deposit_trie_append(None, ctypes.c_void_p(lvs[v].data_ptr()), cap, 0,
+                                            ctypes.c_void_p(data.data_ptr()), None, base, ln, depth,
+                                            ctypes.c_void_p(outs[v].data_ptr()), st) == 0
+    torch.cuda.synchronize()
+    times = {v: [] for v in a.variants}
+    for i in range(k):
+        for v, L in libs.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = L.mk_dev_deposit_trie_append(None, ctypes.c_void_p(lvs[v].data_ptr()), cap, base + i,
+                                              ctypes.c_void_p(data.data_ptr() + (base + i) * ln), None, 1, ln, depth,
+                                              ctypes.c_void_p(outs[v].data_ptr()), st)
+            e1.record()
+            torch.cuda.synchronize()
+            assert rc == 0, (v, rc)
+            times[v].append(e0.elapsed_time(e1))
+    roots = {v: bytes(o.cpu().numpy()).hex() for v, o in outs.items()}
+    assert len(set(roots.values())) == 1, roots
+    for v in a.variants:
+        t = times[v][8:]
+        print(json.dumps({"variant": v, "append_cap_log2": a.log2n, "appends": k, "median_us": 1e3 * statistics.median(t),
+                          "min_us": 1e3 * min(t)}))
     print(json.dumps({"root": next(iter(roots.values()), None)}))
 
 
