@@ -870,6 +870,79 @@ __device__ __forceinline__ void store_node3(uint32_t* __restrict__ out, uint64_t
 
 }  // namespace
 
+// Levels of k_wave3 once a level has at most one parent per wave: ONE
+// STATE PER WAVE (mk::spread, ilv words, ~6.4 k cycles per lone-wave
+// permutation against ~12.8 k for a lane pair).  Wave w hashes parent w; the
+// nodes stay in k_wave3's LDS layout (lds[8 node + 2 word + parity]).  GPU
+// lane L holds Keccak lane i = lane_consts(L).i: i < 4 the left node's word
+// i, 4..7 the right node's, 8 / 16 (3 / 16 in the second block of a padded
+// node) the padding bits.
+#ifndef MK_WAVE3_SPREAD
+#define MK_WAVE3_SPREAD 1
+#endif
+template <uint32_t NT>
+__device__ __forceinline__ void wave3_spread_levels(uint32_t* lds, uint64_t& c, uint64_t& m, int& left, int& done,
+                                                    uint32_t pad_at_one) {
+    const uint32_t w = threadIdx.x >> 6, L = threadIdx.x & 63u;
+    const spread::Lane cst = spread::lane_consts(L);
+    const uint32_t i = cst.i;
+    while (left > 0 && (c > 1 || pad_at_one)) {
+        const uint64_t mn = (m + 1) / 2;
+        uint32_t e = 0u, o = 0u;
+        if (w < mn) {  // wave-uniform
+            const bool padded = !(2 * (uint64_t)w + 1 < m);
+            if (i < 4u) {
+                e = lds[16 * w + 2 * i];
+                o = lds[16 * w + 2 * i + 1];
+            } else if (i < 8u && !padded) {
+                e = lds[16 * w + 8 + 2 * (i - 4u)];
+                o = lds[16 * w + 8 + 2 * (i - 4u) + 1];
+            }
+            if (padded) {  // K(l || 0^128): 160 bytes, two blocks
+                spread::keccak_f(e, o, cst);
+                if (i == 3u) e ^= 1u;
+            } else if (i == 8u) {
+                e ^= 1u;
+            }
+            if (i == 16u) o ^= 0x80000000u;
+            spread::keccak_f(e, o, cst);
+        }
+        __syncthreads();
+        if (w < mn && L < 4u) {
+            lds[8 * w + 2 * L] = e;
+            lds[8 * w + 2 * L + 1] = o;
+        }
+        __syncthreads();
+        c = (c + 1) / 2;
+        m = mn;
+        --left;
+        ++done;
+    }
+}
+
+// K(root || le64(n) || 0^24) by wave 0 in spread form; plain digest to out
+__device__ __forceinline__ void wave3_spread_final(const uint32_t* lds, uint64_t n_items, uint32_t* out) {
+    const uint32_t L = threadIdx.x & 63u;
+    const spread::Lane cst = spread::lane_consts(L);
+    const uint32_t i = cst.i;
+    uint32_t e = 0u, o = 0u;
+    if (i < 4u) {
+        e = lds[2 * i];
+        o = lds[2 * i + 1];
+    } else if (i == 4u) {
+        e = ilv::to_ilv((uint32_t)n_items, (uint32_t)(n_items >> 32), 0);
+        o = ilv::to_ilv((uint32_t)n_items, (uint32_t)(n_items >> 32), 1);
+    } else if (i == 8u) {
+        e = 1u;
+    }
+    if (i == 16u) o ^= 0x80000000u;
+    spread::keccak_f(e, o, cst);
+    if (L < 4u) {
+        out[2 * L] = ilv::spread16(e) | (ilv::spread16(o) << 1);
+        out[2 * L + 1] = ilv::spread16(e >> 16) | (ilv::spread16(o >> 16) << 1);
+    }
+}
+
 template <uint32_t NT, bool LEAF>
 __global__ __launch_bounds__(NT) void k_wave3(ReduceArgs a) {
     constexpr uint32_t kSpan = NT / 2;  // first-level nodes (lane pairs) per workgroup
@@ -918,6 +991,7 @@ __global__ __launch_bounds__(NT) void k_wave3(ReduceArgs a) {
     int done = 0;
     while (left > 0 && (c > 1 || a.pad_at_one)) {
         const uint64_t mn = (m + 1) / 2;
+        if (MK_WAVE3_SPREAD && mn <= NT / 64) break;  // one parent per wave from here
         const bool act = k < mn;
         uint32_t l[4], r[4] = {0, 0, 0, 0};
         bool padded = false;
@@ -943,8 +1017,11 @@ __global__ __launch_bounds__(NT) void k_wave3(ReduceArgs a) {
         --left;
         ++done;
     }
+    if (MK_WAVE3_SPREAD) wave3_spread_levels<NT>(lds, c, m, left, done, a.pad_at_one);
     uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
-    if (a.finalize) {
+    if (MK_WAVE3_SPREAD && a.finalize) {
+        if (tid < 64) wave3_spread_final(lds, a.n_items, out);
+    } else if (a.finalize) {
         if (k == 0) {  // K(root || le64(n) || 0^24) on lanes 0/1
             ilv::Half s;
             ilv::zero(s);
