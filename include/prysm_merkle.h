@@ -254,6 +254,14 @@ int mk_deposit_trie_build(mk_call* call, const uint8_t* data, const uint64_t* of
 int mk_dev_deposit_trie_append(mk_call* call, void* d_levels, uint64_t capacity, uint64_t count, const void* d_data,
                                const uint64_t* d_offs, uint64_t k, uint32_t fixed_len, uint32_t depth,
                                void* d_root32, void* stream);
+/* Batch build front: the leaf hashes Hash(deposit) of n deposits into level 0
+ * of an empty trie plus levels 1 .. d_to (the root to d_root32 when d_to ==
+ * depth; d_root32 may be NULL otherwise).  Deposits as in
+ * mk_dev_deposit_trie_append.  With mk_dev_deposit_trie_levels(d_to, depth)
+ * this splits one batch build (deposit_trie.go:29-40) across two streams. */
+int mk_dev_deposit_trie_build(mk_call* call, void* d_levels, uint64_t capacity, const void* d_data,
+                              const uint64_t* d_offs, uint64_t n, uint32_t fixed_len, uint32_t d_to, uint32_t depth,
+                              void* d_root32, void* stream);
 /* Levels d_from+1 .. d_to of the batch build of a `count`-deposit trie whose
  * level d_from is complete (the root to d_root32 when d_to == depth): lets a
  * caller hash the leaves and the wide levels of trie i+1 on one stream while

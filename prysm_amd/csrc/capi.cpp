@@ -779,8 +779,13 @@ int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from,
     return MK_OK;
 }
 
-int trie_levels_build(void* d_levels, uint64_t cap, uint64_t n, uint32_t depth, void* d_root32, hipStream_t st) {
-    return trie_levels_range(d_levels, cap, n, 0, depth, depth, d_root32, st);
+// Batch build front over an empty trie: leaf hashes into level 0, then
+// levels 1 .. d_to.  (Fusing levels 1-2 into the 280-B leaf kernel measured
+// no faster: profiles/r02d/rejected/ab_trie_leaves4.log.)
+int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t* d_offs, uint64_t n,
+               uint32_t fixed_len, uint32_t d_to, uint32_t depth, void* d_root32, hipStream_t st) {
+    TRY(dev_leaf_hashes(d_data, d_offs, n, fixed_len, trie_level(d_levels, cap, 0), st));
+    return trie_levels_range(d_levels, cap, n, 0, d_to, depth, d_root32, st);
 }
 
 int dev_trie_append(void* d_levels, uint64_t cap, uint64_t count, const void* d_data, const uint64_t* d_offs,
@@ -792,9 +797,9 @@ int dev_trie_append(void* d_levels, uint64_t cap, uint64_t count, const void* d_
         HIPCHK(hipMemsetAsync(d_root32, 0, 32, st));
         return MK_OK;
     }
+    if (count == 0) return trie_front(d_levels, cap, d_data, d_offs, k, fixed_len, depth, depth, d_root32, st);
     // leaf hashes of the new deposits: Hash(depositData) (deposit_trie.go:32)
     TRY(dev_leaf_hashes(d_data, d_offs, k, fixed_len, trie_level(d_levels, cap, 0) + 2 * count, st));
-    if (count == 0) return trie_levels_build(d_levels, cap, k, depth, d_root32, st);
     // right edge only: level d changes on [lo, c)
     uint64_t lo = count, c = count + k;
     uint32_t d = 0;
@@ -1571,6 +1576,22 @@ int mk_dev_deposit_trie_append(mk_call* call, void* d_levels, uint64_t capacity,
     return S.done(rc ? rc
                      : dev_trie_append(d_levels, capacity, count, d_data, d_offs, k, fixed_len, depth, d_root32,
                                        (hipStream_t)stream));
+}
+
+int mk_dev_deposit_trie_build(mk_call* call, void* d_levels, uint64_t capacity, const void* d_data,
+                              const uint64_t* d_offs, uint64_t n, uint32_t fixed_len, uint32_t d_to, uint32_t depth,
+                              void* d_root32, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    rc = check_trie(capacity, 0, n, depth);
+    if (rc) return S.done(rc);
+    if (d_to > depth) return S.done(fail(MK_EINVAL, "level %u out of range (0..%u)", d_to, depth));
+    if (n == 0) return S.done(fail(MK_EINVAL, "empty trie"));
+    if (!d_levels || (d_to == depth && !d_root32) || (!d_offs && !d_data && fixed_len))
+        return S.done(fail(MK_EINVAL, "null pointer"));
+    return S.done(trie_front(d_levels, capacity, d_data, d_offs, n, fixed_len, d_to, depth,
+                             d_to == depth ? d_root32 : nullptr, (hipStream_t)stream));
 }
 
 int mk_dev_deposit_trie_levels(mk_call* call, void* d_levels, uint64_t capacity, uint64_t count, uint32_t d_from,

@@ -1698,6 +1698,7 @@ __global__ __launch_bounds__(kRecThreads) void k_keccak_rec(const uint2* __restr
 }
 template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 
+
 // Deposit-trie levels, fused: the workgroup owns input nodes
 // [512*wg, 512*wg + 512) of level d (count cin) and writes `levels` levels
 // d+1 .. d+levels to their slots of the level array (every level is kept:

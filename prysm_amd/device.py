@@ -269,6 +269,23 @@ def deposit_trie_append(levels: torch.Tensor, capacity: int, count: int, data: t
                 device=dev)
 
 
+def deposit_trie_build(levels: torch.Tensor, capacity: int, data: torch.Tensor, n: int, deposit_len: int,
+                       d_to: int, depth: int, root: torch.Tensor = None) -> torch.Tensor:
+    """Batch build front (deposit_trie.go:29-40): Hash of n fixed-length
+    deposits into level 0 of an empty trie and levels 1..d_to (the root too
+    when d_to == depth).  Returns ``levels``."""
+    dev = _dev(levels)
+    if n > capacity or levels.numel() < deposit_trie_levels_bytes(capacity, depth):
+        raise ValueError("level array smaller than the capacity layout")
+    if data.numel() * data.element_size() < n * deposit_len:
+        raise ValueError("deposit buffer shorter than n * deposit_len")
+    if d_to == depth and root is None:
+        root = torch.empty(32, dtype=torch.uint8, device=levels.device)
+    _lib.invoke("mk_dev_deposit_trie_build", _p(levels), capacity, _p(data), None, n, deposit_len, d_to, depth,
+                _p(root) if root is not None else None, _stream(levels.device), device=dev)
+    return levels
+
+
 def deposit_trie_levels(levels: torch.Tensor, capacity: int, count: int, d_from: int, d_to: int, depth: int,
                         root: torch.Tensor = None) -> None:
     """Levels d_from+1 .. d_to of the batch build (level d_from complete);

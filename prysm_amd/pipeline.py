@@ -121,9 +121,7 @@ class TriePipeline:
         if self._done[slot] is not None:
             cur.wait_event(self._done[slot])
         lv, root = self.levels[slot], self.roots[slot]
-        D.hash_batch(deposits, self.n, self.dl, out=lv[:32 * self.n])
-        if self.split:
-            D.deposit_trie_levels(lv, self.n, self.n, 0, self.split, self.depth)
+        D.deposit_trie_build(lv, self.n, deposits, self.n, self.dl, self.split, self.depth)
         self.side.wait_stream(cur)
         with torch.cuda.stream(self.side):
             D.deposit_trie_levels(lv, self.n, self.n, self.split, self.depth, self.depth, root)

@@ -182,3 +182,37 @@ def test_trie_pipeline_stream_of_tries(gpu, n):
         host = d.cpu().numpy()
         want = O.deposit_trie_levels([bytes(host[i * ln:(i + 1) * ln]) for i in range(n)])[0]
         assert roots[t] == want, (t, pipe.split)
+
+
+@pytest.mark.parametrize("n,ln", [(1, 280), (2, 280), (3, 280), (5, 280), (6, 280), (7, 280), (9, 280),
+                                  (1000, 280), (4095, 280), (1003, 44), (37, 281)])
+@pytest.mark.parametrize("d_to", [0, 1, 2, 3, 12])
+def test_build_front_levels(gpu, n, ln, d_to):
+    """mk_dev_deposit_trie_build: leaf hashes + levels 1..d_to of a batch
+    build (280-B deposits on the record kernel, 44-B on the word kernel,
+    281-B on the byte kernel), every written level against the oracle's
+    batch build, then levels d_to..depth and the root."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    depth = 12
+    cap = 1 << 12
+    data = torch.empty((n * ln + 15) // 8 * 8, dtype=torch.uint8, device=gpu)
+    D.synth_fill(data, SEED + 31 * n + ln)
+    lv = torch.zeros(D.deposit_trie_levels_bytes(cap, depth), dtype=torch.uint8, device=gpu)
+    root = torch.empty(32, dtype=torch.uint8, device=gpu)
+    D.deposit_trie_build(lv, cap, data, n, ln, d_to, depth, root if d_to == depth else None)
+    host = data.cpu().numpy()
+    want_root, want = O.deposit_trie_levels([bytes(host[i * ln:(i + 1) * ln]) for i in range(n)], depth)
+    got = lv.cpu().numpy()
+    off, capd = 0, cap
+    for d in range(d_to + 1):
+        c = len(want[d])
+        assert [bytes(got[(off + i) * 32:(off + i + 1) * 32]) for i in range(c)] == want[d], (d, n)
+        off += capd
+        capd = (capd + 1) // 2
+    if d_to < depth:
+        D.deposit_trie_levels(lv, cap, n, d_to, depth, depth, root)
+    assert bytes(root.cpu().numpy()) == want_root
