@@ -133,7 +133,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    # sub-millisecond steps (C1/C3/C5) need ~10-20 ms of work before the
+    # clocks settle: C5 0.559 ms/step after 3 warmup steps, 0.478 after 30;
+    # the 10-ms C4 step is the same after 3 or 20 (profiles/r02d/warmup.txt)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--log2n", type=int, default=28)
     ap.add_argument("--item-len", type=int, default=32)
     ap.add_argument("--cpu-sample-log2n", type=int, default=26)

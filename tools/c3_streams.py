@@ -87,7 +87,7 @@ def main():
             if kind == "serial":
                 registry(cur)
                 balances()
-            elif kind == "hi_split":
+            elif kind.endswith("_split"):
                 split(cur, side)
             elif kind.endswith("first"):
                 side.wait_stream(cur)
@@ -104,7 +104,7 @@ def main():
             final(cur)
         return step
 
-    kinds = ["serial", "hi_first", "hi_split"]
+    kinds = ["serial", "hi_first", "hi_split", "lo_split"]
     steps = {k: make(k) for k in kinds}
     times = {k: [] for k in kinds}
     want = R.state_root(reg, bal)
