@@ -701,18 +701,22 @@ uint64_t edge_max_parents(uint64_t lo, uint64_t c, uint32_t d, uint32_t d_end) {
     return m;
 }
 
-// k_trie_spread over levels d .. d_end-1 (one wave per parent, <= 4 parents)
+// k_trie_spread over levels d .. d_end-1 (one wave per parent, <= 4 parents;
+// with leaves.k > 0 it first hashes the new deposits into level 0 [lo, c))
 int launch_trie_spread(void* d_levels, uint64_t cap, uint32_t d, uint64_t lo, uint64_t c, uint32_t d_end,
-                       uint32_t depth, void* d_root32, hipStream_t st) {
-    const uint64_t m = edge_max_parents(lo, c, d, d_end);
+                       uint32_t depth, void* d_root32, hipStream_t st, mk::SpreadLeaves leaves = {}) {
+    const uint64_t m = std::max<uint64_t>(edge_max_parents(lo, c, d, d_end), leaves.k);
     uint32_t* lv = (uint32_t*)d_levels;
     uint32_t* root = (uint32_t*)d_root32;
     if (m <= 1)
-        hipLaunchKernelGGL(mk::k_trie_spread<1>, dim3(1), dim3(64), 0, st, lv, cap, d, lo, c, d_end, depth, root);
+        hipLaunchKernelGGL(mk::k_trie_spread<1>, dim3(1), dim3(64), 0, st, lv, cap, d, lo, c, d_end, depth, root,
+                           leaves);
     else if (m <= 2)
-        hipLaunchKernelGGL(mk::k_trie_spread<2>, dim3(1), dim3(128), 0, st, lv, cap, d, lo, c, d_end, depth, root);
+        hipLaunchKernelGGL(mk::k_trie_spread<2>, dim3(1), dim3(128), 0, st, lv, cap, d, lo, c, d_end, depth, root,
+                           leaves);
     else if (m <= mk::kSpreadWavesMax)
-        hipLaunchKernelGGL(mk::k_trie_spread<4>, dim3(1), dim3(256), 0, st, lv, cap, d, lo, c, d_end, depth, root);
+        hipLaunchKernelGGL(mk::k_trie_spread<4>, dim3(1), dim3(256), 0, st, lv, cap, d, lo, c, d_end, depth, root,
+                           leaves);
     else
         return fail(MK_EINVAL, "internal: trie edge of %llu parents for the spread kernel", (unsigned long long)m);
     HIPCHK(hipGetLastError());
@@ -796,6 +800,14 @@ int dev_trie_append(void* d_levels, uint64_t cap, uint64_t count, const void* d_
     if (count + k == 0) {
         HIPCHK(hipMemsetAsync(d_root32, 0, 32, st));
         return MK_OK;
+    }
+    if (MK_TRIE_SPREAD && k <= mk::kSpreadWavesMax && edge_max_parents(count, count + k, 0, depth) <=
+                                                          mk::kSpreadWavesMax) {
+        // a few deposits (powchain's one log at a time): the leaf hashes and
+        // the whole right edge in one single-workgroup launch
+        const bool w8 = !d_offs && fixed_len % 8 == 0 && ((uintptr_t)d_data % 8) == 0;
+        mk::SpreadLeaves lv{(const uint8_t*)d_data, d_offs, fixed_len, (uint32_t)k, (uint32_t)w8};
+        return launch_trie_spread(d_levels, cap, 0, count, count + k, depth, depth, d_root32, st, lv);
     }
     if (count == 0) return trie_front(d_levels, cap, d_data, d_offs, k, fixed_len, depth, depth, d_root32, st);
     // leaf hashes of the new deposits: Hash(depositData) (deposit_trie.go:32)

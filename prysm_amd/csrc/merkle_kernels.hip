@@ -1907,14 +1907,57 @@ template __global__ void k_trie_append<1024>(uint32_t*, uint64_t, uint32_t, uint
 // (mk::spread::lane_consts): lanes i < 8 load the message words (left node
 // words 0-3, right node 4-7), i = 8 / 16 carry the 0x01 / 0x80 padding, and
 // lanes 0..3 hold the digest.
+// Keccak-256 of len bytes at p (Hash(depositData), deposit_trie.go:32) in
+// spread form: per 136-B block, lane i < 17 absorbs message word i (bytes
+// past len are 0; 0x01 at byte len, 0x80 at byte 135 of the last block).
+// Result (lo, hi) on the lanes of Keccak lanes 0..3.  W8: p and len are
+// 8-byte aligned, so whole words load at once.
+template <bool W8>
+__device__ __forceinline__ void spread_sponge(const uint8_t* __restrict__ p, uint64_t len, const spread::LaneLH& c,
+                                              uint32_t& lo, uint32_t& hi) {
+    const uint64_t nb = len / 136 + 1;
+    lo = hi = 0u;
+    for (uint64_t b = 0; b < nb; ++b) {  // nb is wave-uniform
+        if (c.i < 17u) {
+            const uint64_t base = 136 * b + 8 * c.i;
+            uint64_t v = 0;
+            if (W8 && base + 8 <= len) {
+                v = *reinterpret_cast<const uint64_t*>(p + base);
+            } else {
+                for (uint32_t k = 0; k < 8; ++k) {
+                    const uint64_t o = base + k;
+                    const uint64_t byte = o < len ? p[o] : 0u;
+                    v |= byte << (8 * k);
+                }
+            }
+            if (len >= base && len < base + 8) v |= 1ull << (8 * (len - base));
+            if (b + 1 == nb && c.i == 16u) v |= 0x8000000000000000ull;
+            lo ^= (uint32_t)v;
+            hi ^= (uint32_t)(v >> 32);
+        }
+        spread::keccak_f_lh(lo, hi, c);
+    }
+}
+
 template <uint32_t NW>
 __global__ __launch_bounds__(64 * NW) void k_trie_spread(uint32_t* __restrict__ levels, uint64_t cap, uint32_t d0,
                                                          uint64_t lo, uint64_t c, uint32_t d_end, uint32_t depth,
-                                                         uint32_t* __restrict__ root_out) {
+                                                         uint32_t* __restrict__ root_out, SpreadLeaves lv) {
     __shared__ uint2 lds[2][4 * NW];
     const uint32_t w = threadIdx.x >> 6, L = threadIdx.x & 63u;
     const spread::LaneLH cst = spread::lane_consts_lh(L);
     const uint32_t i = cst.i;
+    if (w < lv.k) {  // wave w hashes new deposit w into level-0 node lo + w (d0 == 0)
+        const uint64_t a = lv.offs ? lv.offs[w] : (uint64_t)w * lv.fixed_len;
+        const uint64_t len = lv.offs ? lv.offs[w + 1] - a : lv.fixed_len;
+        uint32_t hlo, hhi;
+        if (lv.aligned8)
+            spread_sponge<true>(lv.data + a, len, cst, hlo, hhi);
+        else
+            spread_sponge<false>(lv.data + a, len, cst, hlo, hhi);
+        if (L < 4u) reinterpret_cast<uint2*>(levels)[4 * (lo + w) + L] = make_uint2(hlo, hhi);
+    }
+    __syncthreads();
     uint64_t off = 0, capd = cap;  // node offset and capacity of level d0
     for (uint32_t k = 0; k < d0; ++k) {
         off += capd;
@@ -1955,11 +1998,11 @@ __global__ __launch_bounds__(64 * NW) void k_trie_spread(uint32_t* __restrict__ 
     }
 }
 template __global__ void k_trie_spread<1>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
-                                          uint32_t*);
+                                          uint32_t*, SpreadLeaves);
 template __global__ void k_trie_spread<2>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
-                                          uint32_t*);
+                                          uint32_t*, SpreadLeaves);
 template __global__ void k_trie_spread<4>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
-                                          uint32_t*);
+                                          uint32_t*, SpreadLeaves);
 
 // GenerateMerkleBranch (deposit_trie.go:43-58): branch[d] = the sibling of
 // index's ancestor at level d, 0^32 when that node does not exist.

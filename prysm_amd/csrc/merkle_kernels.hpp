@@ -68,9 +68,17 @@ __global__ void k_trie_append(uint32_t* levels, uint64_t cap, uint32_t d0, uint6
 #define MK_TRIE_SPREAD 1
 #endif
 constexpr uint32_t kSpreadWavesMax = 4;  // k_trie_spread: one state per wave, one wave per SIMD
+// new deposits k_trie_spread hashes into level 0 first (k == 0: none)
+struct SpreadLeaves {
+    const uint8_t* data;
+    const uint64_t* offs;  // device, k+1 entries relative to data; NULL: fixed_len records
+    uint32_t fixed_len;
+    uint32_t k;
+    uint32_t aligned8;     // data, offsets / fixed_len multiples of 8
+};
 template <uint32_t NW>
 __global__ void k_trie_spread(uint32_t* levels, uint64_t cap, uint32_t d0, uint64_t lo, uint64_t c, uint32_t d_end,
-                              uint32_t depth, uint32_t* root_out);
+                              uint32_t depth, uint32_t* root_out, SpreadLeaves lv);
 __global__ void k_trie_branch(const uint4* levels, uint64_t cap, uint64_t count, uint32_t depth, uint64_t index,
                               uint4* branch);
 template <bool LEAF>
