@@ -1,5 +1,8 @@
+"""Compare tools/spread_debug (GPU dump of the spread primitives and one
+round, gpurun_out/spread_debug.json) with the CPU emulation."""
 import json, sys
-exec(open('tools/spread_emu.py').read().split('random.seed(1)')[0])
+sys.path.insert(0, 'tools')
+from spread_emu import *  # noqa: E402,F401,F403
 d=json.load(open('/root/repo/gpurun_out/spread_debug.json'))
 v=d['in'][:64]; w=d['in'][64:]; out=[d['out'][64*k:64*k+64] for k in range(22)]
 e,o=v,w

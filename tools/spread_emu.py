@@ -1,4 +1,11 @@
-import numpy as np, random
+"""CPU emulation of mk::spread (prysm_amd/csrc/keccak_dev.hpp): one Keccak
+state spread over a 64-lane wave, with the cross-lane primitives it uses
+(DPP row_shl/row_shr/row_ror with row masks, v_permlane16/32_swap,
+ds_bpermute) modelled lane by lane.  Checks both word forms (bit-interleaved
+e/o and lo/hi) against a textbook Keccak-f[1600]; tests/test_spread_layout.py
+runs it on the CPU, tools/spread_debug.hip + tools/spread_debug_cmp.py compare
+it with the primitives as the GPU executes them."""
+import random
 M32=0xFFFFFFFF
 RHO=[0,1,62,28,27,36,44,6,55,20,3,10,43,25,39,41,45,15,21,8,18,2,61,56,14]
 RC=[0x0000000000000001,0x0000000000008082,0x800000000000808A,0x8000000080008000,0x000000000000808B,0x0000000080000001,0x8000000080008081,0x8000000000008009,0x000000000000008A,0x0000000000000088,0x0000000080008009,0x000000008000000A,0x000000008000808B,0x800000000000008B,0x8000000000008089,0x8000000000008003,0x8000000000008002,0x8000000000000080,0x000000000000800A,0x800000008000000A,0x8000000080008081,0x8000000000008080,0x0000000080000001,0x8000000080008008]
@@ -71,16 +78,16 @@ def rnd(e,o,rce,rco):
     e=[(be[i]^((~b1[i])&b2[i]&M32))^(CS[i]['iota']&rce) for i in range(64)]
     o=[(bo[i]^((~c1[i])&c2[i]&M32))^(CS[i]['iota']&rco) for i in range(64)]
     return e,o
-random.seed(1)
-A=[random.getrandbits(64) for _ in range(25)]
-e=[ilv(A[c['i']],0) for c in CS]; o=[ilv(A[c['i']],1) for c in CS]
-for r in range(24): e,o=rnd(e,o,RCE[r],RCO[r])
-ref=keccak_f(A)
-got=[unilv(e[8*(i//5)+i%5],o[8*(i//5)+i%5]) for i in range(25)]
-print("match", got==ref)
-for i in range(25):
-    if got[i]!=ref[i]: print(i, hex(got[i]), hex(ref[i]))
-# lo/hi variant
+
+
+def run_ilv(A):
+    e = [ilv(A[c['i']], 0) for c in CS]
+    o = [ilv(A[c['i']], 1) for c in CS]
+    for r in range(24):
+        e, o = rnd(e, o, RCE[r], RCO[r])
+    return [unilv(e[8 * (i // 5) + i % 5], o[8 * (i // 5) + i % 5]) for i in range(25)]
+
+
 def rnd_lh(lo,hi,rcl,rch):
     cl=colsum(lo); ch=colsum(hi)
     ml=[shl(cl,4)[i] if CS[i]['wrap'] else shr(cl,1)[i] for i in range(64)]
@@ -98,7 +105,19 @@ def rnd_lh(lo,hi,rcl,rch):
     lo=[(bl[i]^((~b1[i])&b2[i]&M32))^(CS[i]['iota']&rcl) for i in range(64)]
     hi=[(bh[i]^((~c1[i])&c2[i]&M32))^(CS[i]['iota']&rch) for i in range(64)]
     return lo,hi
-lo=[A[c['i']]&M32 for c in CS]; hi=[A[c['i']]>>32 for c in CS]
-for r in range(24): lo,hi=rnd_lh(lo,hi,RC[r]&M32,RC[r]>>32)
-got=[lo[8*(i//5)+i%5]|(hi[8*(i//5)+i%5]<<32) for i in range(25)]
-print("match_lh", got==ref)
+
+
+def run_lh(A):
+    lo = [A[c['i']] & M32 for c in CS]
+    hi = [A[c['i']] >> 32 for c in CS]
+    for r in range(24):
+        lo, hi = rnd_lh(lo, hi, RC[r] & M32, RC[r] >> 32)
+    return [lo[8 * (i // 5) + i % 5] | (hi[8 * (i // 5) + i % 5] << 32) for i in range(25)]
+
+
+if __name__ == "__main__":
+    random.seed(1)
+    A = [random.getrandbits(64) for _ in range(25)]
+    ref = keccak_f(A)
+    print("match", run_ilv(A) == ref)
+    print("match_lh", run_lh(A) == ref)
