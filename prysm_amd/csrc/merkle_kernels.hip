@@ -1636,36 +1636,20 @@ __global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ 
 }
 
 // Fixed-size records of NW 8-byte words (8-B aligned; deposit leaves: 280 B
-// = 35 words = 3 blocks), grid-stride: a thread hashes records i, i+stride,
-// ...  Block b+1 of the record (or block 0 of the thread's next record) is
-// loaded while block b permutes, so only a thread's very first block waits
-// on memory; 8-B loads need no per-lane alignment select (k_keccak_words
-// spends 2 VALU per word on it).
-#ifndef MK_REC_NT
-#define MK_REC_NT 0
-#endif
+// = 35 words = 3 blocks), grid-stride; each block is loaded right before it
+// is absorbed.  8-B loads need no per-lane alignment select (k_keccak_words
+// spends 2 VALU per word on it).  Prefetching block b+1 into 34 VGPRs while
+// block b permutes was 1-2 % slower on the 2^20-deposit trie (0.588 vs
+// 0.582 ms, profiles/r02d/ab_rec_prefetch.log): the other resident waves
+// hide the load as well.
 template <int NW>
 __global__ __launch_bounds__(kRecThreads) void k_keccak_rec(const uint2* __restrict__ in, uint64_t n,
                                                             uint4* __restrict__ out) {
     constexpr int NB = NW / 17 + 1;
     const uint64_t stride = (uint64_t)gridDim.x * kRecThreads;
-    uint64_t i = (uint64_t)blockIdx.x * kRecThreads + threadIdx.x;
-    if (i >= n) return;
-    uint2 buf[17];
-    auto load = [&](uint64_t rec, int b) {
-        const uint2* p = in + rec * NW + 17 * b;
-#pragma unroll
-        for (int w = 0; w < 17; ++w) {
-#if MK_REC_NT
-            buf[w] = (17 * b + w < NW) ? ld_nt(p + w) : make_uint2(0, 0);
-#else
-            buf[w] = (17 * b + w < NW) ? p[w] : make_uint2(0, 0);
-#endif
-        }
-    };
-    load(i, 0);
 #pragma unroll 1
-    for (; i < n; i += stride) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kRecThreads + threadIdx.x; i < n; i += stride) {
+        const uint2* p = in + i * NW;
         State s;
         zero(s);
 #pragma unroll
@@ -1674,17 +1658,14 @@ __global__ __launch_bounds__(kRecThreads) void k_keccak_rec(const uint2* __restr
             for (int w = 0; w < 17; ++w) {
                 const int idx = 17 * b + w;
                 if (idx < NW) {
-                    s.lo[w] ^= buf[w].x;
-                    s.hi[w] ^= buf[w].y;
+                    const uint2 v = p[idx];
+                    s.lo[w] ^= v.x;
+                    s.hi[w] ^= v.y;
                 } else if (idx == NW) {
                     s.lo[w] ^= 1u;  // domain pad byte right after the message
                 }
             }
             if (b == NB - 1) s.hi[16] ^= 0x80000000u;
-            if (b + 1 < NB)
-                load(i, b + 1);
-            else if (i + stride < n)
-                load(i + stride, 0);
             if (b + 1 < NB)
                 keccak_f(s);
             else
