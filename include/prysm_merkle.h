@@ -165,9 +165,9 @@ int mk_dev_ssz_merkle_finish(mk_call* call, const void* d_roots, uint64_t nroots
 /* Single-process multi-device merkleHash for the cgo caller.  The items are
  * split by mk_ssz_merkle_shard_plan into `nshards` shards; shard s runs on
  * device devs[s] (devs == NULL: device s).  Every device uploads its shards
- * from its own host thread through pinned staging buffers, so the PCIe links
- * copy in parallel and a shard's passes overlap the upload of the device's
- * next shard; every shard is reduced to its frontier level (up to 1024
+ * from its own host thread (chunked async copies from the caller's buffer),
+ * so the PCIe links copy in parallel and a shard's passes overlap the upload
+ * of the device's next shard; every shard is reduced to its frontier level (up to 1024
  * nodes).  When each device holds exactly one shard the frontiers are
  * all-gathered over RCCL (xGMI); otherwise they are copied to devs[0].  The
  * top levels and the length mix-in finish on devs[0]. */

@@ -51,7 +51,7 @@ constexpr uint64_t kAppendMaxRange = 1020;  // k_trie_append<1024>: one parent p
 #ifndef MK_STAGE_BYTES
 #define MK_STAGE_BYTES (32ull << 20)
 #endif
-constexpr size_t kStageBytes = MK_STAGE_BYTES;  // pinned H2D staging slot (2 per device)
+constexpr size_t kStageBytes = MK_STAGE_BYTES;  // H2D chunk of the multi-device upload
 
 #define HIPCHK(x)                                                                            \
     do {                                                                                     \
@@ -106,9 +106,6 @@ struct DevCtx {
     // host-buffer uploads on `copy` overlapping compute on `stream`
     hipStream_t copy = nullptr;
     hipEvent_t h2d = nullptr;
-    void* stage[2] = {nullptr, nullptr};  // pinned H2D staging slots
-    hipEvent_t stage_ev[2] = {nullptr, nullptr};
-    bool stage_used[2] = {false, false};
     hipEvent_t region_ev[2] = {nullptr, nullptr};  // multi: compute of a shard region done
     bool region_used[2] = {false, false};
     SmallStage small;
@@ -156,8 +153,7 @@ int bind_dev(int dev) {
                   hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, hi) == hipSuccess &&
                   hipEventCreateWithFlags(&c->h2d, hipEventDisableTiming) == hipSuccess;
         for (int i = 0; ok && i < 2; ++i)
-            ok = hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming) == hipSuccess &&
-                 hipEventCreateWithFlags(&c->region_ev[i], hipEventDisableTiming) == hipSuccess;
+            ok = hipEventCreateWithFlags(&c->region_ev[i], hipEventDisableTiming) == hipSuccess;
         for (int i = 0; ok && i < SmallStage::kSlots; ++i)
             ok = hipEventCreateWithFlags(&c->small.ev[i], hipEventDisableTiming) == hipSuccess;
         if (!ok) {
@@ -899,24 +895,15 @@ int launch_shard(const uint8_t* d_items, uint64_t sn, uint32_t item_len, uint32_
 
 uint32_t multi_frontier(uint32_t h) { return h > 5 ? std::min<uint32_t>(10, h - 5) : 0; }
 
-// Uploads items[0, bytes) into d_dst through the device's two pinned staging
-// slots (host memcpy into slot i while slot i^1 crosses PCIe) on `copy`.
+// Uploads items[0, bytes) into d_dst on `copy`: chunked hipMemcpyAsync
+// straight from the caller's pageable buffer, i.e. the runtime's own staged
+// DMA (52-55 GB/s on one MI355X link).  The first multi-device form copied
+// through two pinned slots with a host memcpy per chunk; one host thread's
+// memcpy capped that at 22-35 GB/s (profiles/r02d/multi_host_probe.log).
 int staged_upload(DevCtx* c, uint8_t* d_dst, const uint8_t* src, size_t bytes) {
-    for (int i = 0; i < 2; ++i)
-        if (!c->stage[i] && hipHostMalloc(&c->stage[i], kStageBytes, hipHostMallocDefault) != hipSuccess) {
-            c->stage[i] = nullptr;
-            return fail(MK_ENOMEM, "hipHostMalloc(%zu) failed", kStageBytes);
-        }
-    int slot = 0;
-    for (size_t off = 0; off < bytes; off += kStageBytes) {
-        const size_t len = std::min(kStageBytes, bytes - off);
-        if (c->stage_used[slot]) HIPCHK(hipEventSynchronize(c->stage_ev[slot]));
-        std::memcpy(c->stage[slot], src + off, len);
-        HIPCHK(hipMemcpyAsync(d_dst + off, c->stage[slot], len, hipMemcpyHostToDevice, c->copy));
-        HIPCHK(hipEventRecord(c->stage_ev[slot], c->copy));
-        c->stage_used[slot] = true;
-        slot ^= 1;
-    }
+    for (size_t off = 0; off < bytes; off += kStageBytes)
+        HIPCHK(hipMemcpyAsync(d_dst + off, src + off, std::min(kStageBytes, bytes - off), hipMemcpyHostToDevice,
+                              c->copy));
     return MK_OK;
 }
 
