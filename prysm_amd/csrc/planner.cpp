@@ -72,6 +72,14 @@ constexpr uint64_t kReduceNi2MinC1 = 1ull << MK_REDUCE_NI2_MIN_LOG2;  // leaf pa
 #define MK_TOP_ONE_WG 1
 #endif
 constexpr bool kTopOneWg = MK_TOP_ONE_WG != 0;
+// The one-workgroup top pass takes the full 1024 threads even when fewer
+// pairs need them: k_wave3 switches to one state per wave once a level has
+// at most NT/64 parents, so 16 waves run the last 4 levels and the mix-in in
+// the spread form instead of 2 (256 threads) or 1.
+#ifndef MK_TOP_WG1024
+#define MK_TOP_WG1024 1
+#endif
+constexpr bool kTopWg1024 = MK_TOP_WG1024 != 0;
 
 uint32_t ilog2(uint64_t v) {
     uint32_t l = 0;
@@ -164,6 +172,7 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
             while (nt < kMidThreads && ceil_div(c1, nt / 2) > kNodeWaveWgs) nt *= 2;
             if (kTopOneWg)  // the last <= 512 pairs in one workgroup: one launch to the root
                 while (nt < kMidThreads && c1 <= kMidThreads / 2 && c1 > nt / 2) nt *= 2;
+            if (kTopWg1024 && c1 <= kMidThreads / 2) nt = kMidThreads;
         }
         // throughput pass: 2 window pairs per thread on wide passes, 1 on mid-size
         // leaf passes so they still spread over the CUs
