@@ -697,7 +697,7 @@ uint64_t edge_max_parents(uint64_t lo, uint64_t c, uint32_t d, uint32_t d_end) {
     return m;
 }
 
-// k_trie_spread over levels d .. d_end-1 (one wave per parent, <= 4 parents;
+// k_trie_spread over levels d .. d_end-1 (one wave per parent, <= 16 parents;
 // with leaves.k > 0 it first hashes the new deposits into level 0 [lo, c))
 int launch_trie_spread(void* d_levels, uint64_t cap, uint32_t d, uint64_t lo, uint64_t c, uint32_t d_end,
                        uint32_t depth, void* d_root32, hipStream_t st, mk::SpreadLeaves leaves = {}) {
@@ -710,8 +710,11 @@ int launch_trie_spread(void* d_levels, uint64_t cap, uint32_t d, uint64_t lo, ui
     else if (m <= 2)
         hipLaunchKernelGGL(mk::k_trie_spread<2>, dim3(1), dim3(128), 0, st, lv, cap, d, lo, c, d_end, depth, root,
                            leaves);
-    else if (m <= mk::kSpreadWavesMax)
+    else if (m <= 4)
         hipLaunchKernelGGL(mk::k_trie_spread<4>, dim3(1), dim3(256), 0, st, lv, cap, d, lo, c, d_end, depth, root,
+                           leaves);
+    else if (m <= 16 && m <= mk::kSpreadWavesMax)
+        hipLaunchKernelGGL(mk::k_trie_spread<16>, dim3(1), dim3(1024), 0, st, lv, cap, d, lo, c, d_end, depth, root,
                            leaves);
     else
         return fail(MK_EINVAL, "internal: trie edge of %llu parents for the spread kernel", (unsigned long long)m);
@@ -739,7 +742,7 @@ int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from,
     }
     bool root_done = false;
     while (d < d_to) {
-        if (MK_TRIE_SPREAD && c <= 2 * mk::kSpreadWavesMax) {  // the last <= 3 levels + zero-sibling tail
+        if (MK_TRIE_SPREAD && c <= 2 * mk::kSpreadWavesMax) {  // the last <= 5 levels + zero-sibling tail
             void* root = d_to == depth ? d_root32 : nullptr;
             TRY(launch_trie_spread(d_levels, cap, d, 0, c, d_to, depth, root, st));
             root_done = root != nullptr;

@@ -1984,6 +1984,8 @@ template __global__ void k_trie_spread<2>(uint32_t*, uint64_t, uint32_t, uint64_
                                           uint32_t*, SpreadLeaves);
 template __global__ void k_trie_spread<4>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
                                           uint32_t*, SpreadLeaves);
+template __global__ void k_trie_spread<16>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
+                                           uint32_t*, SpreadLeaves);
 
 // GenerateMerkleBranch (deposit_trie.go:43-58): branch[d] = the sibling of
 // index's ancestor at level d, 0^32 when that node does not exist.

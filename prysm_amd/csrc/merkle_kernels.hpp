@@ -67,7 +67,10 @@ __global__ void k_trie_append(uint32_t* levels, uint64_t cap, uint32_t d0, uint6
 #ifndef MK_TRIE_SPREAD
 #define MK_TRIE_SPREAD 1
 #endif
-constexpr uint32_t kSpreadWavesMax = 4;  // k_trie_spread: one state per wave, one wave per SIMD
+#ifndef MK_SPREAD_WAVES_MAX
+#define MK_SPREAD_WAVES_MAX 16
+#endif
+constexpr uint32_t kSpreadWavesMax = MK_SPREAD_WAVES_MAX;  // k_trie_spread: one state per wave (<= 4 per SIMD)
 // new deposits k_trie_spread hashes into level 0 first (k == 0: none)
 struct SpreadLeaves {
     const uint8_t* data;
