@@ -96,12 +96,15 @@ class TriePipeline:
 
     TOP_MAX = 1 << 17  # capi.cpp kTrieTopMax: levels at or below this width run k_trie_top3
 
-    def __init__(self, n: int, deposit_len: int, depth: int, device):
+    def __init__(self, n: int, deposit_len: int, depth: int, device, split: Optional[int] = None):
+        """``split``: the first level built on the side stream (default: the
+        first level of at most TOP_MAX nodes)."""
         self.n, self.dl, self.depth = n, deposit_len, depth
         self.device = torch.device(device)
-        split = 0
-        while split < depth and -(-n // (1 << split)) > self.TOP_MAX:
-            split += 1
+        if split is None:
+            split = 0
+            while split < depth and -(-n // (1 << split)) > self.TOP_MAX:
+                split += 1
         self.split = split
         nbytes = D.deposit_trie_levels_bytes(n, depth)
         self.levels = [torch.empty(nbytes, dtype=torch.uint8, device=self.device) for _ in range(2)]
