@@ -564,6 +564,19 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
     for (uint32_t f = nb; f < sp.nfields; ++f)
         if (sp.kind[f] != MK_FIELD_RAW || sp.len[f] != 8) layout = false;
     const uint32_t nraw = sp.nfields - nb;
+    const bool split = n <= mk::kStructSplitMaxN;  // latency-bound: 4 lanes per record
+    if (kStructReg && layout && split && nb == 3 && nraw == 6) {
+        hipLaunchKernelGGL((mk::k_struct_split<3, 6>), dim3(ceil_div(n, 64)), dim3(256), 0, st, (const uint8_t*)d_rec,
+                           n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);
+        HIPCHK(hipGetLastError());
+        return MK_OK;
+    }
+    if (kStructReg && layout && split && nb == 2 && nraw == 0) {
+        hipLaunchKernelGGL((mk::k_struct_split<2, 0>), dim3(ceil_div(n, 64)), dim3(256), 0, st, (const uint8_t*)d_rec,
+                           n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);
+        HIPCHK(hipGetLastError());
+        return MK_OK;
+    }
     if (kStructReg && layout && nb == 3 && nraw == 6) {
         hipLaunchKernelGGL((mk::k_struct_reg<3, 6>), dim3(ceil_div(n, mk::kStructThreads)), dim3(mk::kStructThreads),
                            0, st, (const uint8_t*)d_rec, n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);

@@ -1561,6 +1561,88 @@ __global__ __launch_bounds__(kStructThreads, MK_STRUCT_REG_WAVES) void k_struct_
 template __global__ void k_struct_reg<3, 6>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
 template __global__ void k_struct_reg<2, 0>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
 
+// The same layouts for SMALL registries (the 16,384-validator C1 shape),
+// where every wave runs alone on its SIMD and the cost is the chain of
+// permutation latencies, not throughput: four lanes per record.  Lanes
+// 0..NB-1 of a record hash its NB bytes fields side by side (one
+// permutation of latency instead of NB), the digests meet in LDS, and lane 0
+// hashes the struct message (2 blocks): 3 serial permutations per record
+// instead of 5.  The host takes this form while 4 lanes per record still fit
+// the chip once (n <= kStructSplitMaxN).
+template <int NB, int NRAW>
+__global__ __launch_bounds__(256) void k_struct_split(const uint8_t* __restrict__ rec, uint64_t n, StructSpec sp,
+                                                      uint32_t vec16, uint4* __restrict__ roots) {
+    static_assert(NB <= 4, "one lane per bytes field");
+    constexpr uint32_t kV = 256 / 4;  // records per workgroup
+    __shared__ uint32_t dg[NB * 8][kV];
+    const uint32_t tid = threadIdx.x, v = tid >> 2, role = tid & 3u;
+    const uint64_t i = (uint64_t)blockIdx.x * kV + v;
+    const bool live = i < n;
+    const uint8_t* r = rec + (live ? i : 0) * sp.rec_len;
+    if (live && role < (uint32_t)NB) {  // Keccak(le32(len) || bytes), one block
+        const uint32_t off = role == 0 ? sp.off[0] : role == 1 ? sp.off[1 % NB] : sp.off[2 % NB];
+        const uint32_t len = role == 0 ? sp.len[0] : role == 1 ? sp.len[1 % NB] : sp.len[2 % NB];
+        uint32_t a[16];
+        load_field16(r + off, len, vec16, a);
+        const uint32_t nd = len / 4 + 1;
+        State s;
+        zero(s);
+#pragma unroll
+        for (int q = 0; q < 18; ++q) {
+            uint32_t x = q == 0 ? len : ((uint32_t)q < nd ? a[q - 1] : 0u);
+            if ((uint32_t)q == nd) x ^= 1u;
+            if (q & 1)
+                s.hi[q / 2] ^= x;
+            else
+                s.lo[q / 2] ^= x;
+        }
+        s.hi[16] ^= 0x80000000u;
+        keccak_f_digest(s);
+        uint4 d0, d1;
+        digest(s, d0, d1);
+        const uint32_t dw[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+        for (int w = 0; w < 8; ++w) dg[8 * role + w][v] = dw[w];
+    }
+    __syncthreads();
+    if (!live || role != 0) return;
+    uint32_t raw[2 * NRAW > 0 ? 2 * NRAW : 1];
+#pragma unroll
+    for (int k = 0; k < NRAW; ++k) {
+        const uint32_t* A32 = reinterpret_cast<const uint32_t*>(r + sp.off[NB + k]);
+        raw[2 * k] = A32[0];
+        raw[2 * k + 1] = A32[1];
+    }
+    constexpr int MW = 8 * NB + 2 * NRAW;  // message dwords
+    constexpr int NBLK = 4 * MW / 136 + 1;
+    State s;
+    zero(s);
+#pragma unroll
+    for (int b = 0; b < NBLK; ++b) {
+#pragma unroll
+        for (int w = 0; w < 34; ++w) {
+            const int q = 34 * b + w;
+            uint32_t x = q < 8 * NB ? dg[q][v] : (q < MW ? raw[q - 8 * NB] : 0u);
+            if (q == MW) x ^= 1u;
+            if (b == NBLK - 1 && w == 33) x ^= 0x80000000u;
+            if (w & 1)
+                s.hi[w / 2] ^= x;
+            else
+                s.lo[w / 2] ^= x;
+        }
+        if (b + 1 < NBLK)
+            keccak_f(s);
+        else
+            keccak_f_digest(s);
+    }
+    uint4 d0, d1;
+    digest(s, d0, d1);
+    roots[2 * i] = d0;
+    roots[2 * i + 1] = d1;
+}
+template __global__ void k_struct_split<3, 6>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
+template __global__ void k_struct_split<2, 0>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
+
 // ----------------------------------------------------------------------------
 // n messages of msg_len bytes, msg_len % 8 == 0, 8-byte aligned: whole-word
 // loads only (deposit leaves: 280 B = 35 words = 3 blocks).

@@ -29,6 +29,12 @@ __global__ void k_struct_fields(const uint8_t* rec, uint64_t n, StructSpec sp, u
 __global__ void k_struct_fused(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
 template <int NB, int NRAW>
 __global__ void k_struct_reg(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
+template <int NB, int NRAW>
+__global__ void k_struct_split(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
+#ifndef MK_STRUCT_SPLIT_MAX_N
+#define MK_STRUCT_SPLIT_MAX_N 32768
+#endif
+constexpr uint64_t kStructSplitMaxN = MK_STRUCT_SPLIT_MAX_N;  // k_struct_split at or below (0: never)
 template <bool LEAF>
 __global__ void k_wave(ReduceArgs a);
 template <bool LEAF>
