@@ -291,7 +291,12 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
             HIPCHK(hipEventCreate(&rec.b));
             HIPCHK(hipEventRecord(rec.a, st));
         }
-        if (ps.wave) {
+        if (ps.sp) {
+            a.wg_base = 0;
+            const uint32_t w8 = (((uintptr_t)a.items % 8) == 0 && a.cb % 8 == 0) ? 1u : 0u;
+            hipLaunchKernelGGL(mk::k_spread_leaf, dim3(ps.nwg), dim3(1024), 0, st, a, w8);
+            HIPCHK(hipGetLastError());
+        } else if (ps.wave) {
             a.wg_base = 0;
             if (ps.w3) {
                 if (ps.leaf)

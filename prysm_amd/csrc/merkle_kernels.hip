@@ -1970,26 +1970,28 @@ template __global__ void k_trie_append<1024>(uint32_t*, uint64_t, uint32_t, uint
 // (mk::spread::lane_consts): lanes i < 8 load the message words (left node
 // words 0-3, right node 4-7), i = 8 / 16 carry the 0x01 / 0x80 padding, and
 // lanes 0..3 hold the digest.
-// Keccak-256 of len bytes at p (Hash(depositData), deposit_trie.go:32) in
-// spread form: per 136-B block, lane i < 17 absorbs message word i (bytes
-// past len are 0; 0x01 at byte len, 0x80 at byte 135 of the last block).
+// Keccak-256 of p[0, la) || 0^lz (a deposit, deposit_trie.go:32; a merkleHash
+// window, hash.go:205-222) in spread form: per 136-B block, lane i < 17
+// absorbs message word i (0x01 at byte la + lz, 0x80 at byte 135 of the
+// last block).
 // Result (lo, hi) on the lanes of Keccak lanes 0..3.  W8: p and len are
 // 8-byte aligned, so whole words load at once.
 template <bool W8>
-__device__ __forceinline__ void spread_sponge(const uint8_t* __restrict__ p, uint64_t len, const spread::LaneLH& c,
-                                              uint32_t& lo, uint32_t& hi) {
+__device__ __forceinline__ void spread_sponge(const uint8_t* __restrict__ p, uint64_t la, const spread::LaneLH& c,
+                                              uint32_t& lo, uint32_t& hi, uint64_t lz = 0) {
+    const uint64_t len = la + lz;  // the message is p[0, la) || 0^lz
     const uint64_t nb = len / 136 + 1;
     lo = hi = 0u;
     for (uint64_t b = 0; b < nb; ++b) {  // nb is wave-uniform
         if (c.i < 17u) {
             const uint64_t base = 136 * b + 8 * c.i;
             uint64_t v = 0;
-            if (W8 && base + 8 <= len) {
+            if (W8 && base + 8 <= la) {
                 v = *reinterpret_cast<const uint64_t*>(p + base);
             } else {
                 for (uint32_t k = 0; k < 8; ++k) {
                     const uint64_t o = base + k;
-                    const uint64_t byte = o < len ? p[o] : 0u;
+                    const uint64_t byte = o < la ? p[o] : 0u;
                     v |= byte << (8 * k);
                 }
             }
@@ -2068,6 +2070,98 @@ template __global__ void k_trie_spread<4>(uint32_t*, uint64_t, uint32_t, uint64_
                                           uint32_t*, SpreadLeaves);
 template __global__ void k_trie_spread<16>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
                                            uint32_t*, SpreadLeaves);
+
+// Small merkleHash leaf passes in spread form (one state per wave): a
+// workgroup of 16 waves owns 16 windows; wave w hashes window w (256 B, the
+// ragged last one, or one padded with 0^128: hash.go:205-222), then the
+// workgroup folds them through up to 4 levels in LDS (parent w on wave w,
+// K(l || r) or K(l || 0^128)), like k_wave3.  The final pass (<= 16
+// windows) continues to the root and the length mix-in.  Where a tree's
+// first level has few windows every wave runs nearly alone, and a window
+// costs 2 x 6.3 k cycles here against 2 x 12.8 k in a lane pair.
+__global__ __launch_bounds__(1024) void k_spread_leaf(ReduceArgs a, uint32_t w8) {
+    __shared__ uint2 nodes[16 * 4];
+    const uint32_t w = threadIdx.x >> 6, L = threadIdx.x & 63u;
+    const spread::LaneLH cst = spread::lane_consts_lh(L);
+    const uint32_t i = cst.i;
+    const uint64_t lo1 = (a.wg_base + blockIdx.x) * 16ull;
+    const uint64_t m1 = a.c1 - lo1 < 16 ? a.c1 - lo1 : 16;
+    if (w < m1) {  // wave-uniform
+        const uint64_t j = lo1 + w;
+        const uint64_t lo = j * 2 * a.cb;
+        uint64_t la;
+        uint32_t lz;
+        if (2 * j + 1 < a.nchunks) {
+            la = (lo + 2 * a.cb < a.total ? lo + 2 * a.cb : a.total) - lo;
+            lz = 0;
+        } else {
+            la = a.total - lo;
+            lz = 128;
+        }
+        uint32_t hlo, hhi;
+        if (w8)
+            spread_sponge<true>(a.items + lo, la, cst, hlo, hhi, lz);
+        else
+            spread_sponge<false>(a.items + lo, la, cst, hlo, hhi, lz);
+        if (L < 4u) nodes[4 * w + L] = make_uint2(hlo, hhi);
+    }
+    __syncthreads();
+    uint64_t c = a.c1, m = m1;
+    int left = a.finalize ? 64 : (int)a.levels - 1;
+    int done = 0;
+    while (left > 0 && (c > 1 || a.pad_at_one)) {
+        const uint64_t mn = (m + 1) / 2;
+        uint32_t slo = 0u, shi = 0u;
+        if (w < mn) {
+            const bool padded = !(2 * (uint64_t)w + 1 < m);
+            if (i < 4u) {
+                const uint2 v = nodes[8 * w + i];
+                slo = v.x;
+                shi = v.y;
+            } else if (i < 8u && !padded) {
+                const uint2 v = nodes[8 * w + i];  // node 2w+1, word i-4
+                slo = v.x;
+                shi = v.y;
+            }
+            if (padded) {  // 160 bytes: two blocks
+                spread::keccak_f_lh(slo, shi, cst);
+                if (i == 3u) slo ^= 1u;
+            } else if (i == 8u) {
+                slo ^= 1u;
+            }
+            if (i == 16u) shi ^= 0x80000000u;
+            spread::keccak_f_lh(slo, shi, cst);
+        }
+        __syncthreads();
+        if (w < mn && L < 4u) nodes[4 * w + L] = make_uint2(slo, shi);
+        __syncthreads();
+        c = (c + 1) / 2;
+        m = mn;
+        --left;
+        ++done;
+    }
+    uint2* out = reinterpret_cast<uint2*>(a.out);
+    if (a.finalize) {
+        if (w == 0) {  // K(root || le64(n) || 0^24)
+            uint32_t slo = 0u, shi = 0u;
+            if (i < 4u) {
+                const uint2 v = nodes[i];
+                slo = v.x;
+                shi = v.y;
+            } else if (i == 4u) {
+                slo = (uint32_t)a.n_items;
+                shi = (uint32_t)(a.n_items >> 32);
+            } else if (i == 8u) {
+                slo = 1u;
+            }
+            if (i == 16u) shi ^= 0x80000000u;
+            spread::keccak_f_lh(slo, shi, cst);
+            if (L < 4u) out[L] = make_uint2(slo, shi);
+        }
+    } else if (w < m && L < 4u) {
+        out[4 * ((lo1 >> done) + w) + L] = nodes[4 * w + L];
+    }
+}
 
 // GenerateMerkleBranch (deposit_trie.go:43-58): branch[d] = the sibling of
 // index's ancestor at level d, 0^32 when that node does not exist.

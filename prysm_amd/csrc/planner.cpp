@@ -80,6 +80,12 @@ constexpr bool kTopOneWg = MK_TOP_ONE_WG != 0;
 #define MK_TOP_WG1024 1
 #endif
 constexpr bool kTopWg1024 = MK_TOP_WG1024 != 0;
+// leaf passes of at most this many windows: k_spread_leaf (0: never)
+#ifndef MK_SPREAD_LEAF_MAX_LOG2
+#define MK_SPREAD_LEAF_MAX_LOG2 12
+#endif
+constexpr uint64_t kSpreadLeafMaxC1 = MK_SPREAD_LEAF_MAX_LOG2 < 0 ? 0 : 1ull << MK_SPREAD_LEAF_MAX_LOG2;
+constexpr uint64_t kSpreadSpan = 16;  // windows per k_spread_leaf workgroup
 
 uint32_t ilog2(uint64_t v) {
     uint32_t l = 0;
@@ -163,8 +169,9 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
             hashes += (double)ceil_div(cin, 2);
         }
         uint64_t c = c1;
-        const bool wave = c1 <= (leaf || !kWave3 ? kLeafWaveMaxC1 : kNodeWaveMaxC1);
-        const bool w3 = kWave3 && wave && (!leaf || kLeafWave3);
+        const bool sp = leaf && c1 <= kSpreadLeafMaxC1;
+        const bool wave = sp || c1 <= (leaf || !kWave3 ? kLeafWaveMaxC1 : kNodeWaveMaxC1);
+        const bool w3 = !sp && kWave3 && wave && (!leaf || kLeafWave3);
         // k_wave3: the smallest workgroup (64..1024 threads, 2 per pair) that
         // keeps the pass within ~256 workgroups, one per CU
         uint32_t nt = w3 ? kWaveThreads : (wave ? kWaveThreads : kReduceThreads);
@@ -177,9 +184,12 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         // throughput pass: 2 window pairs per thread on wide passes, 1 on mid-size
         // leaf passes so they still spread over the CUs
         const uint32_t ni = (!wave && leaf && c1 < kReduceNi2MinC1) ? 1 : 2;
-        const uint64_t span = w3 ? nt / 2 : wave ? (kWave2 ? kWave2Span : kWaveThreads) : (uint64_t)2 * ni * kReduceThreads;
+        if (sp) nt = 1024;
+        const uint64_t span = sp ? kSpreadSpan
+                            : w3 ? nt / 2 : wave ? (kWave2 ? kWave2Span : kWaveThreads) : (uint64_t)2 * ni * kReduceThreads;
         const bool final_pass = c1 <= span;
-        const uint32_t max_lv = w3 ? 1 + ilog2(nt / 2) : wave ? (kWave2 ? kWave2Levels : kWaveLevels) : kMaxPassLevels;
+        const uint32_t max_lv = sp ? 1 + ilog2(kSpreadSpan)
+                              : w3 ? 1 + ilog2(nt / 2) : wave ? (kWave2 ? kWave2Levels : kWaveLevels) : kMaxPassLevels;
         uint32_t lv = final_pass ? remaining : std::min<uint32_t>(max_lv, remaining);
         for (uint32_t l = 1; l < lv; ++l) {  // fused levels above the first
             if (c <= 1 && !pad_at_one) break;
@@ -193,6 +203,7 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         ps.nt = nt;
         a.in_ilv = (w3 && !leaf && !p.passes.empty() && p.passes.back().w3) ? 1 : 0;
         ps.w3 = w3;
+        ps.sp = sp;
         a.out_ilv = w3 ? 1 : 0;  // cleared below for the final pass
         a.levels = lv;
         ps.nwg = ceil_div(c1, span);

@@ -39,6 +39,7 @@ struct Pass {
     bool wave;  // latency pass (k_wave*) instead of the throughput pass (k_reduce)
     uint64_t nwg, nfast;
     bool w3;      // k_wave3 (bit-interleaved latency form)
+    bool sp;      // k_spread_leaf (one state per wave, 16 windows per workgroup)
     uint32_t nt;  // threads per workgroup
     uint32_t ni;  // k_reduce: window pairs per thread (span 512 * ni)
     ReduceArgs a;
