@@ -33,10 +33,7 @@ constexpr bool kSidePrio = MK_SIDE_PRIO != 0;  // library side/copy streams at h
 #ifndef MK_REC_KERNEL
 #define MK_REC_KERNEL 1
 #endif
-constexpr bool kRecKernel = MK_REC_KERNEL != 0;
-#ifndef MK_REC_STAGE
-#define MK_REC_STAGE 0  // k_keccak_rec_lds (LDS-staged record blocks) for 280-B deposit leaves
-#endif  // k_keccak_rec<35> for 280-B deposit leaves
+constexpr bool kRecKernel = MK_REC_KERNEL != 0;  // k_keccak_rec<35> for 280-B deposit leaves
 #ifndef MK_STRUCT_FUSED
 #define MK_STRUCT_FUSED 1
 #endif
@@ -372,10 +369,6 @@ int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, 
     const uint64_t grid = ceil_div(n, 256);
     if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0)
         hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
-    else if (MK_REC_STAGE && kRecKernel && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 &&
-             ((uintptr_t)d_out % 16) == 0)
-        hipLaunchKernelGGL((mk::k_keccak_rec_lds<35>), dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint2*)d_in, n,
-                           (uint4*)d_out);
     else if (kRecKernel && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0)
         hipLaunchKernelGGL((mk::k_keccak_rec<35>),
                            dim3(std::min<uint64_t>(ceil_div(n, mk::kRecThreads), mk::kRecGridMax)),

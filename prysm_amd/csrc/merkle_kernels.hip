@@ -1761,60 +1761,6 @@ __global__ __launch_bounds__(kRecThreads) void k_keccak_rec(const uint2* __restr
 }
 template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 
-// LDS-staged form (MK_REC_STAGE=1): per block, the workgroup loads its 256
-// records' 136-B block slices with consecutive lanes on consecutive words
-// (a wave touches ~5 lines per load instead of 64 strided ones) into LDS,
-// then every thread absorbs its own slice from there.
-#ifndef MK_REC_STAGE
-#define MK_REC_STAGE 0
-#endif
-template <int NW>
-__global__ __launch_bounds__(256) void k_keccak_rec_lds(const uint2* __restrict__ in, uint64_t n,
-                                                        uint4* __restrict__ out) {
-    constexpr int NB = NW / 17 + 1;
-    __shared__ uint2 blk[256 * 17];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t base = (uint64_t)blockIdx.x * 256;
-    const uint32_t nrec = n - base < 256 ? (uint32_t)(n - base) : 256u;
-    State s;
-    zero(s);
-#pragma unroll 1
-    for (int b = 0; b < NB; ++b) {
-        const uint32_t wpb = (17 * (b + 1) <= NW) ? 17u : (uint32_t)(NW - 17 * b);  // words of this block
-        __syncthreads();  // the previous block's slices are absorbed
-        for (uint32_t k = tid; k < nrec * wpb; k += 256) {
-            const uint32_t r = k / wpb, w = k - r * wpb;
-            blk[17 * r + w] = in[(base + r) * NW + 17 * b + w];
-        }
-        __syncthreads();
-        if (tid < nrec) {
-#pragma unroll
-            for (int w = 0; w < 17; ++w) {
-                const int idx = 17 * b + w;
-                if (idx < NW) {
-                    const uint2 v = blk[17 * tid + w];
-                    s.lo[w] ^= v.x;
-                    s.hi[w] ^= v.y;
-                } else if (idx == NW) {
-                    s.lo[w] ^= 1u;
-                }
-            }
-            if (b == NB - 1) s.hi[16] ^= 0x80000000u;
-            if (b + 1 < NB)
-                keccak_f(s);
-            else
-                keccak_f_digest(s);
-        }
-    }
-    if (tid < nrec) {
-        uint4 d0, d1;
-        digest(s, d0, d1);
-        out[2 * (base + tid)] = d0;
-        out[2 * (base + tid) + 1] = d1;
-    }
-}
-template __global__ void k_keccak_rec_lds<35>(const uint2*, uint64_t, uint4*);
-
 
 // Deposit-trie levels, fused: the workgroup owns input nodes
 // [512*wg, 512*wg + 512) of level d (count cin) and writes `levels` levels

@@ -50,8 +50,6 @@ __global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
 __global__ void k_keccak_words(const uint2* in, uint64_t n, uint32_t nwords, uint4* out);
 template <int NW>
 __global__ void k_keccak_rec(const uint2* in, uint64_t n, uint4* out);
-template <int NW>
-__global__ void k_keccak_rec_lds(const uint2* in, uint64_t n, uint4* out);
 
 #ifndef MK_REC_THREADS
 #define MK_REC_THREADS 256
