@@ -283,6 +283,17 @@ void mk_deposit_trie_free(mk_trie* t);
 uint64_t mk_deposit_trie_count(const mk_trie* t);
 /* Appends k deposits (host data, message i = data[offs[i], offs[i+1])). */
 int mk_deposit_trie_append(mk_call* call, mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k);
+/* powchain's deposit-log loop in one call (ProcessDepositLog -> saveInTrie,
+ * powchain/service.go:248-258, 379-386): for each of the k logs in order,
+ * deposit j (data[offs[j], offs[j+1])) is appended iff the trie's Root()
+ * before it equals log_roots[32 j .. 32 j + 32) (the merkle root the log
+ * carries); a mismatching log is skipped, as the reference skips a log
+ * whose saveInTrie fails, and processing continues with the next log.
+ * accepted[j] = 1 if deposit j was appended, else 0.  All roots are
+ * computed on the device in parallel (one chain of `depth` permutations
+ * per log), so a batch costs about one append. */
+int mk_deposit_trie_save_logs(mk_call* call, mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k,
+                              const uint8_t* log_roots, uint8_t* accepted);
 int mk_deposit_trie_root(mk_call* call, mk_trie* t, uint8_t root[32]);
 /* depth x 32 bytes: GenerateMerkleBranch(index). */
 int mk_deposit_trie_branch(mk_call* call, mk_trie* t, uint64_t index, uint8_t* branch);

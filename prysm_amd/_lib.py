@@ -90,6 +90,7 @@ _SIGS = {
     "mk_deposit_trie_free": (None, [_vp]),
     "mk_deposit_trie_count": (_u64, [_vp]),
     "mk_deposit_trie_append": (_int, [_cp, _vp, _vp, _vp, _u64]),
+    "mk_deposit_trie_save_logs": (_int, [_cp, _vp, _vp, _vp, _u64, _vp, _vp]),
     "mk_deposit_trie_root": (_int, [_cp, _vp, _vp]),
     "mk_deposit_trie_branch": (_int, [_cp, _vp, _u64, _vp]),
     "mk_deposit_trie_leaves": (_int, [_cp, _vp, _u64, _u64, _vp]),

@@ -1724,9 +1724,10 @@ void mk_deposit_trie_free(mk_trie* t) {
 
 uint64_t mk_deposit_trie_count(const mk_trie* t) { return t ? t->count : 0; }
 
-static int trie_append(mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k) {
-    if (!t || (k && !offs)) return fail(MK_EINVAL, "null pointer");
-    std::lock_guard<std::mutex> tl(t->mu);
+// keep == nullptr: synchronous (the caller's buffers may die on return);
+// otherwise the relative offsets live in *keep and the caller synchronizes.
+static int trie_append_locked(mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k,
+                              std::vector<uint64_t>* keep = nullptr) {
     if (k == 0) return MK_OK;
     TRY(check_trie(UINT64_MAX, t->count, k, t->depth));
     TRY(bind_dev(t->dev));
@@ -1747,12 +1748,19 @@ static int trie_append(mk_trie* t, const uint8_t* data, const uint64_t* offs, ui
     }
     const uint64_t* d_offs = nullptr;
     uint32_t fixed = 0;
-    std::vector<uint64_t> rel;
+    std::vector<uint64_t> own;
+    std::vector<uint64_t>& rel = keep ? *keep : own;
     TRY(upload_deposits(c, t->in, t->offs, data, offs, k, &d_offs, &fixed, rel));
     TRY(dev_trie_append(t->levels.p, t->cap, t->count, t->in.p, d_offs, k, fixed, t->depth, t->root.p, st));
-    HIPCHK(hipStreamSynchronize(st));  // the caller's buffers and `rel` are released after this
+    if (!keep) HIPCHK(hipStreamSynchronize(st));  // the caller's buffers and `rel` are released after this
     t->count += k;
     return MK_OK;
+}
+
+static int trie_append(mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k) {
+    if (!t || (k && !offs)) return fail(MK_EINVAL, "null pointer");
+    std::lock_guard<std::mutex> tl(t->mu);
+    return trie_append_locked(t, data, offs, k);
 }
 
 int mk_deposit_trie_append(mk_call* call, mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k) {
@@ -1760,9 +1768,7 @@ int mk_deposit_trie_append(mk_call* call, mk_trie* t, const uint8_t* data, const
     return S.done(trie_append(t, data, offs, k));
 }
 
-static int trie_root(mk_trie* t, uint8_t* root) {
-    if (!t || !root) return fail(MK_EINVAL, "null pointer");
-    std::lock_guard<std::mutex> tl(t->mu);
+static int trie_root_locked(mk_trie* t, uint8_t* root) {
     if (t->count == 0) {
         std::memset(root, 0, 32);
         return MK_OK;
@@ -1773,9 +1779,76 @@ static int trie_root(mk_trie* t, uint8_t* root) {
     return MK_OK;
 }
 
+static int trie_root(mk_trie* t, uint8_t* root) {
+    if (!t || !root) return fail(MK_EINVAL, "null pointer");
+    std::lock_guard<std::mutex> tl(t->mu);
+    return trie_root_locked(t, root);
+}
+
 int mk_deposit_trie_root(mk_call* call, mk_trie* t, uint8_t root[32]) {
     Scope S(call);
     return S.done(trie_root(t, root));
+}
+
+// saveInTrie over a batch of logs (service.go:379-386 called per log by
+// ProcessDepositLog :248-258, which skips a log whose check fails): in log
+// order, deposit j is appended iff Root() before it equals log_roots[j].
+// A round appends every remaining deposit at once, computes the root after
+// each (k_trie_prefix_roots) and compares on the host; at the first
+// mismatch the trie is cut back to the deposits before it (the right edge
+// of the new last leaf recomputed) and the next round starts after the
+// skipped log.
+static int trie_save_logs(mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k,
+                          const uint8_t* log_roots, uint8_t* accepted) {
+    if (!t || (k && (!offs || !log_roots || !accepted))) return fail(MK_EINVAL, "null pointer");
+    std::lock_guard<std::mutex> tl(t->mu);
+    uint64_t pos = 0;
+    while (pos < k) {
+        const uint64_t m = k - pos;
+        const uint64_t count0 = t->count;
+        TRY(bind_dev(t->dev));
+        hipStream_t st = ctx()->stream;
+        // d_roots[f] = Root() before log pos + f: [0] the current root, [1..m]
+        // the root after each appended deposit (the last one is the append's)
+        TRY(grow(t->branch, std::max<size_t>(32 * (size_t)t->depth, 32 * (m + 1))));
+        uint8_t* d_roots = (uint8_t*)t->branch.p;
+        if (count0)
+            HIPCHK(hipMemcpyAsync(d_roots, t->root.p, 32, hipMemcpyDeviceToDevice, st));
+        else
+            HIPCHK(hipMemsetAsync(d_roots, 0, 32, st));
+        std::vector<uint64_t> rel;
+        TRY(trie_append_locked(t, data, offs + pos, m, &rel));
+        if (m > 1) {  // one wave per prefix, one wave per SIMD
+            hipLaunchKernelGGL((mk::k_trie_prefix_roots<4>), dim3(ceil_div(m - 1, 4)), dim3(256), 0, st,
+                               (const uint4*)t->levels.p, t->cap, count0, m - 1, t->depth, (uint4*)(d_roots + 32));
+            HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipMemcpyAsync(d_roots + 32 * m, t->root.p, 32, hipMemcpyDeviceToDevice, st));
+        std::vector<uint8_t> roots(32 * (m + 1));
+        HIPCHK(hipMemcpyAsync(roots.data(), d_roots, 32 * (m + 1), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        uint64_t f = 0;
+        while (f < m && std::memcmp(roots.data() + 32 * f, log_roots + 32 * (pos + f), 32) == 0) {
+            accepted[pos + f] = 1;
+            ++f;
+        }
+        if (f == m) break;
+        accepted[pos + f] = 0;  // skipped; the deposits after it were appended tentatively
+        t->count = count0 + f;
+        if (t->count) {  // recompute the last leaf's path without the cut deposits
+            TRY(launch_trie_spread(t->levels.p, t->cap, 0, t->count - 1, t->count, t->depth, t->depth, t->root.p,
+                                   st));
+            HIPCHK(hipStreamSynchronize(st));
+        }
+        pos += f + 1;
+    }
+    return MK_OK;
+}
+
+int mk_deposit_trie_save_logs(mk_call* call, mk_trie* t, const uint8_t* data, const uint64_t* offs, uint64_t k,
+                              const uint8_t* log_roots, uint8_t* accepted) {
+    Scope S(call);
+    return S.done(trie_save_logs(t, data, offs, k, log_roots, accepted));
 }
 
 static int trie_branch(mk_trie* t, uint64_t index, uint8_t* branch) {

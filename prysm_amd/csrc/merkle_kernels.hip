@@ -2163,6 +2163,75 @@ __global__ __launch_bounds__(1024) void k_spread_leaf(ReduceArgs a, uint32_t w8)
     }
 }
 
+// Root() after each of m deposits appended at count0 (powchain's saveInTrie
+// reads Root() before every UpdateDepositTrie, service.go:379-386): wave g
+// walks leaf i = count0 + g to the top in spread form.  At level d the path
+// node p = i >> d is a right child (p odd: its left sibling p - 1 covers only
+// leaves < i, a complete subtree, so the level array holds its final value)
+// or a left child (the right sibling lies past the prefix: 0^32), so the m
+// prefix roots are m independent 32-permutation chains over the level array
+// the batched append left behind.  The left siblings of a chain go to LDS
+// first (lane d loads level d's), then the chain runs with no global loads.
+template <uint32_t NW>
+__global__ __launch_bounds__(64 * NW) void k_trie_prefix_roots(const uint4* __restrict__ levels, uint64_t cap,
+                                                               uint64_t count0, uint64_t m, uint32_t depth,
+                                                               uint4* __restrict__ roots) {
+    __shared__ uint4 sib[NW][64][2];
+    const uint32_t w = threadIdx.x >> 6, L = threadIdx.x & 63u;
+    const uint64_t g = (uint64_t)blockIdx.x * NW + w;
+    const bool live = g < m;  // wave-uniform
+    const uint64_t i = count0 + (live ? g : 0);
+    if (live && L < depth && ((i >> L) & 1u)) {
+        uint64_t off = 0, capd = cap;
+        for (uint32_t d = 0; d < L; ++d) {
+            off += capd;
+            capd = (capd + 1) / 2;
+        }
+        const uint64_t node = off + (i >> L) - 1;
+        sib[w][L][0] = levels[2 * node];
+        sib[w][L][1] = levels[2 * node + 1];
+    }
+    __syncthreads();
+    if (!live) return;
+    const spread::LaneLH cst = spread::lane_consts_lh(L);
+    const uint32_t ci = cst.i;
+    uint32_t plo = 0u, phi = 0u;  // the path node's word ci on lanes ci < 4
+    if (ci < 4u) {
+        const uint2 v = reinterpret_cast<const uint2*>(levels)[4 * i + ci];
+        plo = v.x;
+        phi = v.y;
+    }
+    for (uint32_t d = 0; d < depth; ++d) {
+        const bool right = ((i >> d) & 1u) != 0;  // wave-uniform
+        // path words moved to Keccak lanes 4..7 (GPU lanes 0..3 hold 0..3)
+        const uint32_t src = 4u * ((ci - 4u) & 3u);
+        const uint32_t mlo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)plo);
+        const uint32_t mhi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)phi);
+        uint32_t lo = 0u, hi = 0u;
+        if (ci < 4u) {
+            if (right) {
+                const uint4 h = sib[w][d][ci >> 1];
+                lo = (ci & 1u) ? h.z : h.x;
+                hi = (ci & 1u) ? h.w : h.y;
+            } else {
+                lo = plo;
+                hi = phi;
+            }
+        } else if (ci < 8u && right) {
+            lo = mlo;
+            hi = mhi;
+        } else if (ci == 8u) {
+            lo = 1u;
+        }
+        if (ci == 16u) hi = 0x80000000u;
+        spread::keccak_f_lh(lo, hi, cst);
+        plo = lo;
+        phi = hi;
+    }
+    if (L < 4u) reinterpret_cast<uint2*>(roots)[4 * g + L] = make_uint2(plo, phi);
+}
+template __global__ void k_trie_prefix_roots<4>(const uint4*, uint64_t, uint64_t, uint64_t, uint32_t, uint4*);
+
 // GenerateMerkleBranch (deposit_trie.go:43-58): branch[d] = the sibling of
 // index's ancestor at level d, 0^32 when that node does not exist.
 __global__ void k_trie_branch(const uint4* __restrict__ levels, uint64_t cap, uint64_t count, uint32_t depth,

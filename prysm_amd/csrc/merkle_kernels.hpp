@@ -89,6 +89,9 @@ struct SpreadLeaves {
 template <uint32_t NW>
 __global__ void k_trie_spread(uint32_t* levels, uint64_t cap, uint32_t d0, uint64_t lo, uint64_t c, uint32_t d_end,
                               uint32_t depth, uint32_t* root_out, SpreadLeaves lv);
+template <uint32_t NW>
+__global__ void k_trie_prefix_roots(const uint4* levels, uint64_t cap, uint64_t count0, uint64_t m, uint32_t depth,
+                                    uint4* roots);
 __global__ void k_trie_branch(const uint4* levels, uint64_t cap, uint64_t count, uint32_t depth, uint64_t index,
                               uint4* branch);
 template <bool LEAF>

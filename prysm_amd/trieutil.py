@@ -102,6 +102,36 @@ class DepositTrie:
                     device=self._device)
         self._queue = []
 
+    def save_logs(self, deposits: Sequence[bytes], log_roots: Sequence[bytes]) -> List[bool]:
+        """powchain's ProcessDepositLog -> saveInTrie loop over a batch of logs
+        (beacon-chain/powchain/service.go:248-258, 379-386) in one device call:
+        in log order, deposit j is appended iff Root() before it equals
+        log_roots[j], else the log is skipped.  Returns the per-log accept
+        flags; the roots are computed on the device in parallel."""
+        if len(deposits) != len(log_roots):
+            raise ValueError("one merkle root per log")
+        self._flush()
+        k = len(deposits)
+        if k == 0:
+            return []
+        if self._handle is None:
+            h = ctypes.c_void_p()
+            _lib.invoke("mk_deposit_trie_new", self.depth, max(self._capacity, k), ctypes.byref(h),
+                        device=self._device)
+            self._handle = h
+        data, offs = _flatten([bytes(d) for d in deposits])
+        roots = b"".join(bytes(r) for r in log_roots)
+        if len(roots) != 32 * k:
+            raise ValueError("log roots are 32 bytes")
+        acc = ctypes.create_string_buffer(k)
+        _lib.invoke("mk_deposit_trie_save_logs", self._handle, _ptr(data), _ptr(offs), k, roots, acc,
+                    device=self._device)
+        flags = [b == 1 for b in acc.raw]
+        self.deposit_count += sum(flags)
+        return flags
+
+    SaveLogs = save_logs
+
     def generate_merkle_branch(self, index: int) -> List[bytes]:
         """GenerateMerkleBranch (deposit_trie.go:43-58): the sibling at each of
         the `depth` levels; missing nodes read as 0^32."""

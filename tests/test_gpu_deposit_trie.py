@@ -216,3 +216,48 @@ def test_build_front_levels(gpu, n, ln, d_to):
     if d_to < depth:
         D.deposit_trie_levels(lv, cap, n, d_to, depth, depth, root)
     assert bytes(root.cpu().numpy()) == want_root
+
+
+@pytest.mark.parametrize("start,k,bad", [(0, 1, ()), (0, 40, (0,)), (5, 40, (3, 4, 17, 39)), (1000, 3000, (7, 1500, 2999)),
+                                         (77, 64, tuple(range(0, 64, 2))), (10, 20, tuple(range(20)))])
+def test_save_logs_matches_reference_loop(gpu, start, k, bad):
+    """mk_deposit_trie_save_logs against the reference's per-log loop
+    (ProcessDepositLog -> saveInTrie, powchain/service.go:248-258, 379-386)
+    run on the dict restatement of deposit_trie.go: each log carries the root
+    the trie had before its deposit, except the `bad` ones (a wrong root:
+    the reference skips them and goes on).  Accept flags, Root() and
+    branches must agree."""
+    import random
+
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    rng = random.Random(start * 7919 + k)
+    t, ref = T.DepositTrie(32), O.DictTrie(32)
+    for i in range(start):  # history before the batch
+        d = _deposit(i)
+        t.UpdateDepositTrie(d)
+        ref.update(d)
+    deps = [_deposit(start + i, 280 if i % 5 else 200) for i in range(k)]
+    roots, want = [], []
+    for j, d in enumerate(deps):
+        r = ref.root()
+        if j in bad:
+            r = bytes(rng.getrandbits(8) for _ in range(32))
+        roots.append(r)
+        ok = ref.root() == r
+        want.append(ok)
+        if ok:
+            ref.update(d)
+    got = t.save_logs(deps, roots)
+    assert got == want
+    assert t.Root() == ref.root()
+    n = ref.count
+    for idx in sorted({0, n // 2, n - 1}):
+        if n:
+            assert t.GenerateMerkleBranch(idx) == ref.branch(idx), idx
+    # the trie keeps working as a plain trie afterwards
+    extra = _deposit(start + k + 1)
+    t.UpdateDepositTrie(extra)
+    ref.update(extra)
+    assert t.Root() == ref.root()
