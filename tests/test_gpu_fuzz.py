@@ -1,0 +1,163 @@
+"""Seeded random shapes through every device path against the CPU oracle
+(oracle/: C restatement of hash.go / deposit_trie.go / merkleRoot.go):
+merkleHash at random sizes, item lengths and byte offsets (every planner
+branch: spread leaf passes, lane-pair passes, fused throughput passes),
+many lists per call, struct roots of random layouts (both struct kernels
+and the generic one), deposit tries grown by random batches with the
+per-log check, and MerkleRoot.  Sizes keep the oracle to seconds."""
+import random
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED000000000000 + 1400
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+
+    from prysm_amd import _lib
+
+    assert torch.cuda.is_available()
+    assert _lib.device_count() >= 1
+    return torch.device("cuda:0")
+
+
+def _item_len(rng):
+    return rng.choice([1, 2, 3, 4, 7, 8, 16, 31, 32, 33, 48, 64, 96, 100, 128, 129, 200, 255, 280, 300])
+
+
+def test_fuzz_merkle_hash(gpu):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    rng = random.Random(SEED)
+    for case in range(400):
+        il = _item_len(rng)
+        n = int(2 ** rng.uniform(0, 17.5))
+        n = min(n, (3 << 20) // il)
+        if rng.random() < 0.1:
+            n = rng.choice([0, 1, 2, 3, 4, 5, 16, 17, 255, 256, 257])
+        off = rng.choice([0, 0, 0, 8, 4, 1, 3])
+        host = O.splitmix_bytes(n * il + off + 16, SEED + case)
+        dev_buf = torch.from_numpy(host.copy()).to(gpu)
+        items = dev_buf[off:off + max(n * il, 1)]
+        got = bytes(D.merkle_hash(items, n, il).cpu().numpy())
+        assert got == O.merkle_hash_flat(host[off:off + n * il], n, il), (case, n, il, off)
+
+
+def test_fuzz_merkle_many(gpu):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    rng = random.Random(SEED + 1)
+    for case in range(60):
+        k = rng.randint(1, 40)
+        ns, ils, offs, pos = [], [], [], 0
+        for _ in range(k):
+            il = _item_len(rng)
+            n = rng.choice([0, 1, 2, 3, rng.randint(1, 64), rng.randint(1, 5000), rng.randint(1, 40000)])
+            n = min(n, (1 << 20) // il)
+            pos += rng.choice([0, 0, 8, 3])
+            offs.append(pos)
+            ns.append(n)
+            ils.append(il)
+            pos += n * il
+        host = O.splitmix_bytes(pos + 16, SEED + 100 + case)
+        roots = D.merkle_many(torch.from_numpy(host.copy()).to(gpu), offs, ns, ils).cpu().numpy().reshape(k, 32)
+        for i in range(k):
+            want = O.merkle_hash_flat(host[offs[i]:offs[i] + ns[i] * ils[i]], ns[i], ils[i])
+            assert bytes(roots[i]) == want, (case, i, ns[i], ils[i], offs[i])
+
+
+def _layout(rng):
+    """(fields, record_len): the validator layout, the (2 bytes, 0 raw)
+    layout, or a random mix of hashed byte fields and raw scalars (the flat
+    record contract of mk_ssz_struct_roots: bytes fields at 4-byte offsets,
+    record length a multiple of 4)."""
+    r = rng.random()
+    if r < 0.3:
+        return [(1, 0, 48), (1, 48, 32), (1, 80, 32)] + [(2, 112 + 8 * i, 8) for i in range(6)], 160
+    if r < 0.45:
+        return [(1, 0, 32), (1, 32, 32)], 64
+    fields, pos = [], 0
+    for _ in range(rng.randint(1, 8)):
+        if rng.random() < 0.5:
+            pos = (pos + 3) & ~3
+            ln = rng.choice([1, 4, 8, 20, 32, 33, 48, 64, 96])
+            fields.append((1, pos, ln))
+        else:
+            ln = rng.choice([1, 2, 4, 8])
+            fields.append((2, pos, ln))
+        pos += ln + rng.choice([0, 0, 4])
+    return fields, ((pos + 3) & ~3) + rng.choice([0, 4, 16])
+
+
+def test_fuzz_struct_roots(gpu):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    rng = random.Random(SEED + 2)
+    for case in range(100):
+        fields, rl = _layout(rng)
+        n = rng.choice([1, 2, 63, 64, 65, 1000, 16384, 32768, 32769, rng.randint(1, 70000)])
+        host = O.splitmix_bytes(n * rl + 16, SEED + 200 + case)
+        got = D.struct_roots(torch.from_numpy(host.copy()).to(gpu), n, rl, fields).cpu().numpy()[:32 * n]
+        want = O.struct_roots(host[:n * rl], n, rl, fields, nthreads=8).reshape(-1)
+        assert np.array_equal(got, want), (case, n, rl, fields)
+
+
+def test_fuzz_deposit_trie_batches(gpu):
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    rng = random.Random(SEED + 3)
+    for case in range(12):
+        depth = rng.choice([12, 20, 32])
+        t, ref = T.DepositTrie(depth), O.DictTrie(depth)
+        nxt = 0
+        for _ in range(rng.randint(3, 12)):
+            k = rng.choice([1, 2, 3, 5, 16, 17, 100, 300])
+            deps = [bytes(O.splitmix_bytes(rng.choice([280, 200, 44, 1]), SEED + 300 + case, 64 * (nxt + i)))
+                    for i in range(k)]
+            nxt += k
+            if rng.random() < 0.5:  # plain updates, one read
+                for d in deps:
+                    t.UpdateDepositTrie(d)
+                    ref.update(d)
+            else:  # the per-log check with a few wrong roots
+                roots, want = [], []
+                for d in deps:
+                    r = ref.root() if rng.random() < 0.85 else bytes(32)
+                    roots.append(r)
+                    ok = ref.root() == r
+                    want.append(ok)
+                    if ok:
+                        ref.update(d)
+                assert t.save_logs(deps, roots) == want, case
+            assert t.Root() == ref.root(), case
+        for idx in {0, ref.count // 3, ref.count - 1}:
+            if ref.count:
+                assert t.GenerateMerkleBranch(idx) == ref.branch(idx), (case, idx)
+
+
+def test_fuzz_merkle_root(gpu):
+    from oracle import oracle as O
+    from prysm_amd import hashutil as H
+
+    rng = random.Random(SEED + 4)
+    for case in range(20):
+        n = rng.choice([1, 2, 3, 7, 8, 9, 1000, 8192, rng.randint(1, 20000)])
+        ln = rng.choice([32, 32, 8, 1, 100])
+        vals = [bytes(O.splitmix_bytes(ln, SEED + 400 + case, 16 * i)) for i in range(n)]
+        want = O.merkle_root(list(vals))
+        assert H.MerkleRoot(list(vals)) == want, (case, n, ln)
