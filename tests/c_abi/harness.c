@@ -96,11 +96,17 @@ static void run_once(int t, struct result* r) {
     CHECK(rc == MK_OK && trie, "trie_new rc %d: %s", rc, call.err);
     uint8_t dep[280];
     uint64_t offs[2] = {0, 280};
+    uint8_t* before = malloc(300 * 32); /* Root() read before each deposit */
+    uint8_t* all = malloc(300 * 280);
+    uint64_t* alloffs = malloc(301 * sizeof(uint64_t));
     for (int i = 0; i < 300 && rc == MK_OK; ++i) {
-        rc = mk_deposit_trie_root(&call, trie, out);
+        rc = mk_deposit_trie_root(&call, trie, before + 32 * i);
         fill(dep, 280, SEED_BASE + 0x200, 35 * (uint64_t)i);
+        memcpy(all + 280 * i, dep, 280);
+        alloffs[i] = 280 * (uint64_t)i;
         if (rc == MK_OK) rc = mk_deposit_trie_append(&call, trie, dep, offs, 1);
     }
+    alloffs[300] = 300 * 280;
     uint8_t branch[32 * 32];
     if (rc == MK_OK) rc = mk_deposit_trie_root(&call, trie, out);
     int root_ok = rc == MK_OK && same(out, g_trie_root);
@@ -108,6 +114,37 @@ static void run_once(int t, struct result* r) {
     if (rc == MK_OK) rc = mk_hash(&call, branch, sizeof branch, out);
     CHECK(mk_deposit_trie_count(trie) == 300, "trie count %llu", (unsigned long long)mk_deposit_trie_count(trie));
     mk_deposit_trie_free(trie);
+
+    /* the same 300 logs through the batched per-log check, log 150 carrying a
+     * wrong root: the reference skips it, and every later log then fails its
+     * check too (their roots assume deposit 150) */
+    mk_trie* t2 = NULL;
+    int rc2 = mk_deposit_trie_new(&call, 32, 0, &t2);
+    uint8_t acc[300];
+    uint8_t root2[32];
+    memset(before + 32 * 150, 0xAB, 32);
+    if (rc2 == MK_OK) rc2 = mk_deposit_trie_save_logs(&call, t2, all, alloffs, 300, before, acc);
+    if (rc2 == MK_OK) rc2 = mk_deposit_trie_root(&call, t2, root2);
+    CHECK(rc2 == MK_OK, "save_logs rc %d: %s", rc2, call.err);
+    int acc_ok = 1;
+    for (int i = 0; i < 300; ++i) acc_ok &= acc[i] == (i < 150 ? 1 : 0);
+    CHECK(acc_ok, "thread %d: save_logs accept flags", t);
+    CHECK(mk_deposit_trie_count(t2) == 150, "thread %d: save_logs count %llu", t,
+          (unsigned long long)mk_deposit_trie_count(t2));
+    {
+        /* Root() after the 150 accepted deposits = the root read before deposit 150 in the first loop */
+        mk_trie* t3 = NULL;
+        uint8_t r3[32];
+        int rc3 = mk_deposit_trie_new(&call, 32, 0, &t3);
+        if (rc3 == MK_OK) rc3 = mk_deposit_trie_append(&call, t3, all, alloffs, 150);
+        if (rc3 == MK_OK) rc3 = mk_deposit_trie_root(&call, t3, r3);
+        CHECK(rc3 == MK_OK && memcmp(r3, root2, 32) == 0, "thread %d: save_logs root", t);
+        mk_deposit_trie_free(t3);
+    }
+    mk_deposit_trie_free(t2);
+    free(before);
+    free(all);
+    free(alloffs);
     CHECK(rc == MK_OK, "trie rc %d: %s", rc, call.err);
     CHECK(root_ok, "thread %d: trie root mismatch", t);
     CHECK(same(out, g_branch), "thread %d: branch mismatch", t);
