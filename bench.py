@@ -185,10 +185,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        P.init_process_group(args.backend, dev)
 
     n, item_len = 1 << args.log2n, args.item_len
     sp = P.plan(n, item_len, world)

@@ -26,6 +26,20 @@ import torch
 import torch.distributed as dist
 
 
+def init_process_group(backend: str, device=None) -> None:
+    """One process per GPU.  With backend "nccl" (RCCL over xGMI) the
+    process group's internal stream is created at high priority: the frontier
+    all-gather then gets its own hardware queue instead of queueing behind
+    the next leaf pass that the main stream has already issued (the same rule
+    as every side stream here)."""
+    if backend == "nccl":
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        dist.init_process_group("nccl", device_id=device, pg_options=opts)
+    else:
+        dist.init_process_group(backend)
+
+
 @dataclass
 class ShardPlan:
     height: int
