@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -916,6 +917,19 @@ int launch_shard(const uint8_t* d_items, uint64_t sn, uint32_t item_len, uint32_
 
 uint32_t multi_frontier(uint32_t h) { return h > 5 ? std::min<uint32_t>(10, h - 5) : 0; }
 
+// Test hook (MK_FORCE_COLLECTIVE=1 in the environment when the library is
+// loaded): a one-device multi call takes the sharded path with one shard —
+// frontier pass, ncclCommInitAll + in-place ncclAllGather over one rank,
+// finisher — instead of the plain one-device merkleHash, so the library's
+// RCCL code runs on a one-GPU box (RCCL refuses two ranks on one device).
+bool force_collective() {
+    static const bool on = [] {
+        const char* e = std::getenv("MK_FORCE_COLLECTIVE");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 // Uploads items[0, bytes) into d_dst on `copy`: chunked hipMemcpyAsync
 // straight from the caller's pageable buffer, i.e. the runtime's own staged
 // DMA (52-55 GB/s on one MI355X link).  The first multi-device form copied
@@ -984,7 +998,7 @@ int host_merkle_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int n
     uint32_t h = 0, ne = 0;
     std::vector<uint64_t> begin(nshards + 1);
     TRY(mk::shard_plan(n, item_len, (uint32_t)nshards, &h, &ne, begin.data()));
-    if (ne <= 1) {  // too small to shard: one device
+    if (ne <= 1 && !(nshards == 1 && h > 5 && force_collective())) {  // too small to shard: one device
         mk_call local{};
         local.device = devs[0];
         mk_call* prev = mk::swap_call(&local);
@@ -1082,7 +1096,7 @@ int dev_merkle_multi(const void* const* d_shards, uint64_t n, uint32_t item_len,
     std::vector<uint64_t> begin(ndev + 1);
     TRY(mk::shard_plan(n, item_len, (uint32_t)ndev, &h, &ne, begin.data()));
     auto stream_of = [&](int d) { return streams && streams[d] ? (hipStream_t)streams[d] : g_ctx[d]->stream; };
-    if (ne <= 1) {
+    if (ne <= 1 && !(ndev == 1 && h > 5 && force_collective())) {
         TRY(bind_dev(0));
         DevCtx* c = ctx();
         Plan p;

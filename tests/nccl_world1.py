@@ -21,7 +21,33 @@ from prysm_amd import device as D  # noqa: E402
 from prysm_amd import parallel as P  # noqa: E402
 
 
+def lib_main(log2n: int, n_extra: int):
+    """The library's own RCCL code (MK_FORCE_COLLECTIVE=1, set by the test
+    before this process loads the library): mk_dev_ssz_merkle_hash_multi and
+    mk_ssz_merkle_hash_multi over one device run the one-shard sharded path
+    (frontier, ncclCommInitAll + in-place ncclAllGather, finisher)."""
+    import ctypes
+
+    from prysm_amd import _lib
+
+    assert os.environ.get("MK_FORCE_COLLECTIVE") == "1"
+    dev = torch.device("cuda", 0)
+    n, il = (1 << log2n) + n_extra, 32
+    items = torch.empty(n * il, dtype=torch.uint8, device=dev)
+    D.synth_fill(items, 0x5EED000000000000 + 778)
+    want = bytes(D.merkle_hash(items, n, il).cpu().numpy()).hex()
+    out = torch.empty(32, dtype=torch.uint8, device=dev)
+    got_dev = [bytes(D.merkle_hash_multi([items], n, il, out).cpu().numpy()).hex() for _ in range(2)]
+    host = items.cpu().numpy()
+    buf = ctypes.create_string_buffer(32)
+    devs = (ctypes.c_int * 1)(0)
+    _lib.invoke("mk_ssz_merkle_hash_multi", host.ctypes.data_as(ctypes.c_void_p), n, il, 1, devs, buf)
+    print(json.dumps({"root": got_dev + [buf.raw.hex()], "want": want}), flush=True)
+
+
 def main():
+    if sys.argv[1] == "lib":
+        return lib_main(int(sys.argv[2]), int(sys.argv[3]))
     log2n, k = int(sys.argv[1]), int(sys.argv[2])
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
