@@ -124,10 +124,13 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise MerkleError(MK_ENODEV, f"{LIB_PATH} missing: run __graft_entry__.build() "
+    # PRYSM_MERKLE_LIB: another build of the same library (A/B tooling, e.g.
+    # prysm_amd/lib/variants/); never a different implementation
+    path = os.environ.get("PRYSM_MERKLE_LIB") or LIB_PATH
+    if not os.path.exists(path):
+        raise MerkleError(MK_ENODEV, f"{path} missing: run __graft_entry__.build() "
                                      "(no CPU fallback exists)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     for name, (res, args) in _SIGS.items():
         fn = getattr(L, name)
         fn.restype = res

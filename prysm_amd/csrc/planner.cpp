@@ -80,6 +80,11 @@ constexpr bool kTopOneWg = MK_TOP_ONE_WG != 0;
 #define MK_TOP_WG1024 1
 #endif
 constexpr bool kTopWg1024 = MK_TOP_WG1024 != 0;
+// Largest k_wave3 workgroup the planner picks (64..1024 threads).
+#ifndef MK_W3_MAX_NT
+#define MK_W3_MAX_NT 1024
+#endif
+constexpr uint32_t kW3MaxNt = MK_W3_MAX_NT < kMidThreads ? MK_W3_MAX_NT : kMidThreads;
 // leaf passes of at most this many windows: k_spread_leaf (0: never)
 #ifndef MK_SPREAD_LEAF_MAX_LOG2
 #define MK_SPREAD_LEAF_MAX_LOG2 12
@@ -176,10 +181,10 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         // keeps the pass within ~256 workgroups, one per CU
         uint32_t nt = w3 ? kWaveThreads : (wave ? kWaveThreads : kReduceThreads);
         if (w3) {
-            while (nt < kMidThreads && ceil_div(c1, nt / 2) > kNodeWaveWgs) nt *= 2;
+            while (nt < kW3MaxNt && ceil_div(c1, nt / 2) > kNodeWaveWgs) nt *= 2;
             if (kTopOneWg)  // the last <= 512 pairs in one workgroup: one launch to the root
-                while (nt < kMidThreads && c1 <= kMidThreads / 2 && c1 > nt / 2) nt *= 2;
-            if (kTopWg1024 && c1 <= kMidThreads / 2) nt = kMidThreads;
+                while (nt < kW3MaxNt && c1 <= kW3MaxNt / 2 && c1 > nt / 2) nt *= 2;
+            if (kTopWg1024 && c1 <= kW3MaxNt / 2) nt = kW3MaxNt;
         }
         // throughput pass: 2 window pairs per thread on wide passes, 1 on mid-size
         // leaf passes so they still spread over the CUs

@@ -164,10 +164,15 @@ class ShardedMerklePipeline:
     (``node_frontier_fn``), the all-gather of the frontiers (RCCL on the side
     stream) and, on rank 0, the finisher (``finish_nodes_fn``).  The split
     levels are the ones ``sharded_merkle_hash`` computes in one piece, so the
-    root is the same.  Buffers are double-buffered like
-    ``pipeline.MerklePipeline``: a submit waits for the side-stream work of
-    the tree submitted two calls earlier; a returned root (rank 0; None
-    elsewhere) stays valid until the submit after next.  Every rank must
+    root is the same.  Buffers rotate over ``slots`` sets: a submit waits for
+    the side-stream work of the tree submitted ``slots`` calls earlier; a
+    returned root (rank 0; None elsewhere) stays valid for the next
+    ``slots - 1`` submits.  Three sets, not two: side work dispatched while a
+    leaf pass fills every CU only gets workgroup slots in that pass's tail,
+    so with two sets the next leaf pass often waited for it (one-GPU probe of
+    the 8-GPU rank step, 2^25 items: 0.09-0.11 ms over the leaf pass with
+    two sets, 0.05 with three; tools/rank_step_probe.py,
+    profiles/r02k/rank_step_slots.jsonl).  Every rank must
     submit the same sequence of trees (one collective per tree).
 
     ``ok`` is False when the shard is too small to split (fewer than
@@ -177,7 +182,7 @@ class ShardedMerklePipeline:
     def __init__(self, n_total: int, item_len: int, sp: ShardPlan, rank: int, world: int, device,
                  gather_log2: int = 10, leaf_levels: int = 5, group=None,
                  frontier_fn: Optional[Callable] = None, node_frontier_fn: Optional[Callable] = None,
-                 finish_nodes_fn: Optional[Callable] = None, workspace=None):
+                 finish_nodes_fn: Optional[Callable] = None, workspace=None, slots: int = 3):
         self.n_total, self.item_len, self.sp = n_total, item_len, sp
         self.rank, self.world, self.group = rank, world, group
         self.device = torch.device(device)
@@ -210,21 +215,23 @@ class ShardedMerklePipeline:
         self.frontier_fn, self.node_frontier_fn, self.finish_nodes_fn = frontier_fn, node_frontier_fn, finish_nodes_fn
         block = 32 << self.k
         dev = self.device
-        self.levels = [torch.empty(32 << self.k_leaf, dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.blocks = [torch.zeros(block, dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.gathered = [torch.empty(world * block, dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.outs = [torch.empty(32, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.slots = max(2, int(slots))
+        S = self.slots
+        self.levels = [torch.empty(32 << self.k_leaf, dtype=torch.uint8, device=dev) for _ in range(S)]
+        self.blocks = [torch.zeros(block, dtype=torch.uint8, device=dev) for _ in range(S)]
+        self.gathered = [torch.empty(world * block, dtype=torch.uint8, device=dev) for _ in range(S)]
+        self.outs = [torch.empty(32, dtype=torch.uint8, device=dev) for _ in range(S)]
         self.cuda = dev.type == "cuda"
         # high priority = its own hardware queue (see MerklePipeline)
         self.side = torch.cuda.Stream(device=dev, priority=-1) if self.cuda else None
-        self._done = [None, None]
+        self._done = [None] * S
         self._i = 0
 
     def submit(self, local_items: torch.Tensor) -> Optional[torch.Tensor]:
-        slot = self._i & 1
+        slot = self._i % self.slots
         self._i += 1
         cur = torch.cuda.current_stream(self.device) if self.cuda else None
-        if self.cuda and self._done[slot] is not None:  # side work of two trees back reads this slot
+        if self.cuda and self._done[slot] is not None:  # side work of `slots` trees back reads this slot
             cur.wait_event(self._done[slot])
         level = None
         if self.sn:
