@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
-ARGS=${PROF_ARGS:---steps 10 --warmup 3 --no-cpu-baseline}  # the default bench line's steps
+ARGS=${PROF_ARGS:---steps 10 --warmup 20 --no-cpu-baseline}  # the default bench line's steps and warmup
 D=gpurun_out/prof_$TAG
 mkdir -p $D
 run() {  # name, rocprofv3 options...
