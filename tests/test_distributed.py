@@ -77,7 +77,7 @@ def _worker(rank, world, port, n, item_len, q, frontier=0, pipe=None):
         def finish_nodes(g, count, nt):
             return finish(g, count, nt)
 
-        if pipe is not None:  # (gather_log2, leaf_levels): ShardedMerklePipeline over 3 submitted trees
+        if pipe is not None:  # (gather_log2, leaf_levels[, slots]): ShardedMerklePipeline over several trees
             def node_frontier(level, cnt, hh, kk, pad, out):
                 nodes = [bytes(level[32 * i:32 * i + 32].numpy()) for i in range(cnt)]
                 for _ in range(hh - kk):  # the odd rule incl. a lone node (pad_at_one)
@@ -90,9 +90,10 @@ def _worker(rank, world, port, n, item_len, q, frontier=0, pipe=None):
                 n, item_len, sp, rank, world, "cpu", gather_log2=pipe[0], leaf_levels=pipe[1],
                 frontier_fn=lambda it, sn, il, h, k, pad, out: frontier_fn(it, sn, il, h, k, pad),
                 node_frontier_fn=node_frontier,
-                finish_nodes_fn=lambda g, c, nt, out: finish_nodes(g, c, nt))
+                finish_nodes_fn=lambda g, c, nt, out: finish_nodes(g, c, nt),
+                **({"slots": pipe[2]} if len(pipe) > 2 else {}))
             assert pl.ok
-            roots = [pl.submit(local) for _ in range(3)]
+            roots = [pl.submit(local) for _ in range(max(3, pl.slots + 2))]
             if rank == 0:
                 assert len({bytes(r.numpy()) for r in roots}) == 1
                 q.put(bytes(roots[-1].numpy()))
@@ -143,18 +144,20 @@ def test_frontier_sharded_root_equals_full_root(world, n, k):
     assert root == O.merkle_hash_gen(n, 32, SEED)
 
 
-@pytest.mark.parametrize("world,n,k,leaf", [(2, 1 << 14, 3, 5), (2, 4 * 1000 + 3, 2, 3), (4, 4 * 3000 + 3, 2, 5),
-                                            (4, 1 << 14, 1, 5)])
-def test_pipelined_sharded_root_equals_full_root(world, n, k, leaf):
+@pytest.mark.parametrize("world,n,k,leaf,slots", [(2, 1 << 14, 3, 5, 3), (2, 4 * 1000 + 3, 2, 3, 3),
+                                                  (4, 4 * 3000 + 3, 2, 5, 3), (4, 1 << 14, 1, 5, 3),
+                                                  (2, 1 << 14, 3, 5, 2), (2, 4 * 1000 + 3, 2, 3, 4)])
+def test_pipelined_sharded_root_equals_full_root(world, n, k, leaf, slots):
     """ShardedMerklePipeline: leaf pass to `leaf` levels above the chunks,
     node passes to the 2^k frontier, all-gather and rank-0 finish split off
-    per tree (ragged last shards included)."""
+    per tree (ragged last shards included), `slots` buffer sets rotating
+    over slots + 2 trees."""
     from oracle import oracle as O
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, 32, q, 0, (k, leaf))) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, 32, q, 0, (k, leaf, slots))) for r in range(world)]
     for p in procs:
         p.start()
     root = q.get(timeout=120)
