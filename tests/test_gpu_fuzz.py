@@ -5,6 +5,7 @@ branch: spread leaf passes, lane-pair passes, fused throughput passes),
 many lists per call, struct roots of random layouts (both struct kernels
 and the generic one), deposit tries grown by random batches with the
 per-log check, and MerkleRoot.  Sizes keep the oracle to seconds."""
+import os
 import random
 
 import numpy as np
@@ -12,7 +13,10 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-SEED = 0x5EED000000000000 + 1400
+# PRYSM_FUZZ_SEED shifts every stream (a different set of random shapes);
+# PRYSM_FUZZ_SCALE multiplies the case counts.  Defaults: the committed run.
+SEED = 0x5EED000000000000 + 1400 + 1000 * int(os.environ.get("PRYSM_FUZZ_SEED", "0"))
+SCALE = max(1, int(os.environ.get("PRYSM_FUZZ_SCALE", "1")))
 
 
 @pytest.fixture(scope="module")
@@ -37,7 +41,7 @@ def test_fuzz_merkle_hash(gpu):
     from prysm_amd import device as D
 
     rng = random.Random(SEED)
-    for case in range(400):
+    for case in range(400 * SCALE):
         il = _item_len(rng)
         n = int(2 ** rng.uniform(0, 17.5))
         n = min(n, (3 << 20) // il)
@@ -58,7 +62,7 @@ def test_fuzz_merkle_many(gpu):
     from prysm_amd import device as D
 
     rng = random.Random(SEED + 1)
-    for case in range(60):
+    for case in range(60 * SCALE):
         k = rng.randint(1, 40)
         ns, ils, offs, pos = [], [], [], 0
         for _ in range(k):
@@ -107,7 +111,7 @@ def test_fuzz_struct_roots(gpu):
     from prysm_amd import device as D
 
     rng = random.Random(SEED + 2)
-    for case in range(100):
+    for case in range(100 * SCALE):
         fields, rl = _layout(rng)
         n = rng.choice([1, 2, 63, 64, 65, 1000, 16384, 32768, 32769, rng.randint(1, 70000)])
         host = O.splitmix_bytes(n * rl + 16, SEED + 200 + case)
@@ -121,7 +125,7 @@ def test_fuzz_deposit_trie_batches(gpu):
     from prysm_amd import trieutil as T
 
     rng = random.Random(SEED + 3)
-    for case in range(12):
+    for case in range(12 * SCALE):
         depth = rng.choice([12, 20, 32])
         t, ref = T.DepositTrie(depth), O.DictTrie(depth)
         nxt = 0
@@ -155,7 +159,7 @@ def test_fuzz_merkle_root(gpu):
     from prysm_amd import hashutil as H
 
     rng = random.Random(SEED + 4)
-    for case in range(20):
+    for case in range(20 * SCALE):
         n = rng.choice([1, 2, 3, 7, 8, 9, 1000, 8192, rng.randint(1, 20000)])
         ln = rng.choice([32, 32, 8, 1, 100])
         vals = [bytes(O.splitmix_bytes(ln, SEED + 400 + case, 16 * i)) for i in range(n)]
