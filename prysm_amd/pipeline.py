@@ -25,14 +25,16 @@ from typing import Optional
 import torch
 
 from . import device as D
-from .parallel import frontier_count
+from .parallel import SlotRing, frontier_count
 
 
 class MerklePipeline:
-    def __init__(self, n: int, item_len: int, device, frontier_log2: Optional[int] = None, leaf_levels: int = 5):
+    def __init__(self, n: int, item_len: int, device, frontier_log2: Optional[int] = None, leaf_levels: int = 5,
+                 slots: int = 2, wait_every: int = 1):
         """Split ``frontier_log2`` levels below the root; by default at the
         leaf pass's output level, ``leaf_levels`` above the chunks (21 below
-        the root of a 2^28-item tree of 32-B items)."""
+        the root of a 2^28-item tree of 32-B items).  ``slots`` buffer sets,
+        ``wait_every``: parallel.SlotRing."""
         self.n, self.item_len = n, item_len
         self.device = torch.device(device)
         height, _, _ = D.shard_plan(n, item_len, 1)
@@ -44,10 +46,11 @@ class MerklePipeline:
         self.k = k if k > 0 and frontier_count(n, item_len, height, k) > 1 else 0
         self.ws = D.subtree_workspace(n, item_len, self.device) if self.k else D.merkle_workspace(n, item_len,
                                                                                                    self.device)
-        self.outs = [torch.empty(32, dtype=torch.uint8, device=self.device) for _ in range(2)]
+        self._ring = SlotRing(slots, wait_every)
+        self.outs = [torch.empty(32, dtype=torch.uint8, device=self.device) for _ in range(slots)]
         if self.k:
             self.count = frontier_count(n, item_len, height, self.k)
-            self.bufs = [torch.empty(32 << self.k, dtype=torch.uint8, device=self.device) for _ in range(2)]
+            self.bufs = [torch.empty(32 << self.k, dtype=torch.uint8, device=self.device) for _ in range(slots)]
             self.fin_ws = D.finish_workspace(self.count, self.device)
             # high priority: a default-priority side stream can land on the
             # current stream's hardware queue and serialise behind the next
@@ -56,19 +59,16 @@ class MerklePipeline:
             self.side = torch.cuda.Stream(device=self.device, priority=-1)
         else:
             self.side = torch.cuda.current_stream(self.device)
-        self._done = [None, None]
-        self._i = 0
 
     def submit(self, items: torch.Tensor) -> torch.Tensor:
         """Enqueue merkleHash(items) (n items of item_len bytes); returns the
         (32,) uint8 root tensor, produced on ``self.side``."""
-        slot = self._i & 1
-        self._i += 1
         cur = torch.cuda.current_stream(self.device)
         if not self.k:
+            slot = self._ring.acquire(None)
+            self._ring.release(None)
             return D.merkle_hash(items, self.n, self.item_len, out=self.outs[slot], ws=self.ws)
-        if self._done[slot] is not None:  # the top two trees back still reads this slot
-            cur.wait_event(self._done[slot])
+        slot = self._ring.acquire(cur)  # the top `slots` trees back no longer reads this set
         level = D.merkle_subtree_frontier(items, self.n, self.item_len, self.height, self.k, False,
                                           out=self.bufs[slot], ws=self.ws)
         self.side.wait_stream(cur)
@@ -76,7 +76,7 @@ class MerklePipeline:
             root = D.merkle_finish_nodes(level, self.count, self.n, out=self.outs[slot], ws=self.fin_ws)
             ev = torch.cuda.Event()
             ev.record(self.side)
-        self._done[slot] = ev
+        self._ring.release(ev)
         return root
 
 
@@ -96,9 +96,11 @@ class TriePipeline:
 
     TOP_MAX = 1 << 17  # capi.cpp kTrieTopMax: levels at or below this width run k_trie_top3
 
-    def __init__(self, n: int, deposit_len: int, depth: int, device, split: Optional[int] = None):
+    def __init__(self, n: int, deposit_len: int, depth: int, device, split: Optional[int] = None,
+                 slots: int = 2, wait_every: int = 1):
         """``split``: the first level built on the side stream (default: the
-        first level of at most TOP_MAX nodes)."""
+        first level of at most TOP_MAX nodes); ``slots``, ``wait_every``:
+        parallel.SlotRing."""
         self.n, self.dl, self.depth = n, deposit_len, depth
         self.device = torch.device(device)
         if split is None:
@@ -107,22 +109,18 @@ class TriePipeline:
                 split += 1
         self.split = split
         nbytes = D.deposit_trie_levels_bytes(n, depth)
-        self.levels = [torch.empty(nbytes, dtype=torch.uint8, device=self.device) for _ in range(2)]
-        self.roots = [torch.empty(32, dtype=torch.uint8, device=self.device) for _ in range(2)]
+        self._ring = SlotRing(slots, wait_every)
+        self.levels = [torch.empty(nbytes, dtype=torch.uint8, device=self.device) for _ in range(slots)]
+        self.roots = [torch.empty(32, dtype=torch.uint8, device=self.device) for _ in range(slots)]
         self.side = torch.cuda.Stream(device=self.device, priority=-1)  # its own hardware queue
-        self._done = [None, None]
-        self._i = 0
 
     def submit(self, deposits: torch.Tensor) -> torch.Tensor:
         """Enqueue the trie of n fixed-length deposits held in ``deposits``;
         returns its (32,) root tensor, produced on ``self.side``."""
         if deposits.numel() < self.n * self.dl:
             raise ValueError("deposit buffer shorter than n * deposit_len")
-        slot = self._i & 1
-        self._i += 1
         cur = torch.cuda.current_stream(self.device)
-        if self._done[slot] is not None:
-            cur.wait_event(self._done[slot])
+        slot = self._ring.acquire(cur)
         lv, root = self.levels[slot], self.roots[slot]
         D.deposit_trie_build(lv, self.n, deposits, self.n, self.dl, self.split, self.depth)
         self.side.wait_stream(cur)
@@ -130,5 +128,5 @@ class TriePipeline:
             D.deposit_trie_levels(lv, self.n, self.n, self.split, self.depth, self.depth, root)
             ev = torch.cuda.Event()
             ev.record(self.side)
-        self._done[slot] = ev
+        self._ring.release(ev)
         return root
