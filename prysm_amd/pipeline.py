@@ -12,10 +12,10 @@ the next submitted tree.  The split is the single-shard case of the subtree
 sharding in parallel.py (same planner, same frontier finisher), so each root
 is bit-identical to ``device.merkle_hash`` of the same items.
 
-Frontier levels and roots are double-buffered: a submit waits for the top of
-the tree submitted two calls earlier before it overwrites that tree's
-buffers, and the root returned by a submit stays valid until the submit after
-next.  The root is produced on ``side``; call ``torch.cuda.synchronize()`` or
+Frontier levels and roots rotate over ``slots`` buffer sets (three by
+default): a submit waits for the top of the tree submitted ``slots`` calls
+earlier before it overwrites that tree's buffers, and the root returned by a
+submit stays valid for the next ``slots - 1`` submits.  The root is produced on ``side``; call ``torch.cuda.synchronize()`` or
 make the consuming stream wait on ``side`` before reading it.
 """
 from __future__ import annotations
@@ -30,11 +30,14 @@ from .parallel import SlotRing, frontier_count
 
 class MerklePipeline:
     def __init__(self, n: int, item_len: int, device, frontier_log2: Optional[int] = None, leaf_levels: int = 5,
-                 slots: int = 2, wait_every: int = 1):
+                 slots: int = 3, wait_every: int = 1):
         """Split ``frontier_log2`` levels below the root; by default at the
         leaf pass's output level, ``leaf_levels`` above the chunks (21 below
         the root of a 2^28-item tree of 32-B items).  ``slots`` buffer sets,
-        ``wait_every``: parallel.SlotRing."""
+        ``wait_every``: parallel.SlotRing.  Three sets: a 2^25-item stream
+        runs 1.288 -> 1.254 ms per tree against two (a tree's top waits for
+        the next leaf pass's tail); 2^28 is the same either way
+        (tools/ring_ab.py, profiles/r02r/ring_ab.jsonl)."""
         self.n, self.item_len = n, item_len
         self.device = torch.device(device)
         height, _, _ = D.shard_plan(n, item_len, 1)
@@ -90,9 +93,11 @@ class TriePipeline:
     of at most 2^17 nodes (one launch per level, every lane busy).  On a
     high-priority side stream, overlapping the next trie's leaves: the
     latency-bound top (k_trie_top3 launches) plus the zero-sibling levels
-    up to ``depth`` and the root.  Level arrays and roots are double-buffered
-    like MerklePipeline: a submit waits for the top of the trie two submits
-    back; a returned root stays valid until the submit after next."""
+    up to ``depth`` and the root.  Level arrays and roots rotate over
+    ``slots`` sets (two by default: 2/3/4 sets and a wait every 2-3 submits
+    measured the same, profiles/r02r/ring_ab.jsonl): a submit waits for the
+    top of the trie ``slots`` submits back; a returned root stays valid for
+    the next ``slots - 1`` submits."""
 
     TOP_MAX = 1 << 17  # capi.cpp kTrieTopMax: levels at or below this width run k_trie_top3
 

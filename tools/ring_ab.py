@@ -37,7 +37,7 @@ def main():
         n = 1 << 20
         data = torch.empty(n * 280, dtype=torch.uint8, device=dev)
         D.synth_fill(data, 0x5EED000000000005)
-        work["trie"] = (data, lambda S, W: TriePipeline(n, 280, 32, dev, slots=S, wait_every=W))
+        work["trie"] = (data, lambda S, W, nn=n: TriePipeline(nn, 280, 32, dev, slots=S, wait_every=W))
     for tag, lg in (("m28", 28), ("m25", 25)):
         if tag in a.only:
             n = 1 << lg
