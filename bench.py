@@ -292,7 +292,14 @@ def main():
             status = 1
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+    per_rank = None
     if world > 1:
+        # every rank's step time and leaf-kernel launch average, for the record
+        mine = torch.tensor([elapsed / args.steps * 1e3, leaf_ms / max(leaf_launches, 1)], dtype=torch.float64,
+                            device=t.device)
+        allr = torch.empty(world * 2, dtype=torch.float64, device=t.device)
+        dist.all_gather_into_tensor(allr, mine)
+        per_rank = [[round(x, 4) for x in allr[2 * r:2 * r + 2].tolist()] for r in range(world)]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = t.item()
 
@@ -323,7 +330,8 @@ def main():
                        "shard_height": sp.height, "frontier_log2": k, "pipelined": pipe is not None and k > 0,
                        "root": root_hex, "root_matches_golden": None if golden_root(args.log2n, item_len) is None
                        else root_hex == golden_root(args.log2n, item_len),
-                       "backend": args.backend if world > 1 else None, "share_device": bool(args.share_device)},
+                       "backend": args.backend if world > 1 else None, "share_device": bool(args.share_device),
+                       "per_rank_ms_per_step_and_leaf_ms": per_rank},
             "roofline": {
                 "bound": "valu-int",
                 "kernel": "k_reduce<LEAF, FAST, 2> (leaf pass: 256-B windows + 4 fused levels)",
