@@ -454,7 +454,7 @@ int dev_finish_nodes(const void* d_nodes, uint64_t count, uint64_t n_total, void
     return launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st);
 }
 
-int host_merkle_hash(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t* out) {
+int host_merkle_hash_plain(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t* out) {
     if (!out || (n && item_len && !items)) return fail(MK_EINVAL, "null pointer");
     TRY(bind_call());
     DevCtx* c = ctx();
@@ -471,6 +471,31 @@ int host_merkle_hash(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_
     HIPCHK(hipMemcpyAsync(out, c->out.p, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return MK_OK;
+}
+
+int host_merkle_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int nshards, const int* devs_in,
+                      uint8_t* out);
+
+// merkleHash of a host buffer (the cgo TreeHash path).  A large buffer goes
+// through the sharded path with its shards on this one device: shard i+1
+// crosses PCIe while shard i's passes run, so the compute hides under the
+// copy (8 GiB: copy then compute 162-164 ms) and the device holds
+// two shard regions instead of the whole input.
+#ifndef MK_HOST_OVERLAP_MIN_LOG2
+#define MK_HOST_OVERLAP_MIN_LOG2 28  // bytes; 64 = never
+#endif
+int host_merkle_hash(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t* out) {
+    if (!out || (n && item_len && !items)) return fail(MK_EINVAL, "null pointer");
+    const uint64_t inb = n * (uint64_t)item_len;
+    if (MK_HOST_OVERLAP_MIN_LOG2 < 64 && item_len && n <= (UINT64_MAX / 2) / item_len &&
+        inb >= (1ull << (MK_HOST_OVERLAP_MIN_LOG2 & 63))) {
+        TRY(bind_call());
+        const int d = t_bound;
+        const int ns = (int)std::min<uint64_t>(8, std::max<uint64_t>(2, inb >> 26));  // >= 64 MB per shard
+        std::vector<int> devs(ns, d);
+        return host_merkle_multi(items, n, item_len, ns, devs.data(), out);
+    }
+    return host_merkle_hash_plain(items, n, item_len, out);
 }
 
 // ---- many lists ------------------------------------------------------------------------
@@ -1002,15 +1027,19 @@ int host_merkle_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int n
         mk_call local{};
         local.device = devs[0];
         mk_call* prev = mk::swap_call(&local);
-        const int rc = host_merkle_hash(items, n, item_len, out);
+        const int rc = host_merkle_hash_plain(items, n, item_len, out);
         mk::swap_call(prev);
         return rc ? fail(rc, "%s", local.err) : MK_OK;
     }
-    std::lock_guard<std::mutex> mlk(g_multi_mu);
     std::vector<int> uniq;
     for (int d : devs)
         if (std::find(uniq.begin(), uniq.end(), d) == uniq.end()) uniq.push_back(d);
     const bool one_each = (int)uniq.size() == nshards;
+    // several devices or RCCL: one multi-device call at a time (device lock
+    // order, the communicator cache); shards on one device need only that
+    // device's lock, so one-device calls on different devices stay concurrent
+    std::unique_lock<std::mutex> mlk(g_multi_mu, std::defer_lock);
+    if (uniq.size() > 1 || one_each) mlk.lock();
     const uint32_t k = multi_frontier(h);
     const size_t block = (size_t)32 << k;
     std::vector<MultiJob> jobs;
