@@ -98,6 +98,63 @@ def load_pmc():
         return None, None, None
 
 
+class ClockSampler:
+    """Samples this GPU's current shader clock (sysfs pp_dpm_sclk, the line
+    marked '*') every ~2 ms on a host thread while the timed steps run: the
+    sustained clock of THIS run, beside the PMC figure of a committed
+    profile.  Host-side only (no GPU call); None where the file is absent."""
+
+    def __init__(self, dev_index: int):
+        import threading
+
+        import torch
+
+        self.path = None
+        try:
+            p = torch.cuda.get_device_properties(dev_index)
+            bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+            path = f"/sys/bus/pci/devices/{bdf}/pp_dpm_sclk"
+            if self._read(path) is not None:
+                self.path = path
+        except Exception:
+            pass
+        self.samples = []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True) if self.path else None
+
+    @staticmethod
+    def _read(path):
+        try:
+            with open(path) as f:
+                for line in f:
+                    if line.rstrip().endswith("*"):
+                        return float(line.split(":", 1)[1].strip().split("Mhz")[0].split("MHz")[0])
+        except (OSError, ValueError, IndexError):
+            return None
+        return None
+
+    def _run(self):
+        while not self._stop.is_set():
+            v = self._read(self.path)
+            if v is not None:
+                self.samples.append(v)
+            self._stop.wait(0.002)
+
+    def start(self):
+        if self._t:
+            self._t.start()
+
+    def stop(self):
+        if self._t:
+            self._stop.set()
+            self._t.join()
+        if not self.samples:
+            return None
+        xs = sorted(self.samples)
+        return {"mean_MHz": sum(xs) / len(xs), "median_MHz": xs[len(xs) // 2], "min_MHz": xs[0],
+                "max_MHz": xs[-1], "samples": len(xs), "source": self.path}
+
+
 def golden_root(log2n: int, item_len: int):
     """The committed oracle root of this exact workload, if there is one
     (tests/golden/full_size_roots.json: 2^28 x 32 B, seed 0x5EED..04)."""
@@ -271,6 +328,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    sampler = ClockSampler(local)
+    sampler.start()
     t0 = time.perf_counter()
     last_log = t0
     for i in range(args.steps):
@@ -282,6 +341,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    sclk = sampler.stop()
     D.prof_enable(False)
     leaf_ms, leaf_launches, leaf_perms, leaf_hashes = D.prof_read()
     if rank == 0 and r is not None:
@@ -344,6 +404,10 @@ def main():
                 "effective_clock_GHz": clk,
                 "traffic_source": pmc_src,
                 "frac_at_effective_clock": achieved / (PEAK_INT_OPS / 2.4 * clk) if clk else None,
+                # this run's own clock (rank 0's GPU), sampled from sysfs during the timed steps
+                "sclk_sampled": sclk,
+                "frac_at_sampled_clock": (achieved / (PEAK_INT_OPS / 2.4e3 * sclk["mean_MHz"])
+                                          if sclk and sclk["mean_MHz"] > 0 else None),
                 "perms_per_launch": perms_per_launch,
                 "hashes_per_launch": hashes_per_launch,
                 "avg_launch_ms": avg_leaf_s * 1e3,
