@@ -1723,15 +1723,11 @@ __global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ 
 // spends 2 VALU per word on it).  Prefetching block b+1 into 34 VGPRs while
 // block b permutes was 1-2 % slower on the 2^20-deposit trie (0.588 vs
 // 0.582 ms, profiles/r02d/ab_rec_prefetch.log): the other resident waves
-// hide the load as well.
-#ifndef MK_REC_WAVES
-#define MK_REC_WAVES 1  // occupancy hint (1: none; 100 VGPRs, 4 waves/SIMD)
-#endif
-// (5 waves: 96 VGPRs with 4 dwords spilled; the stream of 2^20-deposit tries
-// got 3 % slower, 0.502/0.505 -> 0.515/0.525 ms/step, profiles/r02m/rejected/)
+// hide the load as well.  At 5 waves/SIMD (96 VGPRs, 4 dwords spilled) the
+// stream of 2^20-deposit tries got 3 % slower (profiles/r02m/rejected/).
 template <int NW>
-__global__ __launch_bounds__(kRecThreads, MK_REC_WAVES) void k_keccak_rec(const uint2* __restrict__ in, uint64_t n,
-                                                                          uint4* __restrict__ out) {
+__global__ __launch_bounds__(kRecThreads) void k_keccak_rec(const uint2* __restrict__ in, uint64_t n,
+                                                            uint4* __restrict__ out) {
     constexpr int NB = NW / 17 + 1;
     const uint64_t stride = (uint64_t)gridDim.x * kRecThreads;
 #pragma unroll 1
