@@ -36,17 +36,26 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+_SCLK = {}  # seconds per step -> the shader clock sampled while that loop ran
+
+
 def _timeit(fn, steps, warmup):
     import torch
+
+    from bench import ClockSampler
 
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
+    sampler = ClockSampler(torch.cuda.current_device())
+    sampler.start()
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / steps
+    sec = (time.perf_counter() - t0) / steps
+    _SCLK[sec] = sampler.stop()
+    return sec
 
 
 def _line(metric, value, unit, args, sec, perms, hashes, config, cpu=None, extra=None):
@@ -58,6 +67,10 @@ def _line(metric, value, unit, args, sec, perms, hashes, config, cpu=None, extra
            "roofline": {"bound": "valu-int", "achieved": achieved / 1e12, "peak": PEAK_INT_OPS / 1e12,
                         "unit": "Tops/s (int32 VALU, whole step)", "frac": achieved / PEAK_INT_OPS,
                         "perms_per_step": perms, "hashes_per_step": hashes}}
+    sclk = _SCLK.get(sec)
+    out["roofline"]["sclk_sampled"] = sclk
+    out["roofline"]["frac_at_sampled_clock"] = (achieved / (PEAK_INT_OPS / 2.4e3 * sclk["mean_MHz"])
+                                                if sclk and sclk["mean_MHz"] > 0 else None)
     if extra:
         out["roofline"].update(extra)
     if cpu:
