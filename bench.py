@@ -100,9 +100,12 @@ def load_pmc():
 
 class ClockSampler:
     """Samples this GPU's current shader clock (sysfs pp_dpm_sclk, the line
-    marked '*') every ~2 ms on a host thread while the timed steps run: the
-    sustained clock of THIS run, beside the PMC figure of a committed
-    profile.  Host-side only (no GPU call); None where the file is absent."""
+    marked '*') every ~2 ms on a host thread while the timed steps run.
+    OFF unless PRYSM_BENCH_SCLK=1: each read is a query to the power-
+    management firmware, and sampling slowed the measured GPU itself (C2
+    1.54 -> 1.82 ms, C4 9.76-9.85 -> 10.06-10.07 ms, alternating runs on one
+    box, profiles/r02z2/ab.txt), so the default bench line carries only the
+    committed PMC clock.  Host-side only; None where the file is absent."""
 
     def __init__(self, dev_index: int):
         import threading
@@ -110,6 +113,9 @@ class ClockSampler:
         import torch
 
         self.path = None
+        if os.environ.get("PRYSM_BENCH_SCLK") != "1":
+            self.samples, self._t = [], None
+            return
         try:
             p = torch.cuda.get_device_properties(dev_index)
             bdf = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
@@ -404,7 +410,7 @@ def main():
                 "effective_clock_GHz": clk,
                 "traffic_source": pmc_src,
                 "frac_at_effective_clock": achieved / (PEAK_INT_OPS / 2.4 * clk) if clk else None,
-                # this run's own clock (rank 0's GPU), sampled from sysfs during the timed steps
+                # this run's own clock (rank 0's GPU) from sysfs, only with PRYSM_BENCH_SCLK=1
                 "sclk_sampled": sclk,
                 "frac_at_sampled_clock": (achieved / (PEAK_INT_OPS / 2.4e3 * sclk["mean_MHz"])
                                           if sclk and sclk["mean_MHz"] > 0 else None),
