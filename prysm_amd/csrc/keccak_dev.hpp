@@ -342,13 +342,30 @@ __device__ __forceinline__ void pad_const(State& s) {
 // Streaming (non-temporal) loads of input that is read exactly once.
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+// Loads of the streamed inputs (items, node levels, deposit records): plain,
+// L2-allocating loads.  Non-temporal loads (MK_LD_NT=1, rounds 1-2) let the
+// leaf kernel's lines leave L2 before all of a window's 16-B loads had hit
+// them: 10.09 GB fetched per 2^28 launch against 8.90 GB with plain loads
+// (8.59 GB algorithmic), and the leaf pass ran 1.3-2.5 % slower
+// (profiles/r02zc/ab.txt, three boxes).
+#ifndef MK_LD_NT
+#define MK_LD_NT 0
+#endif
+__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
+#if MK_LD_NT
     const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
     return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
 }
-__device__ __forceinline__ uint2 ld_nt(const uint2* p) {
+__device__ __forceinline__ uint2 ld_stream(const uint2* p) {
+#if MK_LD_NT
     const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
     return make_uint2(v.x, v.y);
+#else
+    return *p;
+#endif
 }
 
 // Squeeze the 32-byte digest (lanes 0..3, little-endian).

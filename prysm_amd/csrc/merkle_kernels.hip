@@ -136,7 +136,7 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
     // line is fetched once (no L2 re-fetch of the line shared by both blocks)
     uint4 v[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = ld_nt(w + k);
+    for (int k = 0; k < 16; ++k) v[k] = ld_stream(w + k);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         s.lo[2 * k] ^= v[k].x;
@@ -167,7 +167,7 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
         if (b == 0) {
             uint4 v[9];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) v[k] = ld_nt(w + k);
+            for (int k = 0; k < 9; ++k) v[k] = ld_stream(w + k);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 s.lo[2 * k] ^= v[k].x;
@@ -178,10 +178,10 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
             s.lo[16] ^= v[8].x;
             s.hi[16] ^= v[8].y;
         } else {
-            const uint2 t = ld_nt(reinterpret_cast<const uint2*>(w + 8) + 1);
+            const uint2 t = ld_stream(reinterpret_cast<const uint2*>(w + 8) + 1);
             uint4 v[7];
 #pragma unroll
-            for (int k = 0; k < 7; ++k) v[k] = ld_nt(w + 9 + k);
+            for (int k = 0; k < 7; ++k) v[k] = ld_stream(w + 9 + k);
             s.lo[0] ^= t.x;
             s.hi[0] ^= t.y;
 #pragma unroll
@@ -216,7 +216,7 @@ __device__ __forceinline__ void hash_window256_staged(const uint4* __restrict__ 
     State s;
     uint4 v[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = ld_nt(w + k);
+    for (int k = 0; k < 16; ++k) v[k] = ld_stream(w + k);
 #pragma unroll
     for (int k = 0; k < 8; ++k) stg[k * kReduceThreads] = v[8 + k];
 #pragma unroll
@@ -266,7 +266,7 @@ __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w
     State s;
     uint4 v[9];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) v[k] = ld_nt(w + k);
+    for (int k = 0; k < 9; ++k) v[k] = ld_stream(w + k);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         s.lo[2 * k] = v[k].x;
@@ -286,7 +286,7 @@ __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w
     {
         uint4 u[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) u[k] = ld_nt(w + 9 + k);
+        for (int k = 0; k < 4; ++k) u[k] = ld_stream(w + 9 + k);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             s.lo[1 + 2 * k] ^= u[k].x;
@@ -298,7 +298,7 @@ __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w
     {
         uint4 u[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) u[k] = ld_nt(w + 13 + k);
+        for (int k = 0; k < 3; ++k) u[k] = ld_stream(w + 13 + k);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             s.lo[9 + 2 * k] ^= u[k].x;
@@ -437,8 +437,8 @@ __global__ __launch_bounds__(kReduceThreads, (MK_LEAF_SPLIT && LEAF && FAST) ? M
                 hash_window256(w + 16, r0, r1);
             } else {
                 const uint4* in = reinterpret_cast<const uint4*>(a.items) + j0 * 4;
-                hash_pair(ld_nt(in), ld_nt(in + 1), ld_nt(in + 2), ld_nt(in + 3), false, l0, l1);
-                hash_pair(ld_nt(in + 4), ld_nt(in + 5), ld_nt(in + 6), ld_nt(in + 7), false, r0, r1);
+                hash_pair(ld_stream(in), ld_stream(in + 1), ld_stream(in + 2), ld_stream(in + 3), false, l0, l1);
+                hash_pair(ld_stream(in + 4), ld_stream(in + 5), ld_stream(in + 6), ld_stream(in + 7), false, r0, r1);
             }
             hash_pair(l0, l1, r0, r1, false, d0, d1);
             lds[2 * q] = d0;
@@ -817,7 +817,7 @@ __device__ __forceinline__ void hash_pair3(const uint32_t (&l)[4], const uint32_
 __device__ __forceinline__ void hash_window3(const uint4* __restrict__ w, uint32_t p, uint32_t (&d)[4]) {
     uint4 v[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = ld_nt(w + k);
+    for (int k = 0; k < 16; ++k) v[k] = ld_stream(w + k);
     uint32_t m[32];  // message lanes 0..31 as parity-p words
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -1238,8 +1238,8 @@ __global__ __launch_bounds__(256, MK_K64_WAVES) void k_keccak64(const uint4* __r
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint4* p = in + 4 * i;
-    const uint4 v0 = ld_nt(p), v1 = ld_nt(p + 1);
-    const uint4 v2 = ld_nt(p + 2), v3 = ld_nt(p + 3);
+    const uint4 v0 = ld_stream(p), v1 = ld_stream(p + 1);
+    const uint4 v2 = ld_stream(p + 2), v3 = ld_stream(p + 3);
     uint4 d0, d1;
     hash_pair(v0, v1, v2, v3, false, d0, d1);
     out[2 * i] = d0;
@@ -1668,7 +1668,7 @@ __global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ 
             uint2 e[18];
 #pragma unroll
             for (int k = 0; k < 9; ++k) {
-                const uint4 t = (pb + k) < nq ? ld_nt(q + pb + k) : make_uint4(0, 0, 0, 0);
+                const uint4 t = (pb + k) < nq ? ld_stream(q + pb + k) : make_uint4(0, 0, 0, 0);
                 e[2 * k] = make_uint2(t.x, t.y);
                 e[2 * k + 1] = make_uint2(t.z, t.w);
             }
@@ -1697,7 +1697,7 @@ __global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ 
             for (int w = 0; w < 17; ++w) {
                 const uint32_t idx = base + w;
                 if (idx < nwords) {
-                    const uint2 v = ld_nt(p + idx);
+                    const uint2 v = ld_stream(p + idx);
                     s.lo[w] ^= v.x;
                     s.hi[w] ^= v.y;
                 } else if (idx == nwords) {
