@@ -255,9 +255,12 @@ __device__ __forceinline__ void hash_window256_staged(const uint4* __restrict__ 
 // beside the state; the thread's held digests live in its own LDS level
 // slots (k_reduce), so the kernel fits MK_LEAF_SPLIT_WAVES waves per SIMD
 // with 16 KB of LDS per workgroup.  The 128-B line shared by both blocks is
-// fetched twice when it leaves L2 in between (infinity-cache hit).
+// fetched twice when it leaves L2 in between (infinity-cache hit).  The
+// default since plain loads replaced non-temporal ones: 0.4 % faster than the
+// staged form at 2^28, 1-2 % at 2^25 (profiles/r02zg/README.md); the staged
+// form (MK_LEAF_SPLIT=0) lost to it only once its windows stayed in L2.
 #ifndef MK_LEAF_SPLIT
-#define MK_LEAF_SPLIT 0
+#define MK_LEAF_SPLIT 1
 #endif
 #ifndef MK_LEAF_SPLIT_WAVES
 #define MK_LEAF_SPLIT_WAVES 6
