@@ -256,14 +256,17 @@ __device__ __forceinline__ void hash_window256_staged(const uint4* __restrict__ 
 // slots (k_reduce), so the kernel fits MK_LEAF_SPLIT_WAVES waves per SIMD
 // with 16 KB of LDS per workgroup.  The 128-B line shared by both blocks is
 // fetched twice when it leaves L2 in between (infinity-cache hit).  The
-// default since plain loads replaced non-temporal ones: 0.4 % faster than the
-// staged form at 2^28, 1-2 % at 2^25 (profiles/r02zg/README.md); the staged
-// form (MK_LEAF_SPLIT=0) lost to it only once its windows stayed in L2.
+// default since plain loads replaced non-temporal ones: at 6 waves 0.4 %
+// faster than the staged form at 2^28, 1-2 % at 2^25 (profiles/r02zg/README.md),
+// at 5 waves about 1 % more (below).
 #ifndef MK_LEAF_SPLIT
 #define MK_LEAF_SPLIT 1
 #endif
+// 5 waves: 94 VGPRs and no spill, 0.8-1.7 % faster than 6 waves (80 VGPRs,
+// 15 dwords in scratch) and 7 waves (54 spilled) slower still
+// (profiles/r02zi, r02zj).
 #ifndef MK_LEAF_SPLIT_WAVES
-#define MK_LEAF_SPLIT_WAVES 6
+#define MK_LEAF_SPLIT_WAVES 5
 #endif
 __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w, uint4& d0, uint4& d1) {
     State s;
