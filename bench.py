@@ -231,12 +231,6 @@ def main():
     if args.single_process:
         return run_single_process(args)
 
-    import torch
-    import torch.distributed as dist
-
-    from prysm_amd import device as D
-    from prysm_amd import parallel as P
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -245,10 +239,75 @@ def main():
         return 2
     if args.share_device:
         local = 0
+    if world == 1:
+        return run_ranks(args, world, rank, local)
+    # N ranks: every failure (a rank that never joins, a collective that
+    # times out after parallel.dist_timeout(), a HIP/RCCL error) ends this rank
+    # with an error JSON line and a non-zero status instead of a silent hang;
+    # a host-side deadline covers whatever the timeouts do not
+    watchdog = Deadline(float(os.environ.get("PRYSM_BENCH_DEADLINE", "900")),
+                        lambda: error_line(args, world, rank, "deadline exceeded (PRYSM_BENCH_DEADLINE)"))
+    try:
+        return run_ranks(args, world, rank, local)
+    except Exception as e:  # noqa: BLE001 -- reported, then the rank fails
+        error_line(args, world, rank, f"{type(e).__name__}: {e}")
+        return 3
+    finally:
+        watchdog.cancel()
+
+
+class Deadline:
+    """Host-side last resort for the N-rank run: after `seconds` it prints the
+    error line and ends the process with status 124 (os._exit: no exec, and
+    no further GPU call from this thread)."""
+
+    def __init__(self, seconds: float, report):
+        import threading
+
+        self._t = threading.Timer(seconds, self._fire, args=(report,))
+        self._t.daemon = True
+        self._t.start()
+
+    @staticmethod
+    def _fire(report):
+        report()
+        os._exit(124)
+
+    def cancel(self):
+        self._t.cancel()
+
+
+def error_line(args, world: int, rank: int, msg: str) -> None:
+    """The JSON record of a failed N-rank run (rank 0 on stdout, the other
+    ranks on stderr, so the driver still reads one line)."""
+    rec = {"metric": "tree-hash leaves/sec @2^28 chunks (ssz.merkleHash, 32-B leaves)", "value": None,
+           "unit": "leaves/s", "n_gpus": args.gpus, "world_size": world, "rank": rank,
+           "backend": args.backend, "error": msg[:2000]}
+    log(f"rank {rank}: ERROR {msg[:2000]}")
+    print(json.dumps(rec), file=sys.stdout if rank == 0 else sys.stderr, flush=True)
+
+
+def run_ranks(args, world: int, rank: int, local: int) -> int:
+    """One rank of the headline bench (world == 1: the only one)."""
+    import torch
+    import torch.distributed as dist
+
+    from prysm_amd import parallel as P
+
+    if world > 1 and args.backend == "gloo":  # no device needed to rendezvous
+        P.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        P.init_process_group(args.backend, dev)
+    if world > 1 and args.backend == "nccl":
+        P.init_process_group("nccl", dev)
+    from prysm_amd import device as D
+
+    if world > 1:  # what actually initialised, for the record
+        world_pg, backend_pg = dist.get_world_size(), str(dist.get_backend())
+        if world_pg != world:
+            raise RuntimeError(f"process group has {world_pg} ranks, WORLD_SIZE is {world}")
+    else:
+        world_pg, backend_pg = 1, None
 
     n, item_len = 1 << args.log2n, args.item_len
     sp = P.plan(n, item_len, world)
@@ -396,7 +455,7 @@ def main():
                        "shard_height": sp.height, "frontier_log2": k, "pipelined": pipe is not None and k > 0,
                        "root": root_hex, "root_matches_golden": None if golden_root(args.log2n, item_len) is None
                        else root_hex == golden_root(args.log2n, item_len),
-                       "backend": args.backend if world > 1 else None, "share_device": bool(args.share_device),
+                       "backend": backend_pg, "world_size": world_pg, "share_device": bool(args.share_device),
                        "per_rank_ms_per_step_and_leaf_ms": per_rank},
             "roofline": {
                 "bound": "valu-int",

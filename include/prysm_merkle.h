@@ -39,7 +39,10 @@
  *     hipStream_t passed as void* (NULL = the device's default stream); they
  *     enqueue work and return without synchronising.  Their scratch space is
  *     caller-provided (size from the *_workspace_bytes query), so they never
- *     allocate and can be captured into a hipGraph.
+ *     allocate and can be captured into a hipGraph -- except
+ *     mk_dev_ssz_merkle_many (host-planned descriptors, uploaded per call)
+ *     and mk_dev_ssz_merkle_hash_multi (RCCL, library workspaces), which
+ *     refuse / are not meant for capture.
  *   - Thread safety: every entry point may be called concurrently from any OS
  *     thread; host-buffer entry points take a per-device lock, deposit-trie
  *     handles a per-handle lock.
@@ -104,7 +107,10 @@ int mk_dev_ssz_merkle_hash(mk_call* call, const void* d_items, uint64_t n, uint3
  * are HOST arrays (the library plans on the host and uploads the per-list
  * descriptors into the workspace).  Lists of up to 2^15 chunks share one leaf
  * launch and one launch per level; longer lists run their own fused passes.
- * Workspace from mk_ssz_merkle_many_workspace_bytes (same n, item_len). */
+ * Workspace from mk_ssz_merkle_many_workspace_bytes (same n, item_len).
+ * The descriptors go through a small pinned host ring on every call, so the
+ * call cannot be captured into a hipGraph: on a capturing stream it returns
+ * MK_EINVAL. */
 uint64_t mk_ssz_merkle_many_workspace_bytes(const uint64_t* n, const uint32_t* item_len, uint32_t nlists);
 int mk_dev_ssz_merkle_many(mk_call* call, const void* d_items, const uint64_t* offs, const uint64_t* n,
                            const uint32_t* item_len, uint32_t nlists, void* d_roots, void* d_ws, uint64_t ws_bytes,

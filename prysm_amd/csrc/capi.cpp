@@ -110,6 +110,10 @@ struct DevCtx {
     hipEvent_t region_ev[2] = {nullptr, nullptr};  // multi: compute of a shard region done
     bool region_used[2] = {false, false};
     SmallStage small;
+    // mk_dev_ssz_merkle_hash_multi's own frontier blocks / workspaces: that
+    // path enqueues on the caller's streams without this device's `mu`, so it
+    // must never share in/out/ws/aux with the host-buffer entry points
+    DevBuf mout, mws, maux;
 };
 
 std::mutex g_mu;
@@ -506,6 +510,13 @@ int dev_merkle_many(const void* d_items, const mk::ManyPlan& mp, uint32_t nlists
                     (unsigned long long)mp.ws_bytes);
     if (nlists == 0) return MK_OK;
     if (!d_roots || !d_ws) return fail(MK_EINVAL, "null pointer");
+    // the per-list descriptors are planned on the host and uploaded through
+    // the pinned ring: a captured copy node would replay whatever a later
+    // call left in that slot, so this entry point refuses stream capture
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(st, &cap));
+    if (cap != hipStreamCaptureStatusNone)
+        return fail(MK_EINVAL, "mk_dev_ssz_merkle_many cannot be captured into a graph (host-planned descriptors)");
     uint8_t* ws = (uint8_t*)d_ws;
     auto* lists = (mk::ManyList*)(ws + mp.off_lists);
     auto* act = (mk::ManyAct*)(ws + mp.off_act);
@@ -929,14 +940,13 @@ int comms_for(const std::vector<int>& devs, std::vector<ncclComm_t>*& out) {
 // Shard s of the frontier sharding reduced on the bound device: nodes of
 // level (h - k) into d_block (k = 0: the 32-B shard root).
 int launch_shard(const uint8_t* d_items, uint64_t sn, uint32_t item_len, uint32_t h, uint32_t k, uint8_t* d_block,
-                 DevBuf& ws, hipStream_t st, bool grow_ws) {
+                 const DevBuf& ws, hipStream_t st) {
     if (sn == 0) {
         HIPCHK(hipMemsetAsync(d_block, 0, (size_t)32 << k, st));
         return MK_OK;
     }
     Plan p;
     TRY(mk::make_plan(sn, item_len, true, h, true, ((uintptr_t)d_items % 16) == 0, p, false, k));
-    if (grow_ws) TRY(grow(ws, mk::plan_ws_bytes(p)));
     return launch_plan(p, d_items, d_block, (uint8_t*)ws.p, ws.cap, st);
 }
 
@@ -1001,7 +1011,7 @@ int multi_device_worker(const MultiJob& job, const uint8_t* items, const std::ve
         TRY(staged_upload(c, dreg, items + begin[s] * item_len, sn * (size_t)item_len));
         HIPCHK(hipEventRecord(c->h2d, c->copy));
         HIPCHK(hipStreamWaitEvent(c->stream, c->h2d, 0));
-        TRY(launch_shard(dreg, sn, item_len, h, k, (uint8_t*)c->out.p + block * s, c->ws, c->stream, false));
+        TRY(launch_shard(dreg, sn, item_len, h, k, (uint8_t*)c->out.p + block * s, c->ws, c->stream));
         HIPCHK(hipEventRecord(c->region_ev[r], c->stream));
         c->region_used[r] = true;
     }
@@ -1125,32 +1135,48 @@ int dev_merkle_multi(const void* const* d_shards, uint64_t n, uint32_t item_len,
     std::vector<uint64_t> begin(ndev + 1);
     TRY(mk::shard_plan(n, item_len, (uint32_t)ndev, &h, &ne, begin.data()));
     auto stream_of = [&](int d) { return streams && streams[d] ? (hipStream_t)streams[d] : g_ctx[d]->stream; };
+    // one multi call at a time: the mout/mws/maux buffers and the communicator cache
+    std::lock_guard<std::mutex> mlk(g_multi_mu);
     if (ne <= 1 && !(ndev == 1 && h > 5 && force_collective())) {
         TRY(bind_dev(0));
         DevCtx* c = ctx();
         Plan p;
         TRY(mk::make_plan(n, item_len, false, 0, false, ((uintptr_t)d_shards[0] % 16) == 0, p));
-        TRY(grow(c->ws, p.small ? 256 : mk::plan_ws_bytes(p)));
-        return launch_plan(p, (const uint8_t*)d_shards[0], (uint8_t*)d_out32, (uint8_t*)c->ws.p, c->ws.cap,
+        TRY(grow(c->mws, p.small ? 256 : mk::plan_ws_bytes(p)));
+        return launch_plan(p, (const uint8_t*)d_shards[0], (uint8_t*)d_out32, (uint8_t*)c->mws.p, c->mws.cap,
                            stream_of(0));
     }
-    std::lock_guard<std::mutex> mlk(g_multi_mu);
     const uint32_t k = multi_frontier(h);
     const size_t block = (size_t)32 << k;
+    const uint64_t last_nodes = k ? mk::frontier_nodes(begin[ne] - begin[ne - 1], item_len, h, k) : 1;
+    const uint64_t count = ((uint64_t)(ne - 1) << k) + last_nodes;
     std::vector<int> devs(ndev);
     for (int d = 0; d < ndev; ++d) devs[d] = d;
-    for (int d = 0; d < ndev; ++d) {  // every device: its shard to the frontier level, block d
+    // size every buffer (and the communicators) before the first launch, so
+    // no call frees or allocates between its own enqueues
+    for (int d = 0; d < ndev; ++d) {
         TRY(bind_dev(d));
         DevCtx* c = ctx();
-        TRY(grow(c->out, block * ndev + 32));
-        TRY(launch_shard((const uint8_t*)d_shards[d], begin[d + 1] - begin[d], item_len, h, k,
-                         (uint8_t*)c->out.p + block * d, c->ws, stream_of(d), true));
+        TRY(grow(c->mout, block * ndev + 32));
+        const uint64_t sn = begin[d + 1] - begin[d];
+        Plan p;
+        if (sn) {
+            TRY(mk::make_plan(sn, item_len, true, h, true, ((uintptr_t)d_shards[d] % 16) == 0, p, false, k));
+            TRY(grow(c->mws, mk::plan_ws_bytes(p)));
+        }
+        if (d == 0 && k) TRY(grow(c->maux, finish_ws_bytes(count)));
     }
     std::vector<ncclComm_t>* comms = nullptr;
     TRY(comms_for(devs, comms));
+    for (int d = 0; d < ndev; ++d) {  // every device: its shard to the frontier level, block d
+        TRY(bind_dev(d));
+        DevCtx* c = ctx();
+        TRY(launch_shard((const uint8_t*)d_shards[d], begin[d + 1] - begin[d], item_len, h, k,
+                         (uint8_t*)c->mout.p + block * d, c->mws, stream_of(d)));
+    }
     if (ncclGroupStart() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupStart");
     for (int d = 0; d < ndev; ++d) {
-        uint8_t* lvl = (uint8_t*)g_ctx[d]->out.p;
+        uint8_t* lvl = (uint8_t*)g_ctx[d]->mout.p;
         if (ncclAllGather(lvl + block * d, lvl, block, ncclUint8, (*comms)[d], stream_of(d)) != ncclSuccess) {
             ncclGroupEnd();
             return fail(MK_ECOMM, "ncclAllGather on device %d", d);
@@ -1159,13 +1185,8 @@ int dev_merkle_multi(const void* const* d_shards, uint64_t n, uint32_t item_len,
     if (ncclGroupEnd() != ncclSuccess) return fail(MK_ECOMM, "ncclGroupEnd");
     TRY(bind_dev(0));
     DevCtx* c0 = ctx();
-    const uint64_t last_nodes = k ? mk::frontier_nodes(begin[ne] - begin[ne - 1], item_len, h, k) : 1;
-    const uint64_t count = ((uint64_t)(ne - 1) << k) + last_nodes;
-    if (k) {
-        TRY(grow(c0->aux, finish_ws_bytes(count)));
-        return dev_finish_nodes(c0->out.p, count, n, d_out32, c0->aux.p, c0->aux.cap, stream_of(0));
-    }
-    return dev_finish(c0->out.p, ne, n, d_out32, stream_of(0));
+    if (k) return dev_finish_nodes(c0->mout.p, count, n, d_out32, c0->maux.p, c0->maux.cap, stream_of(0));
+    return dev_finish(c0->mout.p, ne, n, d_out32, stream_of(0));
 }
 
 }  // namespace

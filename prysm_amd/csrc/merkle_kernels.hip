@@ -539,80 +539,6 @@ template __global__ void k_reduce<true, true, 1>(ReduceArgs);
 template __global__ void k_reduce<true, false, 1>(ReduceArgs);
 
 // ----------------------------------------------------------------------------
-// Latency-oriented pass for the narrow top of the tree: one wave per
-// workgroup, one first-level node per lane, then up to 6 more levels inside
-// the wave (LDS hand-off, no cross-wave barrier).  Every level costs one
-// permutation latency, instead of the 2-4 serial permutations per level the
-// throughput kernel spends when few workgroups exist.
-template <bool LEAF>
-__global__ __launch_bounds__(kWaveThreads) void k_wave(ReduceArgs a) {
-    __shared__ uint4 lds[2 * kWaveThreads];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t wg = a.wg_base + blockIdx.x;
-    const uint64_t lo1 = wg * kWaveThreads;
-    const uint64_t c1 = a.c1;
-    const uint64_t m1 = (c1 - lo1) < kWaveThreads ? (c1 - lo1) : kWaveThreads;
-    if (tid < m1) {
-        const uint64_t j = lo1 + tid;
-        uint4 d0, d1;
-        if (LEAF && j < a.c1_full) {
-            hash_window256(reinterpret_cast<const uint4*>(a.items) + j * 16, d0, d1);
-        } else {
-            first_level_generic<LEAF>(a, j, d0, d1);
-        }
-        lds[2 * tid] = d0;
-        lds[2 * tid + 1] = d1;
-    }
-    __syncthreads();
-    uint64_t c = c1, m = m1;
-    int left = a.finalize ? 64 : (int)a.levels - 1;
-    int done = 0;
-    while (left > 0 && (c > 1 || a.pad_at_one)) {
-        const uint64_t mn = (m + 1) / 2;
-        const bool act = tid < mn;
-        uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0;
-        bool padded = false;
-        if (act) {
-            l0 = lds[4 * tid];
-            l1 = lds[4 * tid + 1];
-            padded = !(2 * (uint64_t)tid + 1 < m);
-            if (!padded) {
-                r0 = lds[4 * tid + 2];
-                r1 = lds[4 * tid + 3];
-            }
-        }
-        __syncthreads();
-        if (act) {
-            uint4 d0, d1;
-            hash_pair(l0, l1, r0, r1, padded, d0, d1);
-            lds[2 * tid] = d0;
-            lds[2 * tid + 1] = d1;
-        }
-        __syncthreads();
-        c = (c + 1) / 2;
-        m = mn;
-        --left;
-        ++done;
-    }
-    uint4* out = reinterpret_cast<uint4*>(a.out);
-    if (a.finalize) {
-        if (tid == 0) {
-            uint4 d0, d1;
-            hash_final(lds[0], lds[1], a.n_items, d0, d1);
-            out[0] = d0;
-            out[1] = d1;
-        }
-    } else if (tid < m) {
-        const uint64_t lo_out = lo1 >> done;
-        out[2 * (lo_out + tid)] = lds[2 * tid];
-        out[2 * (lo_out + tid) + 1] = lds[2 * tid + 1];
-    }
-}
-
-template __global__ void k_wave<true>(ReduceArgs);
-template __global__ void k_wave<false>(ReduceArgs);
-
-// ----------------------------------------------------------------------------
 // Latency pass with two lanes per state (keccak_dev.hpp, mk::pair): lane pair
 // (2k, 2k+1) owns node k; the even lane carries the low 32-bit halves of the
 // Keccak lanes, the odd lane the high halves.  Nodes live in LDS as 8 dwords;
@@ -1064,63 +990,6 @@ template __global__ void k_wave3<256, true>(ReduceArgs);
 template __global__ void k_wave3<512, true>(ReduceArgs);
 template __global__ void k_wave3<1024, true>(ReduceArgs);
 
-// Narrow top of the deposit trie, two lanes per state: the workgroup owns 64
-// input nodes of level d and writes up to `levels` levels to the level array;
-// once the count is 1 it continues with node = K(node || 0^32) (the levels
-// above the last populated one, deposit_trie.go:33-38), so the top of the
-// trie and its zero-sibling tail are one launch.
-__global__ __launch_bounds__(kWaveThreads) void k_trie_top2(const uint32_t* __restrict__ in, uint64_t cin,
-                                                            uint32_t* __restrict__ lv_out, uint32_t levels) {
-    __shared__ uint32_t lds[8 * kWave2Span];
-    const uint32_t tid = threadIdx.x, k = tid >> 1;
-    const bool odd = (tid & 1u) != 0;
-    const uint32_t p = odd ? 1u : 0u;
-    uint64_t c = cin;
-    uint64_t lo = (uint64_t)blockIdx.x * 2 * kWave2Span;  // first input node of this workgroup
-    uint64_t m = (c - lo) < 2 * kWave2Span ? (c - lo) : 2 * kWave2Span;
-    uint32_t* dst = lv_out;
-    for (uint32_t l = 0; l < levels; ++l) {
-        const uint64_t cn = (c + 1) / 2, mn = (m + 1) / 2;
-        const bool act = k < mn;
-        uint32_t a[4], b[4] = {0, 0, 0, 0};
-        if (act) {
-            const bool right = 2 * (uint64_t)k + 1 < m;
-            if (l == 0) {
-                const uint64_t base = 8 * (lo + 2 * (uint64_t)k);
-#pragma unroll
-                for (int w = 0; w < 4; ++w) a[w] = in[base + 2 * w + p];
-                if (right) {
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) b[w] = in[base + 8 + 2 * w + p];
-                }
-            } else {
-#pragma unroll
-                for (int w = 0; w < 4; ++w) a[w] = lds[16 * k + 2 * w + p];
-                if (right) {
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) b[w] = lds[16 * k + 8 + 2 * w + p];
-                }
-            }
-        }
-        __syncthreads();
-        if (act) {
-            uint32_t d[4];
-            hash_pair2(a, b, false, odd, d);
-            const uint64_t g = lo / 2 + k;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                lds[8 * k + 2 * w + p] = d[w];
-                dst[8 * g + 2 * w + p] = d[w];
-            }
-        }
-        __syncthreads();
-        dst += 8 * cn;
-        c = cn;
-        m = mn;
-        lo /= 2;
-    }
-}
-
 // Narrow top of the deposit trie, bit-interleaved lane pairs (mk::ilv): the
 // workgroup owns NT input nodes of level d (NT/2 lane pairs) and writes
 // `levels` levels to the (plain) level array; once the count is 1 it goes on
@@ -1186,50 +1055,6 @@ __global__ void k_final_small(const uint8_t* __restrict__ items, uint64_t total,
     sponge_generic(items, total, n == 0 ? 128u : 0u, true, n, d0, d1);
     reinterpret_cast<uint4*>(out)[0] = d0;
     reinterpret_cast<uint4*>(out)[1] = d1;
-}
-
-// Multi-GPU finisher: the reference loop over `nroots` 32-B subtree roots
-// (odd -> 0^128 pad), then the length mix-in.  One workgroup.
-__global__ __launch_bounds__(kReduceThreads) void k_finish_roots(const uint4* __restrict__ roots, uint64_t nroots,
-                                                               uint64_t n_items, uint4* out) {
-    __shared__ uint4 lds[2 * kReduceSpan2];
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t k = tid; k < nroots; k += kReduceThreads) {
-        lds[2 * k] = roots[2 * k];
-        lds[2 * k + 1] = roots[2 * k + 1];
-    }
-    __syncthreads();
-    uint64_t m = nroots;
-    while (m > 1) {
-        const uint64_t mn = (m + 1) / 2;
-        const bool act = tid < mn;
-        uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0;
-        bool padded = false;
-        if (act) {
-            l0 = lds[4 * tid];
-            l1 = lds[4 * tid + 1];
-            padded = !(2 * (uint64_t)tid + 1 < m);
-            if (!padded) {
-                r0 = lds[4 * tid + 2];
-                r1 = lds[4 * tid + 3];
-            }
-        }
-        __syncthreads();
-        if (act) {
-            uint4 d0, d1;
-            hash_pair(l0, l1, r0, r1, padded, d0, d1);
-            lds[2 * tid] = d0;
-            lds[2 * tid + 1] = d1;
-        }
-        __syncthreads();
-        m = mn;
-    }
-    if (tid == 0) {
-        uint4 d0, d1;
-        hash_final(lds[0], lds[1], n_items, d0, d1);
-        out[0] = d0;
-        out[1] = d1;
-    }
 }
 
 // ----------------------------------------------------------------------------
@@ -1768,61 +1593,6 @@ __global__ __launch_bounds__(kRecThreads) void k_keccak_rec(const uint2* __restr
 }
 template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 
-
-// Deposit-trie levels, fused: the workgroup owns input nodes
-// [512*wg, 512*wg + 512) of level d (count cin) and writes `levels` levels
-// d+1 .. d+levels to their slots of the level array (every level is kept:
-// GenerateMerkleBranch reads them).  Missing right child = 0^32
-// (deposit_trie.go:35-37).  One node per thread per level.
-__global__ __launch_bounds__(256) void k_trie_reduce(const uint4* __restrict__ in, uint64_t cin,
-                                                     uint4* __restrict__ lv_out, uint32_t levels) {
-    __shared__ uint4 lds[2 * 256];
-    const uint32_t tid = threadIdx.x;
-    const uint64_t wg = blockIdx.x;
-    uint64_t c = cin;                          // global count of the input level
-    uint64_t lo = wg * 512;                    // first input node of this workgroup
-    uint64_t m = (c - lo) < 512 ? (c - lo) : 512;
-    uint4* dst = lv_out;                       // start of level d+1
-    for (uint32_t l = 0; l < levels && c > 1; ++l) {
-        const uint64_t cn = (c + 1) / 2, mn = (m + 1) / 2;
-        const bool act = tid < mn;
-        uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0;
-        if (act) {
-            if (l == 0) {
-                const uint64_t a = 2 * (lo + 2 * (uint64_t)tid);  // uint4 index of input node lo + 2*tid
-                l0 = in[a];
-                l1 = in[a + 1];
-                if (2 * (uint64_t)tid + 1 < m) {
-                    r0 = in[a + 2];
-                    r1 = in[a + 3];
-                }
-            } else {
-                l0 = lds[4 * tid];
-                l1 = lds[4 * tid + 1];
-                if (2 * (uint64_t)tid + 1 < m) {
-                    r0 = lds[4 * tid + 2];
-                    r1 = lds[4 * tid + 3];
-                }
-            }
-        }
-        __syncthreads();
-        if (act) {
-            uint4 d0, d1;
-            hash_pair(l0, l1, r0, r1, false, d0, d1);
-            lds[2 * tid] = d0;
-            lds[2 * tid + 1] = d1;
-            const uint64_t g = lo / 2 + tid;  // global index at level d+l+1
-            dst[2 * g] = d0;
-            dst[2 * g + 1] = d1;
-        }
-        __syncthreads();
-        dst += 2 * cn;
-        c = cn;
-        m = mn;
-        lo /= 2;
-    }
-}
-
 // ----------------------------------------------------------------------------
 // Deposit trie level: node j = K(in[2j] || (2j+1 < cin ? in[2j+1] : 0^32)),
 // the map-miss-reads-zero rule of deposit_trie.go:35-37.
@@ -1840,22 +1610,6 @@ __global__ __launch_bounds__(256) void k_trie_level(const uint4* __restrict__ in
     hash_pair(l0, l1, r0, r1, false, d0, d1);
     out[2 * j] = d0;
     out[2 * j + 1] = d1;
-}
-
-// Levels above the last populated one: node = K(node || 0^32), `count` times;
-// levels[i] receives the node of the i-th level above `node` (the last one is
-// the root).
-__global__ void k_trie_tail(uint4* __restrict__ node, uint32_t count, uint4* __restrict__ levels) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    uint4 a0 = node[0], a1 = node[1];
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    for (uint32_t i = 0; i < count; ++i) {
-        hash_pair(a0, a1, z, z, false, a0, a1);
-        if (levels) {
-            levels[2 * i] = a0;
-            levels[2 * i + 1] = a1;
-        }
-    }
 }
 
 // Batched VerifyMerkleBranch (deposit_trie.go:68-81): thread i folds its

@@ -36,13 +36,10 @@ __global__ void k_struct_split(const uint8_t* rec, uint64_t n, StructSpec sp, ui
 #endif
 constexpr uint64_t kStructSplitMaxN = MK_STRUCT_SPLIT_MAX_N;  // k_struct_split at or below (0: never)
 template <bool LEAF>
-__global__ void k_wave(ReduceArgs a);
-template <bool LEAF>
 __global__ void k_wave2(ReduceArgs a);
 template <uint32_t NT, bool LEAF>
 __global__ void k_wave3(ReduceArgs a);
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
-__global__ void k_finish_roots(const uint4* roots, uint64_t nroots, uint64_t n_items, uint4* out);
 __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);
 __global__ void k_keccak_fixed(const uint8_t* in, uint64_t n, uint32_t msg_len, uint4* out);
 __global__ void k_keccak_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint4* out);
@@ -59,11 +56,8 @@ constexpr uint32_t kRecThreads = MK_REC_THREADS;  // k_keccak_rec workgroup size
 #define MK_REC_GRID 4096
 #endif
 constexpr uint32_t kRecGridMax = MK_REC_GRID;  // k_keccak_rec grid cap (A/B at 2^20: 512..4096 WGs, 4096 best)
-__global__ void k_trie_reduce(const uint4* in, uint64_t cin, uint4* lv_out, uint32_t levels);
-__global__ void k_trie_top2(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels);
 template <uint32_t NT>
 __global__ void k_trie_top3(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels, uint64_t capn);
-__global__ void k_trie_tail(uint4* node, uint32_t count, uint4* levels);
 __global__ void k_verify_branches(const uint4* leaves, const uint4* branches, const uint64_t* indices,
                                   uint32_t depth, uint32_t tree_depth, const uint4* roots, uint64_t n,
                                   uint8_t* ok);

@@ -10,9 +10,7 @@ constexpr uint32_t kReduceThreads = 256;             // 4 waves
 constexpr uint64_t kReduceSpan1 = 4 * kReduceThreads;  // first-level nodes per workgroup
 constexpr uint64_t kReduceSpan2 = kReduceSpan1 / 2;    // level-2 nodes per workgroup (LDS)
 constexpr uint32_t kMaxPassLevels = 5;               // levels per non-final pass (1024 -> 64)
-constexpr uint32_t kWaveThreads = 64;                // latency pass: one wave per workgroup
-constexpr uint32_t kWaveLevels = 7;                  // first level + 6 in-wave levels (64 -> 1)
-constexpr uint64_t kWaveMaxC1 = 1ull << 16;          // use the latency pass at or below this width (A/B: 2^19 is slower)
+constexpr uint32_t kWaveThreads = 64;                // k_wave2: one wave per workgroup
 constexpr uint32_t kWave2Span = kWaveThreads / 2;    // two lanes per state: 32 nodes per wave
 constexpr uint32_t kWave2Levels = 6;                 // first level + 5 in-wave levels (32 -> 1)
 constexpr uint32_t kMidThreads = 1024;               // largest k_wave3: 16 waves, 512 lane pairs, 10 levels

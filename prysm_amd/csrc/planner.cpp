@@ -37,14 +37,12 @@ mk_call* swap_call(mk_call* c) {
 }
 
 // ---- configuration (compile-time knobs; A/B variants via the Makefile) ----------
-#ifndef MK_WAVE2
-#define MK_WAVE2 1
-#endif
-constexpr bool kWave2 = MK_WAVE2 != 0;  // two-lanes-per-state latency pass
+// latency passes: k_wave2 (two lanes per state, lo/hi halves) or, by default,
+// k_wave3 (bit-interleaved lane pairs, one state per wave at the top)
 #ifndef MK_WAVE3
 #define MK_WAVE3 1
 #endif
-constexpr bool kWave3 = kWave2 && MK_WAVE3 != 0;  // node latency passes bit-interleaved (k_wave3)
+constexpr bool kWave3 = MK_WAVE3 != 0;  // node latency passes bit-interleaved (k_wave3)
 #ifndef MK_NODE_WAVE_MAX_LOG2
 #define MK_NODE_WAVE_MAX_LOG2 17
 #endif
@@ -191,10 +189,10 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         const uint32_t ni = (!wave && leaf && c1 < kReduceNi2MinC1) ? 1 : 2;
         if (sp) nt = 1024;
         const uint64_t span = sp ? kSpreadSpan
-                            : w3 ? nt / 2 : wave ? (kWave2 ? kWave2Span : kWaveThreads) : (uint64_t)2 * ni * kReduceThreads;
+                            : w3 ? nt / 2 : wave ? kWave2Span : (uint64_t)2 * ni * kReduceThreads;
         const bool final_pass = c1 <= span;
         const uint32_t max_lv = sp ? 1 + ilog2(kSpreadSpan)
-                              : w3 ? 1 + ilog2(nt / 2) : wave ? (kWave2 ? kWave2Levels : kWaveLevels) : kMaxPassLevels;
+                              : w3 ? 1 + ilog2(nt / 2) : wave ? kWave2Levels : kMaxPassLevels;
         uint32_t lv = final_pass ? remaining : std::min<uint32_t>(max_lv, remaining);
         for (uint32_t l = 1; l < lv; ++l) {  // fused levels above the first
             if (c <= 1 && !pad_at_one) break;

@@ -19,25 +19,38 @@ defaults are the HIP entry points of prysm_amd.device.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
+from datetime import timedelta
 from typing import Callable, Optional
 
 import torch
 import torch.distributed as dist
 
 
-def init_process_group(backend: str, device=None) -> None:
+def dist_timeout() -> timedelta:
+    """Collective / rendezvous timeout of the bench's process group: 120 s
+    unless PRYSM_DIST_TIMEOUT (seconds) says otherwise.  torch's default (10
+    minutes) would let a hung first cross-device RCCL init or all-gather burn
+    a whole driver run silently."""
+    return timedelta(seconds=float(os.environ.get("PRYSM_DIST_TIMEOUT", "120")))
+
+
+def init_process_group(backend: str, device=None, timeout: Optional[timedelta] = None) -> None:
     """One process per GPU.  With backend "nccl" (RCCL over xGMI) the
     process group's internal stream is created at high priority: the frontier
     all-gather then gets its own hardware queue instead of queueing behind
     the next leaf pass that the main stream has already issued (the same rule
-    as every side stream here)."""
+    as every side stream here).  Every rendezvous and
+    collective gives up after `timeout` (dist_timeout() by default) instead
+    of waiting forever for a rank that never comes."""
+    timeout = timeout or dist_timeout()
     if backend == "nccl":
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
-        dist.init_process_group("nccl", device_id=device, pg_options=opts)
+        dist.init_process_group("nccl", device_id=device, pg_options=opts, timeout=timeout)
     else:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, timeout=timeout)
 
 
 class SlotRing:

@@ -4,6 +4,8 @@ synthetic inputs bench.py / tools/bench_configs.py use, so the GPU tests can
 check the device path bit-exactly at full size (restatement-derived, like
 restatement_vectors.json; the oracle is pinned by reference_vectors.json).
 
+  c1: TreeHash([]*ValidatorRecord) of 16,384 synthetic validators (C struct
+      roots + merkleHash, cross-checked against the reflective ssz_ref walk)
   c2: hashutil.Hash of 2^24 x 64-B SplitMix64 messages -> Keccak-256 of the
       concatenated 2^24 digests (a checksum of checksums)
   c3: TreeHash of State{1,000,000 synthetic validators, balances}
@@ -13,7 +15,7 @@ restatement_vectors.json; the oracle is pinned by reference_vectors.json).
       with 1,000,000 validators (oracle/ssz_ref.py's reflective restatement,
       the registry root from the C oracle's struct roots + merkleHash)
 
-Run:  python tests/golden/make_full_size.py [c2,c3,c3_state,c4,c5]
+Run:  python tests/golden/make_full_size.py [c1,c2,c3,c3_state,c4,c5]
 (C oracle, all host cores; about a minute on 8 cores; named configs are
 recomputed and merged into the existing file).
 """
@@ -72,6 +74,29 @@ def main(only=None):
             out = json.load(f)
     want = lambda c: not only or c in only  # noqa: E731
     t0 = time.time()
+
+    if want("c1"):
+        # BASELINE config 1: ssz.TreeHash([]*ValidatorRecord) of 16,384
+        # synthetic validators (bench_configs.py c1's seeded registry).  Two
+        # independent oracle paths must agree: the C struct roots + merkleHash
+        # and the reflective type walk of ssz/hash.go:118-159 (ssz_ref.py).
+        from oracle import ssz_ref as OS
+        from prysm_amd import registry as R
+
+        n = 16_384
+        reg = R.synthetic_registry(n, SEED + 1)
+        roots = O.struct_roots(reg.records.view(np.uint8).reshape(-1), n, 160, R.VALIDATOR_FIELDS, nthreads=nt)
+        root = O.merkle_hash_flat(roots.reshape(-1), n, 32, nthreads=nt)
+        t_ref = ("slice", ("ptr", ("struct", "ssz.ValidatorRecord",
+                                   [("Pubkey", ("bytes",)), ("WithdrawalCredentialsHash32", ("bytes",)),
+                                    ("RandaoCommitmentHash32", ("bytes",))] +
+                                   [(f, ("uint", 64)) for f in ("RandaoLayers", "ActivationEpoch", "ExitEpoch",
+                                                                "WithdrawalEpoch", "PenalizedEpoch", "StatusFlags")])))
+        refl = OS.tree_hash(t_ref, reg.as_dicts())
+        assert refl == root, "c1: reflective restatement and C struct path disagree"
+        out["c1"] = {"n": n, "seed": SEED + 1, "root": root.hex(),
+                     "generator": "registry.synthetic_registry(16384, seed) (SplitMix64 stream)",
+                     "checked": "C oracle struct roots + merkleHash == reflective ssz_ref.tree_hash"}
 
     if want("c2"):
         n = 1 << 24

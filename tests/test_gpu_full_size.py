@@ -2,6 +2,8 @@
 results (tests/golden/full_size_roots.json, tests/golden/make_full_size.py):
 the same seeded synthetic inputs bench.py measures, checked bit-exactly.
 
+  c1  16,384-validator TreeHash (typed Hashable path, reflective mirror,
+      device-resident records)
   c2  2^24 x 64-B Hash           (Keccak-256 of the 2^24 digests)
   c3  1,000,000-validator State  (registry root, balances root, state root)
   c4  2^28 x 32-B merkleHash     (8 GiB on the device), unsharded, as
@@ -71,6 +73,28 @@ def test_c4_full_2p28(gpu):
     torch.cuda.synchronize()
     assert pipe.k == 21 and [bytes(r.cpu().numpy()).hex() for r in roots] == [g["root"]] * 2
     del items
+
+
+@pytest.mark.gpu
+def test_c1_full_16384_validators(gpu):
+    """BASELINE config 1 at its size: ssz.TreeHash([]*ValidatorRecord) of
+    16,384 validators (shared/ssz/hash.go:118-159) through the typed Hashable
+    path, the reflective mirror and the device-resident struct-list call."""
+    import torch
+
+    from prysm_amd import device as D
+    from prysm_amd import registry as R
+    from prysm_amd import ssz as S
+
+    g = GOLD["c1"]
+    reg = R.synthetic_registry(g["n"], g["seed"])
+    assert reg.tree_hash_ssz().hex() == g["root"]
+    assert S.tree_hash(reg, R.REGISTRY_HASHABLE).hex() == g["root"]
+    assert S.tree_hash(reg.as_dicts(), S.Slice(S.Ptr(R.VALIDATOR_SSZ))).hex() == g["root"]
+    drec = torch.from_numpy(reg.records.view(np.uint8).reshape(-1).copy()).to(gpu)
+    root = D.struct_list_root(drec, g["n"], 160, R.VALIDATOR_FIELDS)
+    torch.cuda.synchronize()
+    assert bytes(root.cpu().numpy()).hex() == g["root"]
 
 
 @pytest.mark.gpu

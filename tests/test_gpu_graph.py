@@ -114,3 +114,35 @@ def test_graph_deposit_trie_append(gpu):
     g_one.replay()
     torch.cuda.synchronize()
     assert bytes(root.cpu().numpy()) == O.deposit_trie_levels(deps, depth)[0]
+
+
+def test_graph_capture_refused_by_merkle_many(gpu):
+    """mk_dev_ssz_merkle_many plans its descriptors on the host and uploads
+    them through a pinned ring on every call; a captured copy would replay a
+    slot a later call overwrote, so a capturing stream gets MK_EINVAL (and the
+    same call outside capture still works)."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import _lib
+    from prysm_amd import device as D
+
+    ns, ils = [300, 17, 1], [32, 8, 32]
+    offs = [0, 300 * 32, 300 * 32 + 17 * 8 + 8]
+    items = torch.empty(offs[-1] + 32, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 11)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    err = None
+    with torch.cuda.graph(g):
+        try:
+            D.merkle_many(items, offs, ns, ils)
+        except _lib.MerkleError as e:
+            err = e
+    assert err is not None and err.code == _lib.MK_EINVAL and "captured" in str(err)
+    roots = D.merkle_many(items, offs, ns, ils)
+    torch.cuda.synchronize()
+    host = items.cpu().numpy()
+    for i in range(3):
+        want = O.merkle_hash_flat(host[offs[i]:offs[i] + ns[i] * ils[i]], ns[i], ils[i])
+        assert bytes(roots[32 * i:32 * i + 32].cpu().numpy()) == want

@@ -68,8 +68,10 @@ def test_multi_golden_2p26_eight_shards(gpu):
 
 @pytest.mark.parametrize("ndev", [2, 4, 8])
 def test_multi_rccl_devices(gpu, ndev):
-    """One shard per device, RCCL all-gather of the frontiers (xGMI): the
-    golden-size C4 tree and a ragged n, host and device-resident forms."""
+    """One shard per device, RCCL all-gather of the frontiers (xGMI): a ragged
+    n and 2^24 items (host and device-resident forms, vs the oracle), then the
+    golden-size C4 tree (2^28 items generated shard by shard on the devices,
+    vs tests/golden/full_size_roots.json)."""
     import torch
 
     from oracle import oracle as O
@@ -78,6 +80,20 @@ def test_multi_rccl_devices(gpu, ndev):
 
     if _lib.device_count() < ndev:
         pytest.skip(f"needs {ndev} GPUs, {_lib.device_count()} visible")
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "full_size_roots.json")))["c4"]
+    n, il = g["n"], g["item_len"]
+    h, ne, begin = D.shard_plan(n, il, ndev)
+    shards = []
+    for d in range(ndev):
+        t = torch.empty((begin[d + 1] - begin[d]) * il, dtype=torch.uint8, device=f"cuda:{d}")
+        D.synth_fill(t, g["seed"], begin[d] * il // 8)
+        shards.append(t)
+    out = torch.empty(32, dtype=torch.uint8, device="cuda:0")
+    D.merkle_hash_multi(shards, n, il, out)
+    for d in range(ndev):
+        torch.cuda.synchronize(d)
+    assert bytes(out.cpu().numpy()).hex() == g["root"]
+    del shards
     for n in (999_999, 1 << 24):
         items = O.splitmix_bytes(n * 32, SEED + 77)
         want = O.merkle_hash_flat(items, n, 32, nthreads=16)
@@ -107,6 +123,39 @@ def test_dev_multi_single_device(gpu):
     D.merkle_hash_multi([items], n, 32, out)
     torch.cuda.synchronize()
     assert bytes(out.cpu().numpy()) == O.merkle_hash_gen(n, 32, SEED + 5, nthreads=16)
+
+
+def test_dev_multi_then_host_call_unsynchronised(gpu):
+    """A host-buffer merkleHash issued right after a device-resident multi
+    call, with no synchronisation in between: the multi path has its own
+    per-device buffers, so neither root is disturbed (the host call runs on
+    the library's stream while the multi call's work is still queued on the
+    caller's)."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    n1, n2 = 1 << 20, 200_003
+    items = torch.empty(n1 * 32, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 31)
+    host = O.splitmix_bytes(n2 * 32, SEED + 32)
+    out = torch.empty(32, dtype=torch.uint8, device=gpu)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        D.merkle_hash_multi([items], n1, 32, out)
+        got2 = _host_merkle(host, n2, 32)
+        torch.cuda.synchronize()
+        assert bytes(out.cpu().numpy()) == O.merkle_hash_gen(n1, 32, SEED + 31, nthreads=16)
+        assert got2 == O.merkle_hash_flat(host, n2, 32, nthreads=16)
+
+
+def _host_merkle(items: np.ndarray, n: int, item_len: int) -> bytes:
+    from prysm_amd import _lib
+
+    out = ctypes.create_string_buffer(32)
+    _lib.invoke("mk_ssz_merkle_hash", items.ctypes.data_as(ctypes.c_void_p), n, item_len, out)
+    return out.raw
 
 
 def test_call_context_errors_and_device_restore(gpu):

@@ -455,7 +455,7 @@ def test_verify_branches_batch(gpu):
 
 
 # ------------------------------------------------------------------ typed registry (Hashable plugin)
-@pytest.mark.parametrize("n", [1, 2, 5, 300, 4099, 70_001])
+@pytest.mark.parametrize("n", [1, 2, 5, 300, 4099, 16_384, 70_001])
 def test_registry_struct_roots_and_list_root(gpu, n):
     from oracle import oracle as O
     from prysm_amd import registry as R
