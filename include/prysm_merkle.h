@@ -119,6 +119,21 @@ int mk_dev_ssz_merkle_many(mk_call* call, const void* d_items, const uint64_t* o
 int mk_ssz_merkle_many(mk_call* call, const uint8_t* items, const uint64_t* offs, const uint64_t* n,
                        const uint32_t* item_len, uint32_t nlists, uint8_t* roots);
 
+/* ---- ssz.TreeHash of a list of byte strings (hash.go:100-107, 118-139) -- */
+/* TreeHash([][N]byte) / TreeHash([][]byte) with n elements of elem_len bytes
+ * each, contiguous: makeSliceHasher hashes every element with hashedEncoding
+ * (Keccak(le32(elem_len) || element)) and runs merkleHash over those 32-B
+ * digests.  One call, no host round trip: with 32-B elements (16-B aligned)
+ * the digests are computed inside the tree's leaf pass and never reach HBM.
+ * Workspace from mk_ssz_tree_hash_bytes_list_workspace_bytes (for a 16-B
+ * aligned d_elems; other alignments need the two-phase size, n*32 + the
+ * plan's, and report MK_ENOMEM when the workspace is short). */
+uint64_t mk_ssz_tree_hash_bytes_list_workspace_bytes(uint64_t n, uint32_t elem_len);
+int mk_dev_ssz_tree_hash_bytes_list(mk_call* call, const void* d_elems, uint64_t n, uint32_t elem_len,
+                                    void* d_out32, void* d_ws, uint64_t ws_bytes, void* stream);
+int mk_ssz_tree_hash_bytes_list(mk_call* call, const uint8_t* elems, uint64_t n, uint32_t elem_len,
+                                uint8_t out[32]);
+
 /* ---- subtree sharding across GPUs ----------------------- */
 /* Split a merkleHash of n items over `nshards` devices: every shard is a
  * power-of-two-aligned run of 2^height chunks.  item_begin[nshards+1] gets

@@ -141,6 +141,29 @@ def merkle_hash(lst) -> bytes:
     return out.raw
 
 
+def elem_digests(elems: np.ndarray, n: int, elem_len: int, nthreads: int = 1, chunk: int = 1 << 22) -> np.ndarray:
+    """hashedEncoding of n byte strings of elem_len bytes (hash.go:100-107):
+    Keccak(le32(elem_len) || element) -> (n, 32), in chunks of messages."""
+    elems = np.ascontiguousarray(elems, dtype=np.uint8).reshape(-1)
+    out = np.empty((n, 32), dtype=np.uint8)
+    pre = np.frombuffer(int(elem_len).to_bytes(4, "little"), dtype=np.uint8)
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        msgs = np.empty((hi - lo, 4 + elem_len), dtype=np.uint8)
+        msgs[:, :4] = pre
+        if elem_len:
+            msgs[:, 4:] = elems[lo * elem_len:hi * elem_len].reshape(hi - lo, elem_len)
+        out[lo:hi] = keccak256_batch(msgs.reshape(-1), 4 + elem_len, nthreads)
+    return out
+
+
+def tree_hash_bytes_list(elems: np.ndarray, n: int, elem_len: int, nthreads: int = 1) -> bytes:
+    """ssz.TreeHash of a slice of n byte strings of elem_len bytes
+    (makeSliceHasher, hash.go:118-139): merkleHash over their hashedEncoding
+    digests.  Composition of the pinned Keccak and merkleHash restatements."""
+    return merkle_hash_flat(elem_digests(elems, n, elem_len, nthreads).reshape(-1), n, 32, nthreads)
+
+
 def merkle_hash_gen(n: int, item_len: int, seed: int, nthreads: int = 1) -> bytes:
     out = ctypes.create_string_buffer(32)
     rc = lib().or_merkle_hash_gen(n, item_len, seed, out, nthreads)

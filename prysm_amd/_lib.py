@@ -57,6 +57,9 @@ _SIGS = {
     "mk_ssz_merkle_hash": (_int, [_cp, _vp, _u64, _u32, _vp]),
     "mk_ssz_merkle_workspace_bytes": (_u64, [_u64, _u32]),
     "mk_dev_ssz_merkle_hash": (_int, [_cp, _vp, _u64, _u32, _vp, _vp, _u64, _vp]),
+    "mk_ssz_tree_hash_bytes_list_workspace_bytes": (_u64, [_u64, _u32]),
+    "mk_dev_ssz_tree_hash_bytes_list": (_int, [_cp, _vp, _u64, _u32, _vp, _vp, _u64, _vp]),
+    "mk_ssz_tree_hash_bytes_list": (_int, [_cp, _vp, _u64, _u32, _vp]),
     "mk_ssz_merkle_many_workspace_bytes": (_u64, [_vp, _vp, _u32]),
     "mk_dev_ssz_merkle_many": (_int, [_cp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _u64, _vp]),
     "mk_ssz_merkle_many": (_int, [_cp, _vp, _vp, _vp, _vp, _u32, _vp]),

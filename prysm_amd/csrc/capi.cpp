@@ -332,7 +332,10 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                 }
                 ReduceArgs g = a;
                 g.wg_base = ps.nfast;
-                if (ps.leaf && ps.ni == 1)
+                if (ps.leaf && a.elem_len)  // planned with NI = 1
+                    hipLaunchKernelGGL((mk::k_reduce_elem<false>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads), 0,
+                                       gs, g);
+                else if (ps.leaf && ps.ni == 1)
                     hipLaunchKernelGGL((mk::k_reduce<true, false, 1>), dim3(ps.nwg - ps.nfast), dim3(kReduceThreads),
                                        0, gs, g);
                 else if (ps.leaf)
@@ -346,7 +349,9 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
             }
             if (ps.nfast) {
                 a.wg_base = 0;
-                if (ps.leaf && ps.ni == 1)
+                if (ps.leaf && a.elem_len)
+                    hipLaunchKernelGGL((mk::k_reduce_elem<true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+                else if (ps.leaf && ps.ni == 1)
                     hipLaunchKernelGGL((mk::k_reduce<true, true, 1>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
                 else if (ps.leaf)
                     hipLaunchKernelGGL((mk::k_reduce<true, true, 2>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
@@ -456,6 +461,93 @@ int dev_finish_nodes(const void* d_nodes, uint64_t count, uint64_t n_total, void
     Plan p;
     TRY(mk::make_plan(count, 32, false, 0, false, ((uintptr_t)d_nodes % 16) == 0, p, true, 0, n_total));
     return launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st);
+}
+
+// ---- TreeHash of a list of byte strings (makeSliceHasher + hashedEncoding) ---------------
+// The tree's items are the n element digests K(le32(elem_len) || element)
+// (hash.go:100-107, 118-139).  Fused (k_reduce_elem, no digest array) when
+// the elements are 32 B, 16-B aligned and the leaf pass is a throughput
+// pass; otherwise the digests go to the workspace first (k_elem_digests) and
+// the ordinary plan runs over them.
+struct ElemPlan {
+    Plan p;
+    bool fused = false;
+    uint64_t dig_bytes = 0;  // two-phase: digest array at the start of the workspace
+    uint64_t ws_bytes = 0;
+};
+
+int make_elem_plan(uint64_t n, uint32_t elem_len, bool aligned16, ElemPlan& e) {
+    e = ElemPlan();
+    if (n > (UINT64_MAX / 4) / 32) return fail(MK_EINVAL, "n too large");
+    const bool fast32 = elem_len == 32 && aligned16;
+    TRY(mk::make_plan(n, 32, false, 0, false, fast32, e.p, false, 0, 0, /*leaf_ni1=*/fast32));
+    e.fused = fast32 && !e.p.small && !e.p.passes.empty() && !e.p.passes[0].wave && !e.p.passes[0].sp;
+    if (!e.fused && fast32) TRY(mk::make_plan(n, 32, false, 0, false, true, e.p));  // the ordinary plan over digests
+    if (e.fused) {
+        Pass& ps = e.p.passes[0];
+        ps.a.elem_len = 32;
+        ps.perms += (double)n;  // one permutation per 36-B element message
+        ps.hashes += (double)n;
+        e.ws_bytes = mk::plan_ws_bytes(e.p);
+    } else {
+        e.dig_bytes = (32 * n + 255) & ~255ull;
+        e.ws_bytes = e.dig_bytes + (e.p.small ? 256 : mk::plan_ws_bytes(e.p));
+    }
+    return MK_OK;
+}
+
+int dev_tree_hash_elems(const void* d_elems, uint64_t n, uint32_t elem_len, void* d_out32, void* d_ws,
+                        uint64_t ws_bytes, hipStream_t st) {
+    if (!d_out32 || (n && elem_len && !d_elems)) return fail(MK_EINVAL, "null pointer");
+    ElemPlan e;
+    TRY(make_elem_plan(n, elem_len, ((uintptr_t)d_elems % 16) == 0, e));
+    if (ws_bytes < e.ws_bytes)
+        return fail(MK_ENOMEM, "workspace too small: %llu < %llu", (unsigned long long)ws_bytes,
+                    (unsigned long long)e.ws_bytes);
+    if (n && !d_ws) return fail(MK_EINVAL, "null workspace");
+    if (e.fused) return launch_plan(e.p, (const uint8_t*)d_elems, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st);
+    uint8_t* dig = (uint8_t*)d_ws;
+    if (n) {
+        const uint32_t fast32 = (elem_len == 32 && ((uintptr_t)d_elems % 16) == 0) ? 1u : 0u;
+        ProfRec rec{};
+        const bool prof = prof_on();
+        if (prof) {
+            HIPCHK(hipEventCreate(&rec.a));
+            HIPCHK(hipEventCreate(&rec.b));
+            HIPCHK(hipEventRecord(rec.a, st));
+        }
+        hipLaunchKernelGGL(mk::k_elem_digests, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_elems, n,
+                           elem_len, fast32, (uint4*)dig);
+        HIPCHK(hipGetLastError());
+        if (prof) {
+            HIPCHK(hipEventRecord(rec.b, st));
+            rec.perms = (double)n * (double)mk::perms_for_len((uint64_t)elem_len + 4);
+            rec.hashes = (double)n;
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            g_prof.push_back(rec);
+        }
+    }
+    return launch_plan(e.p, dig, (uint8_t*)d_out32, dig + e.dig_bytes, ws_bytes - e.dig_bytes, st);
+}
+
+int host_tree_hash_elems(const uint8_t* elems, uint64_t n, uint32_t elem_len, uint8_t* out) {
+    if (!out || (n && elem_len && !elems)) return fail(MK_EINVAL, "null pointer");
+    if (elem_len && n > (UINT64_MAX / 4) / elem_len) return fail(MK_EINVAL, "n * elem_len overflows");
+    TRY(bind_call());
+    DevCtx* c = ctx();
+    std::lock_guard<std::mutex> lk(c->mu);
+    ElemPlan e;
+    TRY(make_elem_plan(n, elem_len, true, e));
+    const size_t inb = n * (size_t)elem_len;
+    TRY(grow(c->in, inb));
+    TRY(grow(c->out, 32));
+    TRY(grow(c->ws, e.ws_bytes));
+    hipStream_t st = c->stream;
+    if (inb) HIPCHK(hipMemcpyAsync(c->in.p, elems, inb, hipMemcpyHostToDevice, st));
+    TRY(dev_tree_hash_elems(c->in.p, n, elem_len, c->out.p, c->ws.p, c->ws.cap, st));
+    HIPCHK(hipMemcpyAsync(out, c->out.p, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return MK_OK;
 }
 
 int host_merkle_hash_plain(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t* out) {
@@ -1318,6 +1410,24 @@ int mk_dev_ssz_merkle_hash(mk_call* call, const void* d_items, uint64_t n, uint3
 int mk_ssz_merkle_hash(mk_call* call, const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t out[32]) {
     Scope S(call);
     return S.done(host_merkle_hash(items, n, item_len, out));
+}
+
+uint64_t mk_ssz_tree_hash_bytes_list_workspace_bytes(uint64_t n, uint32_t elem_len) {
+    ElemPlan e;
+    if (make_elem_plan(n, elem_len, true, e) != MK_OK) return 0;
+    return e.ws_bytes;
+}
+
+int mk_dev_ssz_tree_hash_bytes_list(mk_call* call, const void* d_elems, uint64_t n, uint32_t elem_len,
+                                    void* d_out32, void* d_ws, uint64_t ws_bytes, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    return S.done(rc ? rc : dev_tree_hash_elems(d_elems, n, elem_len, d_out32, d_ws, ws_bytes, (hipStream_t)stream));
+}
+
+int mk_ssz_tree_hash_bytes_list(mk_call* call, const uint8_t* elems, uint64_t n, uint32_t elem_len, uint8_t out[32]) {
+    Scope S(call);
+    return S.done(host_tree_hash_elems(elems, n, elem_len, out));
 }
 
 uint64_t mk_ssz_merkle_many_workspace_bytes(const uint64_t* n, const uint32_t* item_len, uint32_t nlists) {

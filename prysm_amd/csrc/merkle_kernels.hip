@@ -359,6 +359,65 @@ __device__ __forceinline__ void first_level_generic(const ReduceArgs& a, uint64_
     }
 }
 
+// Phase B of a fused pass (k_reduce, k_reduce_elem) after the workgroup's
+// first two levels sit in LDS (m2 level-2 nodes, lds[2k], lds[2k+1]): the
+// remaining levels in LDS, one node per thread per level (read -> barrier ->
+// permute -> write -> barrier), then the workgroup's nodes (or, in the final
+// pass, the root with the length mix-in) to HBM.
+template <int NI>
+__device__ __forceinline__ void reduce_levels_out(const ReduceArgs& a, uint4* lds, uint32_t tid, uint64_t wg,
+                                                  uint64_t c2, uint64_t m2, bool pair) {
+    constexpr uint64_t kSpan1 = 2 * NI * kReduceThreads;
+    constexpr uint64_t kSpan2 = kSpan1 / 2;
+    uint64_t c = c2, m = m2;
+    int left = a.finalize ? 64 : (int)a.levels - (pair ? 2 : 1);
+    int done = 0;
+    while (left > 0 && (c > 1 || a.pad_at_one)) {
+        const uint64_t mn = (m + 1) / 2;
+        const bool act = tid < mn;
+        uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0;
+        bool padded = false;
+        if (act) {
+            l0 = lds[4 * tid];
+            l1 = lds[4 * tid + 1];
+            padded = !(2 * (uint64_t)tid + 1 < m);
+            if (!padded) {
+                r0 = lds[4 * tid + 2];
+                r1 = lds[4 * tid + 3];
+            }
+        }
+        __syncthreads();
+        if (act) {
+            uint4 d0, d1;
+            hash_pair(l0, l1, r0, r1, padded, d0, d1);
+            lds[2 * tid] = d0;
+            lds[2 * tid + 1] = d1;
+        }
+        __syncthreads();
+        c = (c + 1) / 2;
+        m = mn;
+        --left;
+        ++done;
+    }
+
+    // ---- output ------------------------------------------------------------
+    uint4* out = reinterpret_cast<uint4*>(a.out);
+    if (a.finalize) {
+        if (tid == 0) {
+            uint4 d0, d1;
+            hash_final(lds[0], lds[1], a.n_items, d0, d1);
+            out[0] = d0;
+            out[1] = d1;
+        }
+    } else {
+        const uint64_t lo_out = ((pair ? wg * kSpan2 : wg * kSpan1)) >> done;
+        for (uint32_t k = tid; k < m; k += kReduceThreads) {
+            out[2 * (lo_out + k)] = lds[2 * k];
+            out[2 * (lo_out + k) + 1] = lds[2 * k + 1];
+        }
+    }
+}
+
 // One fused reduce pass.  256 threads; the workgroup owns first-level nodes
 // [S*wg, S*wg+S) with S = 512*NI (NI = 2 for wide passes; NI = 1 halves the
 // serial work per thread so mid-size trees still spread over all CUs),
@@ -481,54 +540,7 @@ __global__ __launch_bounds__(kReduceThreads, (MK_LEAF_SPLIT && LEAF && FAST) ? M
     }
     __syncthreads();
 
-    // ---- phase B: levels in LDS -------------------------------------------
-    uint64_t c = c2, m = m2;
-    int left = a.finalize ? 64 : (int)a.levels - (pair ? 2 : 1);
-    int done = 0;
-    while (left > 0 && (c > 1 || a.pad_at_one)) {
-        const uint64_t mn = (m + 1) / 2;
-        const bool act = tid < mn;
-        uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0;
-        bool padded = false;
-        if (act) {
-            l0 = lds[4 * tid];
-            l1 = lds[4 * tid + 1];
-            padded = !(2 * (uint64_t)tid + 1 < m);
-            if (!padded) {
-                r0 = lds[4 * tid + 2];
-                r1 = lds[4 * tid + 3];
-            }
-        }
-        __syncthreads();
-        if (act) {
-            uint4 d0, d1;
-            hash_pair(l0, l1, r0, r1, padded, d0, d1);
-            lds[2 * tid] = d0;
-            lds[2 * tid + 1] = d1;
-        }
-        __syncthreads();
-        c = (c + 1) / 2;
-        m = mn;
-        --left;
-        ++done;
-    }
-
-    // ---- output ------------------------------------------------------------
-    uint4* out = reinterpret_cast<uint4*>(a.out);
-    if (a.finalize) {
-        if (tid == 0) {
-            uint4 d0, d1;
-            hash_final(lds[0], lds[1], a.n_items, d0, d1);
-            out[0] = d0;
-            out[1] = d1;
-        }
-    } else {
-        const uint64_t lo_out = ((pair ? wg * kSpan2 : wg * kSpan1)) >> done;
-        for (uint32_t k = tid; k < m; k += kReduceThreads) {
-            out[2 * (lo_out + k)] = lds[2 * k];
-            out[2 * (lo_out + k) + 1] = lds[2 * k + 1];
-        }
-    }
+    reduce_levels_out<NI>(a, lds, tid, wg, c2, m2, pair);
 }
 
 template __global__ void k_reduce<true, true, 2>(ReduceArgs);
@@ -537,6 +549,243 @@ template __global__ void k_reduce<false, true, 2>(ReduceArgs);
 template __global__ void k_reduce<false, false, 2>(ReduceArgs);
 template __global__ void k_reduce<true, true, 1>(ReduceArgs);
 template __global__ void k_reduce<true, false, 1>(ReduceArgs);
+
+// ----------------------------------------------------------------------------
+// ssz.TreeHash of a list of byte strings in one pass (makeSliceHasher over
+// []byte / [N]byte elements, hash.go:118-139 with hashedEncoding,
+// hash.go:100-107): the tree's items are the element digests
+// K(le32(elem_len) || element), 32 B each, 4 per chunk, so a level-1 window is
+// the 8 digests of 8 consecutive elements.  k_reduce_elem computes those
+// digests in registers and goes straight on into the window, the pair level
+// and the LDS levels -- no n x 32-B digest array in HBM.
+
+// K(le32(32) || e), e = 32 B at a 16-B aligned address: one block.
+__device__ __forceinline__ void elem32_digest(const uint4* __restrict__ e, uint32_t (&d)[8]) {
+    asm volatile("" ::: "memory");  // the loads stay here (not hoisted over earlier permutations)
+    const uint4 v0 = ld_stream(e), v1 = ld_stream(e + 1);
+    State s;
+    s.lo[0] = 32u;  // le32(len)
+    s.hi[0] = v0.x;
+    s.lo[1] = v0.y;
+    s.hi[1] = v0.z;
+    s.lo[2] = v0.w;
+    s.hi[2] = v1.x;
+    s.lo[3] = v1.y;
+    s.hi[3] = v1.z;
+    s.lo[4] = v1.w;
+    s.hi[4] = 1u;  // domain pad at byte 36
+#pragma unroll
+    for (int k = 5; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+    s.hi[16] = 0x80000000u;
+    keccak_f_digest(s);
+    d[0] = s.lo[0];
+    d[1] = s.hi[0];
+    d[2] = s.lo[1];
+    d[3] = s.hi[1];
+    d[4] = s.lo[2];
+    d[5] = s.hi[2];
+    d[6] = s.lo[3];
+    d[7] = s.hi[3];
+}
+
+__device__ __noinline__ void sponge_prefix4(const uint8_t* __restrict__ A, uint32_t L, uint4& d0, uint4& d1);
+
+// K(le32(L) || p[0, L)) for any length and alignment (byte loads).
+__device__ __noinline__ void elem_digest_any(const uint8_t* __restrict__ p, uint32_t L, uint32_t (&d)[8]) {
+    uint4 d0, d1;
+    if ((((uintptr_t)p) & 3u) == 0) {
+        sponge_prefix4(p, L, d0, d1);
+    } else {
+        const uint64_t len = (uint64_t)L + 4;
+        const uint64_t nb = len / 136 + 1;
+        State s;
+        zero(s);
+        for (uint64_t b = 0; b < nb; ++b) {
+#pragma unroll 1
+            for (int w = 0; w < 17; ++w) {
+                uint32_t h[2] = {0u, 0u};
+#pragma unroll 1
+                for (int k = 0; k < 8; ++k) {
+                    const uint64_t m = b * 136 + 8u * w + k;
+                    uint32_t byte = 0;
+                    if (m < 4)
+                        byte = (L >> (8 * m)) & 0xFFu;
+                    else if (m < len)
+                        byte = p[m - 4];
+                    else if (m == len)
+                        byte = 1u;  // domain pad
+                    h[k >> 2] |= byte << (8 * (k & 3));
+                }
+                if (b == nb - 1 && w == 16) h[1] ^= 0x80000000u;
+                s.lo[w] ^= h[0];
+                s.hi[w] ^= h[1];
+            }
+            keccak_f(s);
+        }
+        digest(s, d0, d1);
+    }
+    d[0] = d0.x, d[1] = d0.y, d[2] = d0.z, d[3] = d0.w;
+    d[4] = d1.x, d[5] = d1.y, d[6] = d1.z, d[7] = d1.w;
+}
+
+// Full window of 8 elements of 32 B (256 contiguous bytes, 16-B aligned).
+// Two Keccak states cannot be live at once within 128 VGPRs (a permutation
+// alone takes ~80), so digests 4..7 -- the last 8 bytes of block 1 and all of
+// block 2 of the window message -- are parked in this thread's LDS column
+// (stg[k * kReduceThreads], dword-major across the workgroup: conflict-free),
+// digests 0..3 stay in registers as block 1, and the window absorbs block 2
+// from LDS after its first permutation.
+__device__ __forceinline__ void elem_window32(const uint4* __restrict__ w, uint32_t* stg, uint4& o0, uint4& o1) {
+#pragma unroll
+    for (int e = 4; e < 8; ++e) {
+        uint32_t d[8];
+        elem32_digest(w + 2 * e, d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) stg[(8 * (e - 4) + k) * kReduceThreads] = d[k];
+    }
+    uint32_t m[32];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        uint32_t d[8];
+        elem32_digest(w + 2 * e, d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) m[8 * e + k] = d[k];
+    }
+    State s;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        s.lo[k] = m[2 * k];
+        s.hi[k] = m[2 * k + 1];
+    }
+    s.lo[16] = stg[0];
+    s.hi[16] = stg[kReduceThreads];
+#pragma unroll
+    for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+    keccak_f(s);
+#pragma unroll
+    for (int q = 0; q < 30; ++q) {  // block 2 = staged dwords 2..31
+        const uint32_t v = stg[(2 + q) * kReduceThreads];
+        if (q & 1)
+            s.hi[q >> 1] ^= v;
+        else
+            s.lo[q >> 1] ^= v;
+    }
+    s.lo[15] ^= 1u;  // byte 256 = byte 120 of block 2
+    s.hi[16] ^= 0x80000000u;
+    keccak_f_digest(s);
+    digest(s, o0, o1);
+}
+
+// Window j of the digest tree in general form: digests [8j, min(8j+8, n)),
+// odd chunk count -> the 128-B zero chunk appended (hash.go:225-228).
+__device__ __noinline__ void elem_window_generic(const ReduceArgs& a, uint64_t j, uint4& o0, uint4& o1) {
+    const uint64_t n = a.n_items;
+    const uint32_t cnt = (uint32_t)((n - 8 * j) < 8 ? (n - 8 * j) : 8);
+    const bool padded = !(2 * j + 1 < a.nchunks);
+    const uint32_t L = a.elem_len;
+    uint32_t m[64];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if ((uint32_t)e < cnt) elem_digest_any(a.items + (8 * j + e) * (uint64_t)L, L, d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) m[8 * e + k] = d[k];
+    }
+    const uint32_t lm = 32 * cnt + (padded ? 128u : 0u);  // message bytes (<= 256, a multiple of 4)
+    const uint32_t nb = lm / 136 + 1;
+    State s;
+    zero(s);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        if ((uint32_t)b >= nb) break;
+#pragma unroll
+        for (int w = 0; w < 34; ++w) {
+            const int q = 34 * b + w;
+            uint32_t v = q < 64 ? m[q] : 0u;
+            if ((uint32_t)q * 4 == lm) v ^= 1u;
+            if ((uint32_t)b == nb - 1 && w == 33) v ^= 0x80000000u;
+            if (w & 1)
+                s.hi[w >> 1] ^= v;
+            else
+                s.lo[w >> 1] ^= v;
+        }
+        if ((uint32_t)b + 1 < nb)
+            keccak_f(s);
+        else
+            keccak_f_digest(s);
+    }
+    digest(s, o0, o1);
+}
+
+#ifndef MK_ELEM_WAVES
+#define MK_ELEM_WAVES 4
+#endif
+// The leaf pass of the element-digest tree (a.n_items elements, a.nchunks =
+// ceil(n / 4) chunks, a.c1 windows), one window pair per thread (NI = 1:
+// 512 windows = 4096 elements per workgroup; LDS 8 KB of levels + 32 KB of
+// staged digests, so 4 workgroups of 4 waves fill a CU's 160 KB at 4
+// waves/SIMD).  FAST: every window of the workgroup has 8 elements of 32 B,
+// 16-B aligned (host-checked).  Otherwise the general window (any elem_len
+// and alignment, ragged last window, odd pad).
+template <bool FAST>
+__global__ __launch_bounds__(kReduceThreads, FAST ? MK_ELEM_WAVES : 1) void k_reduce_elem(ReduceArgs a) {
+    constexpr int NI = 1;
+    constexpr uint64_t kSpan1 = 2 * NI * kReduceThreads;
+    constexpr uint64_t kSpan2 = kSpan1 / 2;
+    __shared__ uint4 lds[2 * kSpan2];
+    __shared__ uint32_t stg[FAST ? 32 * kReduceThreads : 1];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t wg = a.wg_base + blockIdx.x;
+    const uint64_t lo1 = wg * kSpan1;
+    const uint64_t c1 = a.c1;
+    const uint64_t m1 = (c1 - lo1) < kSpan1 ? (c1 - lo1) : kSpan1;
+    const bool pair = a.levels >= 2 && c1 > 1;  // the host plans k_reduce_elem for trees of > 2^17 windows
+    const uint64_t c2 = pair ? (c1 + 1) / 2 : c1;
+    const uint64_t m2 = pair ? (m1 + 1) / 2 : m1;
+    const uint32_t q = tid;
+    if (FAST || q < m2) {
+        const uint64_t j0 = lo1 + 2 * (uint64_t)q;
+        uint4 l0, l1, r0 = make_uint4(0, 0, 0, 0), r1 = r0, d0, d1;
+        bool padded = false;
+        if constexpr (FAST) {
+            const uint4* w = reinterpret_cast<const uint4*>(a.items) + j0 * 16;
+            elem_window32(w, stg + tid, d0, d1);
+            lds[2 * q] = d0;  // the left digest waits in this thread's own level slot
+            lds[2 * q + 1] = d1;
+            elem_window32(w + 16, stg + tid, r0, r1);
+            l0 = lds[2 * q];
+            l1 = lds[2 * q + 1];
+        } else {
+            elem_window_generic(a, j0, l0, l1);
+            padded = !(2 * (uint64_t)q + 1 < m1);
+            if (!padded) elem_window_generic(a, j0 + 1, r0, r1);
+        }
+        hash_pair(l0, l1, r0, r1, padded, d0, d1);
+        lds[2 * q] = d0;
+        lds[2 * q + 1] = d1;
+    }
+    __syncthreads();
+    reduce_levels_out<NI>(a, lds, tid, wg, c2, m2, pair);
+}
+
+template __global__ void k_reduce_elem<true>(ReduceArgs);
+template __global__ void k_reduce_elem<false>(ReduceArgs);
+
+// Element digests K(le32(elem_len) || element i) -> out[i] (32 B): the first
+// half of the two-phase form, for trees too small for k_reduce_elem's
+// throughput pass and for element lengths other than 32.
+__global__ __launch_bounds__(256) void k_elem_digests(const uint8_t* __restrict__ elems, uint64_t n, uint32_t elem_len,
+                                                      uint32_t fast32, uint4* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t d[8];
+    if (fast32)
+        elem32_digest(reinterpret_cast<const uint4*>(elems) + 2 * i, d);
+    else
+        elem_digest_any(elems + i * (uint64_t)elem_len, elem_len, d);
+    out[2 * i] = make_uint4(d[0], d[1], d[2], d[3]);
+    out[2 * i + 1] = make_uint4(d[4], d[5], d[6], d[7]);
+}
 
 // ----------------------------------------------------------------------------
 // Latency pass with two lanes per state (keccak_dev.hpp, mk::pair): lane pair

@@ -110,7 +110,7 @@ uint32_t levels_to_one(uint64_t count) {
 
 // ---- merkleHash pass plan ---------------------------------------------------------
 int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool pad_at_one, bool aligned16, Plan& p,
-              bool node_input, uint32_t frontier, uint64_t mixin_n) {
+              bool node_input, uint32_t frontier, uint64_t mixin_n, bool leaf_ni1) {
     p = Plan();
     p.n = n;
     if (n > 0 && item_len == 0) return fail(MK_EINVAL, "item_len == 0 (reference: integer divide by zero)");
@@ -186,7 +186,7 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         }
         // throughput pass: 2 window pairs per thread on wide passes, 1 on mid-size
         // leaf passes so they still spread over the CUs
-        const uint32_t ni = (!wave && leaf && c1 < kReduceNi2MinC1) ? 1 : 2;
+        const uint32_t ni = (!wave && leaf && (c1 < kReduceNi2MinC1 || leaf_ni1)) ? 1 : 2;
         if (sp) nt = 1024;
         const uint64_t span = sp ? kSpreadSpan
                             : w3 ? nt / 2 : wave ? kWave2Span : (uint64_t)2 * ni * kReduceThreads;

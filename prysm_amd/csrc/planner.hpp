@@ -62,9 +62,10 @@ struct Plan {
 // rule alive at count 1).  node_input: n 32-B nodes reduced pairwise
 // (MerkleRoot heap bands, a gathered frontier level); without subtree mode the
 // final pass mixes in `mixin_n`.  frontier (subtree mode): stop `frontier`
-// levels below the subtree root and write that level.
+// levels below the subtree root and write that level.  leaf_ni1: the leaf
+// pass's throughput workgroups take one window pair per thread (k_reduce_elem).
 int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool pad_at_one, bool aligned16, Plan& p,
-              bool node_input = false, uint32_t frontier = 0, uint64_t mixin_n = 0);
+              bool node_input = false, uint32_t frontier = 0, uint64_t mixin_n = 0, bool leaf_ni1 = false);
 uint64_t plan_ws_bytes(const Plan& p);
 
 int shard_plan(uint64_t n, uint32_t item_len, uint32_t nshards, uint32_t* height, uint32_t* nonempty,

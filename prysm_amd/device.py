@@ -103,6 +103,26 @@ def merkle_hash(items: torch.Tensor, n: int, item_len: int, out: torch.Tensor = 
     return out
 
 
+def tree_hash_bytes_list_workspace(n: int, elem_len: int, device) -> torch.Tensor:
+    nb = _lib.load().mk_ssz_tree_hash_bytes_list_workspace_bytes(n, elem_len)
+    return torch.empty(max(nb, 256), dtype=torch.uint8, device=device)
+
+
+def tree_hash_bytes_list(elems: torch.Tensor, n: int, elem_len: int, out: torch.Tensor = None,
+                         ws: torch.Tensor = None) -> torch.Tensor:
+    """ssz.TreeHash of a list of n byte strings of elem_len bytes each
+    (makeSliceHasher + hashedEncoding, shared/ssz/hash.go:100-107, 118-139):
+    merkleHash over K(le32(elem_len) || element_i), in one call with the
+    element digests fused into the leaf pass (32-B elements)."""
+    if out is None:
+        out = torch.empty(32, dtype=torch.uint8, device=elems.device)
+    if ws is None:
+        ws = tree_hash_bytes_list_workspace(n, elem_len, elems.device)
+    _lib.invoke("mk_dev_ssz_tree_hash_bytes_list", _p(elems), n, elem_len, _p(out), _p(ws), ws.numel(),
+                _stream(elems.device), device=_dev(elems))
+    return out
+
+
 def merkle_many(items: torch.Tensor, offs, ns, item_lens, out: torch.Tensor = None,
                 ws: torch.Tensor = None) -> torch.Tensor:
     """merkleHash of many lists in one call (list i = ns[i] items of

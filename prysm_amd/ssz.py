@@ -252,6 +252,13 @@ def _hash_many(t: SSZType, vals: Sequence, memo: dict) -> np.ndarray:
             return np.frombuffer(b"".join(hash_batch_var([b""] * n)), dtype=np.uint8).reshape(n, 32)
         return hash_batch(np.ascontiguousarray(np.concatenate(cols, axis=1)), sum(c.shape[1] for c in cols))
     if isinstance(t, (Slice, Array)):
+        # one list of equal-length byte strings: element digests and the tree
+        # in one library call (mk_ssz_tree_hash_bytes_list)
+        if n == 1 and isinstance(t.elem, (Bytes, ByteArray)) and len(vals[0]):
+            bs = [bytes(e) for e in vals[0]]
+            if all(len(b) == len(bs[0]) for b in bs):
+                flat = np.frombuffer(b"".join(bs), dtype=np.uint8) if len(bs[0]) else np.zeros(0, np.uint8)
+                return np.frombuffer(tree_hash_bytes_list(flat, len(bs), len(bs[0])), dtype=np.uint8).reshape(1, 32)
         # every list of this nesting level in one library call (mk_ssz_merkle_many)
         if isinstance(t.elem, (Bool, Uint)):
             encs = [_scalar_bytes(t.elem, v) for v in vals]
@@ -277,6 +284,19 @@ def merkle_hash_flat(items: np.ndarray, n: int, item_len: int) -> bytes:
         raise ZeroDivisionError("integer divide by zero")  # hash.go:207 panics
     out = ctypes.create_string_buffer(32)
     _lib.invoke("mk_ssz_merkle_hash", _ptr(a) if a.size else None, n, item_len, out)
+    return out.raw
+
+
+def tree_hash_bytes_list(elems: np.ndarray, n: int, elem_len: int) -> bytes:
+    """ssz.TreeHash of a slice of n byte strings of elem_len bytes each,
+    contiguous in ``elems`` (makeSliceHasher + hashedEncoding, hash.go:100-107,
+    118-139): merkleHash over Keccak(le32(elem_len) || element), one GPU call
+    (mk_ssz_tree_hash_bytes_list)."""
+    a = np.ascontiguousarray(elems, dtype=np.uint8).reshape(-1)
+    if a.size < n * elem_len:
+        raise ValueError("elements buffer shorter than n*elem_len")
+    out = ctypes.create_string_buffer(32)
+    _lib.invoke("mk_ssz_tree_hash_bytes_list", _ptr(a) if a.size else None, n, elem_len, out)
     return out.raw
 
 

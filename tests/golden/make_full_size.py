@@ -10,12 +10,14 @@ restatement_vectors.json; the oracle is pinned by reference_vectors.json).
       concatenated 2^24 digests (a checksum of checksums)
   c3: TreeHash of State{1,000,000 synthetic validators, balances}
   c4: merkleHash of 2^28 x 32-B SplitMix64 items (the headline tree)
+  c4tree: TreeHash([][32]byte) of 2^28 SplitMix64 elements (the C4 secondary:
+      every element hashed as Keccak(le32(32) || element), then merkleHash)
   c5: depth-32 deposit trie root of 2^20 x 280-B SplitMix64 deposits
   c3_state: TreeHash of the synthetic pb.BeaconState of prysm_amd/state.py
       with 1,000,000 validators (oracle/ssz_ref.py's reflective restatement,
       the registry root from the C oracle's struct roots + merkleHash)
 
-Run:  python tests/golden/make_full_size.py [c1,c2,c3,c3_state,c4,c5]
+Run:  python tests/golden/make_full_size.py [c1,c2,c3,c3_state,c4,c4tree,c5]
 (C oracle, all host cores; about a minute on 8 cores; named configs are
 recomputed and merged into the existing file).
 """
@@ -125,6 +127,21 @@ def main(only=None):
         n = 1 << 28
         out["c4"] = {"n": n, "item_len": 32, "seed": SEED + 4,
                      "root": O.merkle_hash_gen(n, 32, SEED + 4, nthreads=nt).hex()}
+
+    if want("c4tree"):
+        # SURVEY 8(d)'s C4 secondary: TreeHash([][32]byte) of 2^28 elements =
+        # merkleHash over Keccak(le32(32) || element_i) (hash.go:100-107,118-139);
+        # elements generated chunk by chunk from the SplitMix64 stream
+        n, L, seed = 1 << 28, 32, SEED + 0x40
+        dig = np.empty((n, 32), dtype=np.uint8)
+        step = 1 << 24
+        for lo in range(0, n, step):
+            chunk = O.splitmix_bytes(step * L, seed, word0=lo * L // 8)
+            dig[lo:lo + step] = O.elem_digests(chunk, step, L, nthreads=nt)
+        out["c4tree"] = {"n": n, "elem_len": L, "seed": seed,
+                         "root": O.merkle_hash_flat(dig.reshape(-1), n, 32, nthreads=nt).hex(),
+                         "what": "ssz.TreeHash([][32]byte): merkleHash over Keccak(le32(32) || element)"}
+        del dig
 
     if want("c5"):
         n, dl = 1 << 20, 280

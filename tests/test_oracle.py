@@ -168,3 +168,25 @@ def test_generator_and_subtree_oracles_agree():
         chunks = [O.keccak256(chunks[i] + chunks[i + 1]) for i in range(0, len(chunks), 2)]
     final = O.keccak256(chunks[0] + struct.pack("<Q", n) + bytes(24))
     assert final == O.merkle_hash_gen(n, item_len, seed)
+
+
+def test_tree_hash_bytes_list_oracle_routes():
+    """The composed oracle for TreeHash of a byte-string list (hashedEncoding
+    digests + merkleHash) equals the reflective restatement, and chunked
+    digest generation (make_full_size.py c4tree) equals one pass."""
+    import numpy as np
+
+    from oracle import oracle as O
+    from oracle import ssz_ref as OS
+
+    rng = np.random.default_rng(3)
+    for n, L in ((0, 32), (1, 32), (4, 32), (5, 32), (8, 32), (9, 32), (130, 32), (17, 48), (40, 0), (6, 140)):
+        vals = [bytes(rng.integers(0, 256, L, dtype=np.uint8)) for _ in range(n)]
+        flat = np.frombuffer(b"".join(vals), dtype=np.uint8) if n * L else np.zeros(0, np.uint8)
+        assert O.tree_hash_bytes_list(flat, n, L) == OS.tree_hash(("slice", ("bytes",)), vals), (n, L)
+    items = O.splitmix_bytes(5000 * 32, 11)
+    one = O.elem_digests(items, 5000, 32)
+    parts = np.concatenate([O.elem_digests(O.splitmix_bytes(1000 * 32, 11, word0=lo * 4), 1000, 32)
+                            for lo in range(0, 5000, 1000)])
+    assert np.array_equal(one, parts)
+    assert np.array_equal(O.elem_digests(items, 5000, 32, chunk=777), one)
