@@ -216,8 +216,9 @@ def main():
                          "overlapping the next step's leaf pass: N=1 the node passes and the length mix-in "
                          "(prysm_amd/pipeline.py), N>1 each rank's node passes, the all-gather and rank 0's "
                          "finisher (parallel.ShardedMerklePipeline).  0 = one stream")
-    ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c5"],
-                    help="BASELINE.json config: c4 = headline (default); c1/c2/c3/c5 = single-GPU side benches")
+    ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c4tree", "c5"],
+                    help="BASELINE.json config: c4 = headline (default); c1/c2/c3/c5 = single-GPU side benches; "
+                         "c4tree = the C4 secondary, TreeHash([][32]byte) of 2^28 elements")
     ap.add_argument("--single-process", action="store_true",
                     help="N devices from one process through mk_dev_ssz_merkle_hash_multi (the cgo caller's "
                          "form: one shard per device, RCCL all-gather inside the library)")

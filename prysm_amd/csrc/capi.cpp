@@ -273,8 +273,22 @@ void launch_wave3(uint32_t nt, uint64_t nwg, const ReduceArgs& a, hipStream_t st
     }
 }
 
+// Test hook (MK_INJECT_EHIP=1 in the environment when the library is
+// loaded): every merkle plan launch and Hash batch fails the way a failed HIP
+// launch does (MK_EHIP with its detail in the call's context), so a binding
+// can prove a GPU failure reaches its caller as an error and is never
+// answered by a CPU fallback (tests/c_abi/harness.c `inject`).
+bool inject_ehip() {
+    static const bool on = [] {
+        const char* e = std::getenv("MK_INJECT_EHIP");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t* d_ws, uint64_t ws_bytes,
                 hipStream_t st) {
+    if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
     if (p.small) {
         hipLaunchKernelGGL(mk::k_final_small, dim3(1), dim3(64), 0, st, d_items, p.total, p.n, d_out32);
         HIPCHK(hipGetLastError());
@@ -375,6 +389,7 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
 // ---- hashing ----------------------------------------------------------------------
 int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, hipStream_t st) {
     if (n == 0) return MK_OK;
+    if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
     if (!d_out || (!d_in && msg_len)) return fail(MK_EINVAL, "null pointer");
     const uint64_t grid = ceil_div(n, 256);
     if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0)

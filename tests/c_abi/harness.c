@@ -8,6 +8,11 @@
  * failures come back through the failing call's own mk_call context.
  *
  *   harness <threads> <rounds> <merkle_hex x8> <batch_hex x8> <trie_root_hex> <branch_hex> <many_hex x3>
+ *   MK_INJECT_EHIP=1 harness inject
+ *
+ * `inject` runs with the library's failure-injection hook on: every compute
+ * call must come back with MK_EHIP and the detail in its own mk_call (the
+ * cgo package maps it to an error; only MK_ENODEV may select a CPU path).
  *
  * Inputs are SplitMix64 streams, identical to oracle/merkle_ref.c.
  */
@@ -189,7 +194,35 @@ static void* worker(void* p) {
     return NULL;
 }
 
+/* With MK_INJECT_EHIP=1: a failed HIP launch inside the library surfaces as
+ * MK_EHIP with its detail in the failing call's context, for every family. */
+static int inject_check(void) {
+    mk_call call;
+    uint8_t out[32];
+    uint8_t* items = calloc(100003, 32);
+    int bad = 0;
+    struct {
+        const char* name;
+        int rc;
+    } r[3];
+    call.device = -1;
+    r[0].name = "mk_ssz_merkle_hash";
+    r[0].rc = mk_ssz_merkle_hash(&call, items, 100003, 32, out);
+    bad |= r[0].rc != MK_EHIP || call.code != MK_EHIP || !strstr(call.err, "injected");
+    r[1].name = "mk_hash_batch";
+    r[1].rc = mk_hash_batch(&call, items, 1000, 64, items + 64000);
+    bad |= r[1].rc != MK_EHIP || call.code != MK_EHIP || !strstr(call.err, "injected");
+    r[2].name = "mk_ssz_tree_hash_bytes_list";
+    r[2].rc = mk_ssz_tree_hash_bytes_list(&call, items, 100003, 32, out);
+    bad |= r[2].rc != MK_EHIP || call.code != MK_EHIP || !strstr(call.err, "injected");
+    free(items);
+    for (int i = 0; i < 3; ++i) printf("%s -> %d (%s)\n", r[i].name, r[i].rc, mk_strerror(r[i].rc));
+    printf(bad ? "FAIL: injected failure not surfaced\n" : "ok: injected failures surfaced as MK_EHIP\n");
+    return bad;
+}
+
 int main(int argc, char** argv) {
+    if (argc == 2 && strcmp(argv[1], "inject") == 0) return inject_check();
     if (argc != 3 + NT_MAX + NT_MAX + 2 + 3) {
         fprintf(stderr, "usage: %s threads rounds merkle x8 batch x8 trie_root branch many x3\n", argv[0]);
         return 2;

@@ -200,6 +200,18 @@ def test_c_abi_harness_8_threads(gpu):
     assert "ok: 8 threads x 2 rounds" in r.stdout
 
 
+def test_c_abi_injected_failure_surfaces(gpu):
+    """With the library's failure-injection hook (MK_INJECT_EHIP=1), every
+    compute family returns MK_EHIP with the detail in its own mk_call: the
+    cgo binding turns that into an error and never into
+    a CPU answer."""
+    exe = _build_harness()
+    r = subprocess.run([exe, "inject"], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, MK_INJECT_EHIP="1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok: injected failures surfaced as MK_EHIP" in r.stdout
+
+
 def _build_harness() -> str:
     out = os.path.join(ROOT, "tests", "c_abi", "harness")
     src = os.path.join(ROOT, "tests", "c_abi", "harness.c")

@@ -1,5 +1,5 @@
 """Single-GPU side benchmarks for the other BASELINE.json configs
-(bench.py --config c1|c2|c3|c5).  Same JSON shape as the headline line; inputs
+(bench.py --config c1|c2|c3|c4tree|c5).  Same JSON shape as the headline line; inputs
 resident in HBM before timing; hipEvent-free wall timing bracketed by
 torch.cuda.synchronize(); the dominant kernel is timed with the library's
 own hipEvents where the library exposes them (merkle passes).
@@ -9,6 +9,8 @@ own hipEvents where the library exposes them (merkle passes).
   c2: hashutil.Hash over 2^24 x 64-B messages (one Keccak-f each)
   c3: TreeHash of a synthetic 1,000,000-validator State{registry, balances}
       via the typed Hashable path (struct kernels + merkleHash)
+  c4tree: ssz.TreeHash([][32]byte) of 2^28 elements (SURVEY 8(d)'s C4
+      secondary: element digests fused into the leaf pass)
   c5: depth-32 deposit trie from 2^20 x 280-B synthetic deposits
 """
 import ctypes
@@ -220,6 +222,60 @@ def run_config(args):
         _line("TreeHash of a 1M-validator State (registry + balances)", n / sec, "validators/s", args, sec, perms, hashes,
               {"workload": "C3: synthetic State{[]*ValidatorRecord, []uint64}, 1,000,000 validators",
                "n": n, "root": got.hex()}, cpu)
+        return
+
+    if args.config == "c4tree":
+        # SURVEY 8(d)'s C4 secondary: ssz.TreeHash([][32]byte) of 2^28
+        # elements (8 GiB in HBM) = merkleHash over Keccak(le32(32) || e_i):
+        # +2^28 permutations on top of C4 (x3.67 the work), element digests
+        # fused into the leaf pass (k_reduce_elem); one call per step.
+        import json as _json
+
+        g = _json.load(open(os.path.join(ROOT, "tests", "golden", "full_size_roots.json")))["c4tree"]
+        n, el = g["n"], g["elem_len"]
+        items = torch.empty(n * el, dtype=torch.uint8, device=dev)
+        D.synth_fill(items, g["seed"])
+        out = torch.empty(32, dtype=torch.uint8, device=dev)
+        ws = D.tree_hash_bytes_list_workspace(n, el, dev)
+        D.tree_hash_bytes_list(items, n, el, out=out, ws=ws)
+        torch.cuda.synchronize()
+        root = bytes(out.cpu().numpy()).hex()
+        if root != g["root"]:
+            raise SystemExit(f"c4tree: root {root} != golden {g['root']}")
+        D.prof_enable(True)
+        D.prof_read()
+        sec = _timeit(lambda: D.tree_hash_bytes_list(items, n, el, out=out, ws=ws), args.steps, args.warmup)
+        D.prof_enable(False)
+        leaf_ms, launches, lperms, lhashes = D.prof_read()
+        # whole step: n element perms + the C4-shaped tree (2^25 windows x 2,
+        # 2^25 - 1 pair nodes, 1 mix-in); one final permutation per hash
+        perms = n + (n // 8) * 2 + (n // 8 - 1) + 1
+        hashes = n + n // 8 + (n // 8 - 1) + 1
+        nl = max(launches, 1)
+        leaf_s = leaf_ms / 1e3 / nl
+        leaf_ops = (lperms / nl) * OPS_PER_PERM - (lhashes / nl) * OPS_SAVED_PER_HASH
+        cpu = None
+        if not args.no_cpu_baseline:
+            from oracle import oracle as O
+
+            m = 1 << 23
+            host = O.splitmix_bytes(m * el, g["seed"])
+            t0 = time.perf_counter()
+            O.tree_hash_bytes_list(host, m, el, nthreads=1)
+            dt = time.perf_counter() - t0
+            cpu = {"value": m / dt, "unit": "leaves/s", "cores": 1, "kind": "port", "cpu_model": _cpu_model(),
+                   "sample": f"oracle elem digests + merkleHash, 2^23 x 32-B elements (same stream), 1 thread, "
+                             f"{dt:.1f} s"}
+        _line("tree-hash leaves/sec @2^28 chunks, TreeHash([][32]byte) (element digests + merkleHash)", n / sec,
+              "leaves/s", args, sec, perms, hashes,
+              {"workload": "C4 secondary: ssz.TreeHash of 2^28 x [32]byte elements (8 GiB), one device call, "
+                           "element digests fused into the leaf pass", "n": n, "elem_len": el, "root": root,
+               "root_matches_golden": True},
+              cpu, {"kernel": "k_reduce_elem<FAST> (8 element digests + window + pair level + 3 LDS levels)",
+                    "leaf_kernel_ms": leaf_s * 1e3, "leaf_kernel_achieved": leaf_ops / leaf_s / 1e12,
+                    "leaf_kernel_frac": leaf_ops / leaf_s / PEAK_INT_OPS,
+                    "leaf_perms_per_launch": lperms / nl, "leaf_hashes_per_launch": lhashes / nl,
+                    "perms_per_leaf": perms / n, "hbm_GBps_algorithmic": n * el / leaf_s / 1e9})
         return
 
     if args.config == "c5":
