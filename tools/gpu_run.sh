@@ -1,0 +1,61 @@
+#!/bin/bash
+# The one parameterised GPU-box runner (it replaces round 2's one-off
+# tools/r02*.sh scripts, which git history keeps).  Every step has its own
+# time limit; the first failing step ends the run (no GPU work after a fault,
+# an abort or a timeout).  Outputs under gpurun_out/<TAG>/.
+#
+#   bash tools/gpu_run.sh TAG STEP [STEP ...]
+#
+#   tests                   pytest -m gpu (every GPU test) + __graft_entry__.smoke()
+#   pytest:PATH             one test file / node id
+#   bench:CFG               bench.py --config CFG (c1 c2 c3 c4 c4tree c5), JSON line kept
+#   profile:CFG:KERNEL      rocprofv3 kernel-trace stats + separate PMC passes of CFG's
+#                           bench line (tools/profile.sh); KERNEL = substring of the
+#                           dominant kernel's name for the summary
+#   ab:ARGS:VARIANTS        tools/ab_leaf.py one-process A/B; ARGS and VARIANTS use '+'
+#                           for spaces (e.g. ab:--trie+--log2n+20:main+rec2)
+#   rankstep:LOG2N:WORLD    tools/rank_step_probe.py (one rank's pipelined step, 3 sets)
+#   rehearse8               tools/rehearse8.sh (8 gloo ranks sharing the GPU, golden root)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=$1
+shift
+O=gpurun_out/$TAG
+mkdir -p $O
+for step in "$@"; do
+  IFS=: read -r kind a b <<< "$step"
+  name=$(echo "$step" | tr ':/+ <>,' '______')
+  case $kind in
+    tests)
+      timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+        > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+      tail -1 $O/pytest_gpu.log
+      timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+      tail -1 $O/smoke.log ;;
+    pytest)
+      timeout -k 10 600 python -u -m pytest "$a" -x -v --timeout 200 --timeout-method thread \
+        > $O/$name.log 2>&1 || { tail -30 $O/$name.log; exit 1; }
+      tail -1 $O/$name.log ;;
+    bench)
+      timeout -k 10 400 python bench.py --config $a > $O/bench_$a.json 2> $O/bench_$a.err || { tail -5 $O/bench_$a.err; exit 1; }
+      cat $O/bench_$a.json ;;
+    profile)
+      TAG=${TAG}_$a PROF_ARGS="--config $a --steps 10 --warmup 20 --no-cpu-baseline" KERNEL="$b" \
+        bash tools/profile.sh > $O/profile_$a.log 2>&1 || { tail -8 $O/profile_$a.log; exit 1; }
+      cp gpurun_out/prof_${TAG}_$a/summary.json $O/pmc_$a.json && echo "profile $a ok" ;;
+    ab)
+      timeout -k 10 400 python tools/ab_leaf.py ${a//+/ } --rounds 9 ${b//+/ } > $O/$name.log 2>&1 || { tail -8 $O/$name.log; exit 1; }
+      grep variant $O/$name.log | cut -c1-160 ;;
+    rankstep)
+      timeout -k 10 240 python tools/rank_step_probe.py --log2n $a --world $b --slots 3 > $O/rankstep_${a}_$b.txt 2>&1 \
+        || { tail -5 $O/rankstep_${a}_$b.txt; exit 1; }
+      tail -1 $O/rankstep_${a}_$b.txt ;;
+    rehearse8)
+      bash tools/rehearse8.sh > $O/rehearse8.log 2>&1 || { tail -20 $O/rehearse8.log; exit 1; }
+      cp gpurun_out/rehearse8_summary.json $O/ && echo "rehearse8 ok" ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "done $TAG"

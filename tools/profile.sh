@@ -18,5 +18,5 @@ run stats --kernel-trace --stats || exit $?
 run fetch --pmc FETCH_SIZE || exit $?
 run write --pmc WRITE_SIZE || exit $?
 run sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE || exit $?
-run lds --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_WAIT_ANY || exit $?
+run lds --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CU_CYCLES SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES || exit $?
 python3 tools/pmc_summary.py $D > $D/summary.json && cat $D/summary.json
