@@ -25,7 +25,7 @@ O=gpurun_out/$TAG
 mkdir -p $O
 for step in "$@"; do
   IFS=: read -r kind a b <<< "$step"
-  name=$(echo "$step" | tr ':/+ <>,' '______')
+  name=$(echo "$step" | sed 's/--//g' | tr ':/+ <>,.' '_______')
   case $kind in
     tests)
       timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
