@@ -535,8 +535,12 @@ int dev_tree_hash_elems(const void* d_elems, uint64_t n, uint32_t elem_len, void
             HIPCHK(hipEventCreate(&rec.b));
             HIPCHK(hipEventRecord(rec.a, st));
         }
-        hipLaunchKernelGGL(mk::k_elem_digests, dim3(ceil_div(n, 256)), dim3(256), 0, st, (const uint8_t*)d_elems, n,
-                           elem_len, fast32, (uint4*)dig);
+        if (fast32)
+            hipLaunchKernelGGL(mk::k_elem_digests<true>, dim3(ceil_div(n, 256)), dim3(256), 0, st,
+                               (const uint8_t*)d_elems, n, elem_len, (uint4*)dig);
+        else
+            hipLaunchKernelGGL(mk::k_elem_digests<false>, dim3(ceil_div(n, 256)), dim3(256), 0, st,
+                               (const uint8_t*)d_elems, n, elem_len, (uint4*)dig);
         HIPCHK(hipGetLastError());
         if (prof) {
             HIPCHK(hipEventRecord(rec.b, st));

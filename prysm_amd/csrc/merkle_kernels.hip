@@ -774,18 +774,24 @@ template __global__ void k_reduce_elem<false>(ReduceArgs);
 // Element digests K(le32(elem_len) || element i) -> out[i] (32 B): the first
 // half of the two-phase form, for trees too small for k_reduce_elem's
 // throughput pass and for element lengths other than 32.
+// FAST32: 32-B elements at a 16-B aligned base (one block, 16-B loads);
+// otherwise any length and alignment (the general sponge, its own kernel so
+// the fast form keeps its few VGPRs).
+template <bool FAST32>
 __global__ __launch_bounds__(256) void k_elem_digests(const uint8_t* __restrict__ elems, uint64_t n, uint32_t elem_len,
-                                                      uint32_t fast32, uint4* __restrict__ out) {
+                                                      uint4* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t d[8];
-    if (fast32)
+    if constexpr (FAST32)
         elem32_digest(reinterpret_cast<const uint4*>(elems) + 2 * i, d);
     else
         elem_digest_any(elems + i * (uint64_t)elem_len, elem_len, d);
     out[2 * i] = make_uint4(d[0], d[1], d[2], d[3]);
     out[2 * i + 1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
+template __global__ void k_elem_digests<true>(const uint8_t*, uint64_t, uint32_t, uint4*);
+template __global__ void k_elem_digests<false>(const uint8_t*, uint64_t, uint32_t, uint4*);
 
 // ----------------------------------------------------------------------------
 // Latency pass with two lanes per state (keccak_dev.hpp, mk::pair): lane pair

@@ -26,7 +26,8 @@ template <bool LEAF, bool FAST, int NI>
 __global__ void k_reduce(ReduceArgs a);
 template <bool FAST>
 __global__ void k_reduce_elem(ReduceArgs a);
-__global__ void k_elem_digests(const uint8_t* elems, uint64_t n, uint32_t elem_len, uint32_t fast32, uint4* out);
+template <bool FAST32>
+__global__ void k_elem_digests(const uint8_t* elems, uint64_t n, uint32_t elem_len, uint4* out);
 template <bool FAST>
 __global__ void k_struct_fields(const uint8_t* rec, uint64_t n, StructSpec sp, uint8_t* msg);
 __global__ void k_struct_fused(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
