@@ -1905,9 +1905,18 @@ __global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ 
 // 0.582 ms, profiles/r02d/ab_rec_prefetch.log): the other resident waves
 // hide the load as well.  At 5 waves/SIMD (96 VGPRs, 4 dwords spilled) the
 // stream of 2^20-deposit tries got 3 % slower (profiles/r02m/rejected/).
+#ifndef MK_REC_WAVES
+#define MK_REC_WAVES 1
+#endif
+// MK_REC_SPLIT: a block's 17 loads in two groups (the second issued once the
+// first is absorbed), so at most 9 words wait in VGPRs beside the state and
+// the kernel fits MK_REC_WAVES waves per SIMD.
+#ifndef MK_REC_SPLIT
+#define MK_REC_SPLIT 0
+#endif
 template <int NW>
-__global__ __launch_bounds__(kRecThreads) void k_keccak_rec(const uint2* __restrict__ in, uint64_t n,
-                                                            uint4* __restrict__ out) {
+__global__ __launch_bounds__(kRecThreads, MK_REC_WAVES) void k_keccak_rec(const uint2* __restrict__ in, uint64_t n,
+                                                                          uint4* __restrict__ out) {
     constexpr int NB = NW / 17 + 1;
     const uint64_t stride = (uint64_t)gridDim.x * kRecThreads;
 #pragma unroll 1
@@ -1919,6 +1928,7 @@ __global__ __launch_bounds__(kRecThreads) void k_keccak_rec(const uint2* __restr
         for (int b = 0; b < NB; ++b) {
 #pragma unroll
             for (int w = 0; w < 17; ++w) {
+                if (MK_REC_SPLIT && w == 9) asm volatile("" ::: "memory");
                 const int idx = 17 * b + w;
                 if (idx < NW) {
                     const uint2 v = p[idx];
@@ -2032,7 +2042,11 @@ template __global__ void k_keccak_rec_dma<35>(const uint2*, uint64_t, uint4*);
 // ----------------------------------------------------------------------------
 // Deposit trie level: node j = K(in[2j] || (2j+1 < cin ? in[2j+1] : 0^32)),
 // the map-miss-reads-zero rule of deposit_trie.go:35-37.
-__global__ __launch_bounds__(256) void k_trie_level(const uint4* __restrict__ in, uint64_t cin, uint4* __restrict__ out) {
+#ifndef MK_TRIE_LEVEL_WAVES
+#define MK_TRIE_LEVEL_WAVES 1
+#endif
+__global__ __launch_bounds__(256, MK_TRIE_LEVEL_WAVES) void k_trie_level(const uint4* __restrict__ in, uint64_t cin,
+                                                                        uint4* __restrict__ out) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t cout = (cin + 1) / 2;
     if (j >= cout) return;

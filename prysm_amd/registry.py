@@ -120,6 +120,58 @@ def state_root(registry: ValidatorRegistry, balances: np.ndarray) -> bytes:
     return hash_batch_var([reg + bal_root])[0]
 
 
+class DeviceStateHasher:
+    """TreeHash of State{ValidatorRegistry, ValidatorBalances} from records and
+    balances resident in HBM (BASELINE config 3, device-resident), with every
+    buffer allocated once.  Schedule on two streams: the struct kernel (5
+    permutations per validator, at the VALU issue ceiling) runs ALONE; the
+    balances tree then runs on a high-priority side stream beside the
+    registry tree.  Both trees are narrow and latency-bound (~20 levels of
+    one permutation latency each), so they fill each other's idle issue
+    slots; running the balances tree beside the struct kernel instead stole
+    ~90 us of the struct kernel's issue slots for a tree that needs ~10 us of
+    them (profiles/r03b: k_struct_reg 441 us alone, 533 us beside it)."""
+
+    def __init__(self, n: int, device):
+        import torch
+
+        from . import device as D
+
+        self.n, self.dev = n, device
+        L = _lib.load()
+        f = _fields(VALIDATOR_FIELDS)
+        self.roots = torch.empty(max(32, 32 * n), dtype=torch.uint8, device=device)
+        self.msg_ws = torch.empty(max(256, n * L.mk_ssz_struct_msg_len(f, len(VALIDATOR_FIELDS))), dtype=torch.uint8,
+                                  device=device)
+        self.reg_ws = D.merkle_workspace(n, 32, device)
+        self.bal_ws = D.merkle_workspace(n, 8, device)
+        self.pair = torch.empty(64, dtype=torch.uint8, device=device)  # reg_root || bal_root
+        self.out = torch.empty(32, dtype=torch.uint8, device=device)
+        self.side = torch.cuda.Stream(device=device, priority=-1)  # its own hardware queue
+        self.ev_roots = torch.cuda.Event()
+        self.ev_bal = torch.cuda.Event()
+
+    def submit(self, records, balances):
+        """records: (n*160,) uint8 device tensor; balances: (n*8,) uint8.
+        Enqueues on the current stream and returns the 32-B root tensor."""
+        import torch
+
+        from . import device as D
+
+        n = self.n
+        cur = torch.cuda.current_stream(self.dev)
+        D.struct_roots(records, n, 160, VALIDATOR_FIELDS, out=self.roots, ws=self.msg_ws)
+        self.ev_roots.record(cur)
+        self.side.wait_event(self.ev_roots)
+        with torch.cuda.stream(self.side):
+            D.merkle_hash(balances, n, 8, out=self.pair[32:], ws=self.bal_ws)
+            self.ev_bal.record(self.side)
+        D.merkle_hash(self.roots, n, 32, out=self.pair[:32], ws=self.reg_ws)
+        cur.wait_event(self.ev_bal)
+        D.hash_batch(self.pair, 1, 64, out=self.out)
+        return self.out
+
+
 FAR_FUTURE_EPOCH = (1 << 64) - 1  # shared/params/config.go:118
 _GAMMA = np.uint64(0x9E3779B97F4A7C15)
 

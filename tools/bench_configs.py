@@ -178,28 +178,15 @@ def run_config(args):
         bal = R.synthetic_balances(n, seed + 3)
         rec = torch.from_numpy(reg.records.view(np.uint8).reshape(-1).copy()).to(dev)
         dbal = torch.from_numpy(bal.view(np.uint8).copy()).to(dev)
-        spec = R._fields(R.VALIDATOR_FIELDS)
-        nf = len(R.VALIDATOR_FIELDS)
-        ws = torch.empty(L.mk_ssz_struct_list_workspace_bytes(n, spec, nf) + 4096, dtype=torch.uint8, device=dev)
-        bws = D.merkle_workspace(n, 8, dev)
-        roots = torch.empty(64, dtype=torch.uint8, device=dev)
-        out = torch.empty(32, dtype=torch.uint8, device=dev)
-
-        # high priority: its own hardware queue, so the balances tree really
-        # overlaps the struct kernel (tools/c3_streams.py: 0.91 -> 0.77 ms)
-        side = torch.cuda.Stream(device=dev, priority=-1)
+        # registry.DeviceStateHasher: struct kernel alone, then the registry
+        # and balances trees side by side (two latency-bound trees on two
+        # high-priority queues), then Keccak(reg_root || bal_root)
+        hasher = R.DeviceStateHasher(n, dev)
 
         def step():
-            # the two State fields are independent trees: balances on a second stream
-            cur = torch.cuda.current_stream(dev)
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                D.merkle_hash(dbal, n, 8, out=roots[32:], ws=bws)
-            _lib.check(L.mk_dev_ssz_struct_list_root(None, P(rec), n, 160, spec, nf, P(roots), P(ws), ws.numel(), st()),
-                       "registry")
-            cur.wait_stream(side)
-            _lib.check(L.mk_dev_hash_batch(None, P(roots), 1, 64, P(out), st()), "state")
+            return hasher.submit(rec, dbal)
 
+        out = hasher.out
         sec = _timeit(step, args.steps, args.warmup)
         got = bytes(out.cpu().numpy())
         assert got == R.state_root(reg, bal), "c3 root mismatch vs host-buffer path"
