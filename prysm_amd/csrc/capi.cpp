@@ -31,15 +31,15 @@ namespace {
 #define MK_SIDE_PRIO 1
 #endif
 constexpr bool kSidePrio = MK_SIDE_PRIO != 0;  // library side/copy streams at high priority
-// Tail split (experiment, 0 = off): of a leaf pass with more than 4x this many
-// full 1024-window workgroups, the last MK_TAIL_SPLIT of them run as twice as
-// many 512-window workgroups (k_reduce NI = 1, same output level) on a second
-// stream, so the pass's last round is made of half-length workgroups.
-#ifndef MK_TAIL_SPLIT
-#define MK_TAIL_SPLIT 0
-#endif
-#ifndef MK_TAIL_PRIO
-#define MK_TAIL_PRIO 0
+// Half-span tail (0 = off): of a leaf pass with at least 4x this many full
+// 1024-window workgroups, the last MK_HALF_TAIL spans run as twice as many
+// 512-window workgroups at the end of the same grid (k_reduce a.half_from),
+// so the straggling last round is made of half-length workgroups.  (Round 3
+// first tried them as a second kernel on another stream, MK_TAIL_SPLIT: the
+// two grids' workgroups interleave and the 2^25 leaf pass got 5 % slower,
+// profiles/r03e.)
+#ifndef MK_HALF_TAIL
+#define MK_HALF_TAIL 0
 #endif
 #ifndef MK_REC_KERNEL
 #define MK_REC_KERNEL 1
@@ -114,11 +114,7 @@ struct DevCtx {
     std::mutex side_mu;
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
-    // MK_TAIL_SPLIT: the last full spans of a leaf pass as half-size
-    // workgroups on a second stream that fill the pass's tail (see launch_plan)
-    std::mutex tail_mu;
-    hipStream_t tail = nullptr;
-    hipEvent_t tfork = nullptr, tjoin = nullptr;
+
     // host-buffer uploads on `copy` overlapping compute on `stream`
     hipStream_t copy = nullptr;
     hipEvent_t h2d = nullptr;
@@ -172,9 +168,6 @@ int bind_dev(int dev) {
                   hipEventCreateWithFlags(&c->join, hipEventDisableTiming) == hipSuccess &&
                   hipStreamCreateWithPriority(&c->copy, hipStreamNonBlocking, hi) == hipSuccess &&
                   hipEventCreateWithFlags(&c->h2d, hipEventDisableTiming) == hipSuccess;
-        ok = ok && hipStreamCreateWithPriority(&c->tail, hipStreamNonBlocking, MK_TAIL_PRIO ? hi : lo) == hipSuccess &&
-             hipEventCreateWithFlags(&c->tfork, hipEventDisableTiming) == hipSuccess &&
-             hipEventCreateWithFlags(&c->tjoin, hipEventDisableTiming) == hipSuccess;
         for (int i = 0; ok && i < 2; ++i)
             ok = hipEventCreateWithFlags(&c->region_ev[i], hipEventDisableTiming) == hipSuccess;
         for (int i = 0; ok && i < SmallStage::kSlots; ++i)
@@ -379,29 +372,16 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                 HIPCHK(hipGetLastError());
                 if (c) HIPCHK(hipEventRecord(c->join, c->side));
             }
-            // tail split: the last `tsplit` full spans as 2x NI = 1 workgroups on c->tail
-            const uint64_t tsplit = (MK_TAIL_SPLIT > 0 && ps.leaf && !a.elem_len && ps.ni == 2 &&
-                                     ps.nfast > 4ull * MK_TAIL_SPLIT) ? (uint64_t)MK_TAIL_SPLIT : 0;
-            DevCtx* tc = tsplit ? ctx() : nullptr;
-            std::unique_lock<std::mutex> tlk;
-            if (tsplit) {
-                tlk = std::unique_lock<std::mutex>(tc->tail_mu);
-                HIPCHK(hipEventRecord(tc->tfork, st));
-                HIPCHK(hipStreamWaitEvent(tc->tail, tc->tfork, 0));
-            }
             if (ps.nfast) {
                 a.wg_base = 0;
-                if (tsplit) {
-                    hipLaunchKernelGGL((mk::k_reduce<true, true, 2>), dim3(ps.nfast - tsplit), dim3(kReduceThreads), 0,
-                                       st, a);
-                    HIPCHK(hipGetLastError());
-                    ReduceArgs t = a;
-                    t.wg_base = 2 * (ps.nfast - tsplit);  // NI = 1 units: same windows, same output level
-                    hipLaunchKernelGGL((mk::k_reduce<true, true, 1>), dim3(2 * tsplit), dim3(kReduceThreads), 0,
-                                       tc->tail, t);
-                    HIPCHK(hipGetLastError());
-                    HIPCHK(hipEventRecord(tc->tjoin, tc->tail));
-                    HIPCHK(hipStreamWaitEvent(st, tc->tjoin, 0));
+                // half-span tail (MK_HALF_TAIL): the last T full spans as 2T
+                // half-length workgroups at the end of the same grid
+                const uint64_t T = (MK_HALF_TAIL > 0 && ps.leaf && !a.elem_len && ps.ni == 2 &&
+                                    ps.nfast >= 4ull * MK_HALF_TAIL) ? (uint64_t)MK_HALF_TAIL : 0;
+                if (T) {
+                    a.half_from = ps.nfast - T;
+                    hipLaunchKernelGGL((mk::k_reduce<true, true, 2>), dim3(ps.nfast + T), dim3(kReduceThreads), 0, st,
+                                       a);
                 } else if (ps.leaf && a.elem_len)
                     hipLaunchKernelGGL((mk::k_reduce_elem<true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
                 else if (ps.leaf && ps.ni == 1)

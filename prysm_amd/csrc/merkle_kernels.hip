@@ -365,10 +365,8 @@ __device__ __forceinline__ void first_level_generic(const ReduceArgs& a, uint64_
 // permute -> write -> barrier), then the workgroup's nodes (or, in the final
 // pass, the root with the length mix-in) to HBM.
 template <int NI>
-__device__ __forceinline__ void reduce_levels_out(const ReduceArgs& a, uint4* lds, uint32_t tid, uint64_t wg,
+__device__ __forceinline__ void reduce_levels_out(const ReduceArgs& a, uint4* lds, uint32_t tid, uint64_t lo1,
                                                   uint64_t c2, uint64_t m2, bool pair) {
-    constexpr uint64_t kSpan1 = 2 * NI * kReduceThreads;
-    constexpr uint64_t kSpan2 = kSpan1 / 2;
     uint64_t c = c2, m = m2;
     int left = a.finalize ? 64 : (int)a.levels - (pair ? 2 : 1);
     int done = 0;
@@ -410,7 +408,7 @@ __device__ __forceinline__ void reduce_levels_out(const ReduceArgs& a, uint4* ld
             out[1] = d1;
         }
     } else {
-        const uint64_t lo_out = ((pair ? wg * kSpan2 : wg * kSpan1)) >> done;
+        const uint64_t lo_out = (pair ? lo1 / 2 : lo1) >> done;  // the workgroup's first node of this level
         for (uint32_t k = tid; k < m; k += kReduceThreads) {
             out[2 * (lo_out + k)] = lds[2 * k];
             out[2 * (lo_out + k) + 1] = lds[2 * k + 1];
@@ -437,9 +435,16 @@ __global__ __launch_bounds__(kReduceThreads, (MK_LEAF_SPLIT && LEAF && FAST) ? M
     __shared__ uint4 lds[kLdsU4];
     const uint32_t tid = threadIdx.x;
     const uint64_t wg = a.wg_base + blockIdx.x;
-    const uint64_t lo1 = wg * kSpan1;
+    // a.half_from > 0 (FAST split leaf passes, MK_HALF_TAIL): workgroups from
+    // that index on take half a span (one window pair per thread), so the
+    // pass's last, straggling round is made of half-length workgroups; they
+    // are dispatched last because they have the highest indices
+    const bool half = kSplit && NI == 2 && a.half_from && wg >= a.half_from;
+    const uint64_t lo1 = half ? a.half_from * kSpan1 + (wg - a.half_from) * (kSpan1 / 2) : wg * kSpan1;
+    const int ni = half ? 1 : NI;
+    const uint64_t span1 = half ? kSpan1 / 2 : kSpan1;
     const uint64_t c1 = a.c1;
-    const uint64_t m1 = (c1 - lo1) < kSpan1 ? (c1 - lo1) : kSpan1;
+    const uint64_t m1 = (c1 - lo1) < span1 ? (c1 - lo1) : span1;
     const bool pair = a.levels >= 2 && (c1 > 1 || a.pad_at_one);
     const uint64_t c2 = pair ? (c1 + 1) / 2 : c1;
     const uint64_t m2 = pair ? (m1 + 1) / 2 : m1;
@@ -449,7 +454,7 @@ __global__ __launch_bounds__(kReduceThreads, (MK_LEAF_SPLIT && LEAF && FAST) ? M
         // the left window's digest waits in the thread's own level slot (the
         // pair node overwrites it), so no digest is held across a window
 #pragma unroll 1
-        for (int i = 0; i < NI; ++i) {
+        for (int i = 0; i < ni; ++i) {
             const uint32_t q = i * kReduceThreads + tid;
             const uint4* w = reinterpret_cast<const uint4*>(a.items) + (lo1 + 2 * (uint64_t)q) * 16;
             uint4 l0, l1, r0, r1, d0, d1;
@@ -540,7 +545,7 @@ __global__ __launch_bounds__(kReduceThreads, (MK_LEAF_SPLIT && LEAF && FAST) ? M
     }
     __syncthreads();
 
-    reduce_levels_out<NI>(a, lds, tid, wg, c2, m2, pair);
+    reduce_levels_out<NI>(a, lds, tid, lo1, c2, m2, pair);
 }
 
 template __global__ void k_reduce<true, true, 2>(ReduceArgs);
@@ -765,7 +770,7 @@ __global__ __launch_bounds__(kReduceThreads, FAST ? MK_ELEM_WAVES : 1) void k_re
         lds[2 * q + 1] = d1;
     }
     __syncthreads();
-    reduce_levels_out<NI>(a, lds, tid, wg, c2, m2, pair);
+    reduce_levels_out<NI>(a, lds, tid, lo1, c2, m2, pair);
 }
 
 template __global__ void k_reduce_elem<true>(ReduceArgs);

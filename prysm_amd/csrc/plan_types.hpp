@@ -31,6 +31,7 @@ struct ReduceArgs {
     uint64_t wg_base;      // workgroup index offset of this launch
     uint32_t in_ilv;       // k_wave3: input nodes are bit-interleaved lane pairs
     uint32_t out_ilv;      // k_wave3: write bit-interleaved output nodes
+    uint64_t half_from;    // k_reduce FAST leaf (split form): workgroups >= this take half a span (0 = none)
     uint32_t elem_len;     // LEAF, k_reduce_elem: `items` are n elements of elem_len bytes and the
                            // tree's 32-B items are their digests K(le32(elem_len) || element)
 };
