@@ -31,15 +31,21 @@ namespace {
 #define MK_SIDE_PRIO 1
 #endif
 constexpr bool kSidePrio = MK_SIDE_PRIO != 0;  // library side/copy streams at high priority
-// Half-span tail (0 = off): of a leaf pass with at least 4x this many full
-// 1024-window workgroups, the last MK_HALF_TAIL spans run as twice as many
-// 512-window workgroups at the end of the same grid (k_reduce a.half_from),
-// so the straggling last round is made of half-length workgroups.  (Round 3
-// first tried them as a second kernel on another stream, MK_TAIL_SPLIT: the
-// two grids' workgroups interleave and the 2^25 leaf pass got 5 % slower,
-// profiles/r03e.)
+// Half-span tail (0 = off): of a leaf pass of 4 x MK_HALF_TAIL ..
+// MK_HALF_TAIL_MAX full 1024-window workgroups (a few rounds of the 1,280
+// resident slots: the per-rank shards of a multi-GPU tree), the last
+// MK_HALF_TAIL spans run as twice as many 512-window workgroups at the end
+// of the same grid (k_reduce a.half_from), so the straggling last round is
+// made of half-length workgroups.  One process, same box (profiles/r03f):
+// 2^25 leaf pass 1.2986 -> 1.2902 ms, the 8-GPU rank step 1.3526 -> 1.3330
+// ms; 2^26 and 2^28 unchanged (hence the upper bound).  Round 3 first tried
+// them as a second kernel on another stream (MK_TAIL_SPLIT): the two grids'
+// workgroups interleave and the 2^25 leaf pass got 5 % slower (profiles/r03e).
 #ifndef MK_HALF_TAIL
-#define MK_HALF_TAIL 0
+#define MK_HALF_TAIL 256
+#endif
+#ifndef MK_HALF_TAIL_MAX
+#define MK_HALF_TAIL_MAX 8192
 #endif
 #ifndef MK_REC_KERNEL
 #define MK_REC_KERNEL 1
@@ -376,8 +382,10 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                 a.wg_base = 0;
                 // half-span tail (MK_HALF_TAIL): the last T full spans as 2T
                 // half-length workgroups at the end of the same grid
-                const uint64_t T = (MK_HALF_TAIL > 0 && ps.leaf && !a.elem_len && ps.ni == 2 &&
-                                    ps.nfast >= 4ull * MK_HALF_TAIL) ? (uint64_t)MK_HALF_TAIL : 0;
+                const uint64_t T = (MK_HALF_TAIL > 0 && mk::kLeafSplit && ps.leaf && !a.elem_len && ps.ni == 2 &&
+                                    ps.nfast >= 4ull * MK_HALF_TAIL && ps.nfast <= MK_HALF_TAIL_MAX)
+                                       ? (uint64_t)MK_HALF_TAIL
+                                       : 0;
                 if (T) {
                     a.half_from = ps.nfast - T;
                     hipLaunchKernelGGL((mk::k_reduce<true, true, 2>), dim3(ps.nfast + T), dim3(kReduceThreads), 0, st,

@@ -22,6 +22,12 @@ struct StructSpec {                 // flat fixed-layout record (hash.go:141-159
     uint32_t nfields, rec_len, msg_len;
 };
 
+// The leaf kernel's split window form (merkle_kernels.hip); the half-span
+// tail (ReduceArgs::half_from) exists only in it.
+#ifndef MK_LEAF_SPLIT
+#define MK_LEAF_SPLIT 1
+#endif
+constexpr bool kLeafSplit = MK_LEAF_SPLIT != 0;
 template <bool LEAF, bool FAST, int NI>
 __global__ void k_reduce(ReduceArgs a);
 template <bool FAST>

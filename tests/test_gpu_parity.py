@@ -543,3 +543,21 @@ def test_dev_struct_roots(gpu, layout, n):
     got = D.struct_roots(torch.from_numpy(raw.copy()).to("cuda:0"), n, rec_len, spec)
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().reshape(n, 32), want.reshape(n, 32))
+
+
+@pytest.mark.parametrize("n", [1 << 25, (1 << 25) + 12_345, (1 << 24) + 7 * 4096])
+def test_merkle_hash_half_span_tail(gpu, n):
+    """Leaf passes of 1,024..8,192 full workgroups end in half-span
+    workgroups (MK_HALF_TAIL, k_reduce a.half_from): the per-rank shard sizes
+    of a multi-GPU tree.  Unsharded and as an 8-shard frontier level."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    seed = SEED + 2025
+    items = torch.empty(n * 32, dtype=torch.uint8, device="cuda:0")
+    D.synth_fill(items, seed)
+    root = D.merkle_hash(items, n, 32)
+    torch.cuda.synchronize()
+    assert bytes(root.cpu().numpy()) == O.merkle_hash_gen(n, 32, seed, nthreads=16)
