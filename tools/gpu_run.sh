@@ -11,7 +11,7 @@
 #   bench:CFG               bench.py --config CFG (c1 c2 c3 c4 c4tree c5), JSON line kept
 #   profile:CFG:KERNEL      rocprofv3 kernel-trace stats + separate PMC passes of CFG's
 #                           bench line (tools/profile.sh); KERNEL = substring of the
-#                           dominant kernel's name for the summary
+#                           dominant kernel's name for the summary (empty: C4's leaf kernel)
 #   ab:ARGS:VARIANTS        tools/ab_leaf.py one-process A/B; ARGS and VARIANTS use '+'
 #                           for spaces (e.g. ab:--trie+--log2n+20:main+rec2)
 #   rankstep:LOG2N:WORLD    tools/rank_step_probe.py (one rank's pipelined step, 3 sets)
@@ -41,7 +41,8 @@ for step in "$@"; do
       timeout -k 10 400 python bench.py --config $a > $O/bench_$a.json 2> $O/bench_$a.err || { tail -5 $O/bench_$a.err; exit 1; }
       cat $O/bench_$a.json ;;
     profile)
-      TAG=${TAG}_$a PROF_ARGS="--config $a --steps 10 --warmup 20 --no-cpu-baseline" KERNEL="$b" \
+      if [ -n "$b" ]; then export KERNEL="$b"; else unset KERNEL; fi  # empty: the C4 leaf kernel
+      TAG=${TAG}_$a PROF_ARGS="--config $a --steps 10 --warmup 20 --no-cpu-baseline" \
         bash tools/profile.sh > $O/profile_$a.log 2>&1 || { tail -8 $O/profile_$a.log; exit 1; }
       cp gpurun_out/prof_${TAG}_$a/summary.json $O/pmc_$a.json && echo "profile $a ok" ;;
     ab)
