@@ -69,6 +69,15 @@ int main(int argc, char** argv) {
             REQUIRE(replay(p, nchunks, false) == 1);
             REQUIRE(plan_ws_bytes(p) >= 32 * (p.slot_nodes[0] + p.slot_nodes[1]));
         }
+        // the element-digest tree's plan (k_reduce_elem: one window pair per
+        // thread in throughput leaf passes): same tree, NI = 1 leaf workgroups
+        if (n > 4) {
+            Plan ep;
+            REQUIRE(make_plan(n, 32, false, 0, false, true, ep, false, 0, 0, true) == MK_OK);
+            REQUIRE(!ep.small && replay(ep, ceil_div(n, 4), false) == 1);
+            const Pass& lp = ep.passes[0];
+            if (!lp.wave && !lp.sp) REQUIRE(lp.ni == 1 && lp.nwg == ceil_div(lp.a.c1, 2 * kReduceThreads));
+        }
         // shard plan + per-shard frontier plans
         const uint32_t world = (uint32_t)pick(1, 16);
         uint32_t h = 0, ne = 0;
