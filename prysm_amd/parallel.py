@@ -311,3 +311,103 @@ class ShardedMerklePipeline:
         if self.rank == 0:
             return self.finish_nodes_fn(g, self.count, self.n_total, self.outs[slot])
         return None
+
+
+# ---------------------------------------------------------------- deposit trie
+@dataclass
+class TrieShardPlan:
+    """Subtree split of an n-deposit, depth-`depth` trie over `world` ranks
+    (SURVEY.md §8e, C5): rank r holds deposits [r·2^height, (r+1)·2^height)
+    and builds its height-`height` subtree; nonempty ranks contribute a
+    root (an empty shard's node is absent, i.e. 0^32 — the Go map miss of
+    deposit_trie.go:35-37).  height == 0 means: too small to shard, rank 0
+    builds the whole trie."""
+    n: int
+    depth: int
+    height: int
+    nonempty: int
+
+    def items(self, rank: int):
+        if self.height == 0:
+            return (0, self.n) if rank == 0 else (self.n, self.n)
+        lo = min(self.n, rank << self.height)
+        return lo, min(self.n, lo + (1 << self.height))
+
+
+def trie_plan(n: int, world: int, depth: int = 32) -> TrieShardPlan:
+    if world < 1 or n < 0 or n > (1 << depth):
+        raise ValueError("bad trie shard plan arguments")
+    h = 0
+    while (1 << h) * world < n:
+        h += 1
+    ne = -(-n // (1 << h)) if n else 0
+    if h == 0 or ne <= 1 or h >= depth:
+        return TrieShardPlan(n, depth, 0, 1 if n else 0)
+    return TrieShardPlan(n, depth, h, ne)
+
+
+def deposit_subtree_root(data: torch.Tensor, count: int, deposit_len: int, height: int,
+                         out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Root of one shard: the batch build (deposit_trie.go:29-40) of its
+    `count` fixed-length deposits as a depth-`height` trie (the shard's
+    subtree of the global trie: same leaf hashes, same 0^32 for absent
+    nodes), on the device."""
+    from . import device as D
+
+    lv = torch.empty(D.deposit_trie_levels_bytes(count, height), dtype=torch.uint8, device=data.device)
+    out = out if out is not None else torch.empty(32, dtype=torch.uint8, device=data.device)
+    D.deposit_trie_build(lv, count, data, count, deposit_len, height, height, out)
+    return out
+
+
+def deposit_trie_top(roots: torch.Tensor, nonempty: int, world: int, levels_above: int,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The trie above the shards: the `nonempty` gathered shard roots are
+    level 0 of a depth-`levels_above` trie (absent right children 0^32, then
+    the zero-sibling levels up to the full depth), on the device."""
+    from . import device as D
+
+    lv = torch.zeros(D.deposit_trie_levels_bytes(world, levels_above), dtype=torch.uint8, device=roots.device)
+    lv[:32 * nonempty] = roots[:32 * nonempty]
+    out = out if out is not None else torch.empty(32, dtype=torch.uint8, device=roots.device)
+    D.deposit_trie_levels(lv, world, nonempty, 0, levels_above, levels_above, out)
+    return out
+
+
+def sharded_deposit_trie_root(local_data: torch.Tensor, deposit_len: int, tp: TrieShardPlan, rank: int,
+                              world: int, group=None, subtree_fn: Optional[Callable] = None,
+                              top_fn: Optional[Callable] = None,
+                              full_fn: Optional[Callable] = None) -> Optional[torch.Tensor]:
+    """Root of the deposit trie of tp.n fixed-length deposits sharded by
+    subtree over the ranks ("Deposit trie (C5): same split
+    with a 32-B zero pad, plus the zero-sibling levels on GPU 0"): every
+    rank builds its subtree with no communication, one all-gather of 32 B
+    per rank, rank 0 builds the levels above.  Returns the root on rank 0,
+    None elsewhere.  The compute steps are injectable (CPU tests, gloo)."""
+    subtree_fn = subtree_fn or deposit_subtree_root
+    top_fn = top_fn or deposit_trie_top
+    lo, hi = tp.items(rank)
+    dev = local_data.device
+    if tp.height == 0:  # too small to shard: rank 0 builds it all
+        if rank != 0:
+            return None
+        if full_fn is None:
+            def full_fn(d, cnt, ln, depth):
+                if cnt == 0:
+                    return torch.zeros(32, dtype=torch.uint8, device=d.device)
+                return deposit_subtree_root(d, cnt, ln, depth)
+        return full_fn(local_data, tp.n, deposit_len, tp.depth)
+    if hi > lo:
+        root = subtree_fn(local_data, hi - lo, deposit_len, tp.height)
+    else:
+        root = torch.zeros(32, dtype=torch.uint8, device=dev)
+    if root.is_cuda and dist.get_backend(group) == "gloo":
+        host = torch.empty(32 * world, dtype=torch.uint8)
+        dist.all_gather_into_tensor(host, root.cpu(), group=group)
+        gathered = host.to(dev)
+    else:
+        gathered = torch.empty(32 * world, dtype=root.dtype, device=dev)
+        dist.all_gather_into_tensor(gathered, root, group=group)
+    if rank == 0:
+        return top_fn(gathered, tp.nonempty, world, tp.depth - tp.height)
+    return None

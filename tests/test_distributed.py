@@ -181,3 +181,72 @@ def test_python_plan_matches_c_planner(n, item_len, world):
     assert (ne.value, list(begin)) == (pne, pbegin)
     if pne > 1:
         assert h.value == ph
+
+
+def _trie_worker(rank, world, port, n, q, depth=32):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from oracle import oracle as O
+        from prysm_amd import parallel as P
+
+        dl = 280
+        tp = P.trie_plan(n, world, depth)
+        lo, hi = tp.items(rank)
+        full = O.splitmix_bytes(max(n, 1) * dl, SEED + 5)
+        local = torch.from_numpy(full[lo * dl:hi * dl].copy())
+
+        def subtree(data, cnt, ln, h):
+            deps = [bytes(data[i * ln:(i + 1) * ln].numpy()) for i in range(cnt)]
+            return torch.frombuffer(bytearray(O.deposit_trie_levels(deps, h)[0]), dtype=torch.uint8)
+
+        def top(g, ne, world_, above):
+            level = [bytes(g[32 * i:32 * i + 32].numpy()) for i in range(ne)]
+            for _ in range(above):  # absent right child = 0^32 (deposit_trie.go:35-37)
+                if len(level) % 2:
+                    level = level + [bytes(32)]
+                level = [O.keccak256(level[i] + level[i + 1]) for i in range(0, len(level), 2)]
+            return torch.frombuffer(bytearray(level[0]), dtype=torch.uint8)
+
+        def full_fn(data, cnt, ln, d):
+            deps = [bytes(data[i * ln:(i + 1) * ln].numpy()) for i in range(cnt)]
+            return torch.frombuffer(bytearray(O.deposit_trie_levels(deps, d)[0] if cnt else bytes(32)),
+                                    dtype=torch.uint8)
+
+        root = P.sharded_deposit_trie_root(local, dl, tp, rank, world, subtree_fn=subtree, top_fn=top,
+                                           full_fn=full_fn)
+        if rank == 0:
+            q.put((bytes(root.numpy()), tp.height, tp.nonempty))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 1000), (4, 1024), (4, 777), (3, 100), (8, 5), (4, 0), (8, 2049)])
+def test_sharded_deposit_trie_root(world, n):
+    """SURVEY §8e's C5 split: every rank builds its power-of-two subtree of
+    the depth-32 deposit trie, one 32-B all-gather, rank 0 builds the levels
+    above (0^32 for absent nodes, then the zero-sibling levels); the root
+    equals the one-piece build (ragged last shard, empty shards, too small to
+    shard, empty trie)."""
+    from oracle import oracle as O
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trie_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    root, h, ne = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    dl = 280
+    full = O.splitmix_bytes(max(n, 1) * dl, SEED + 5)
+    deps = [bytes(full[i * dl:(i + 1) * dl]) for i in range(n)]
+    want = O.deposit_trie_levels(deps, 32)[0] if n else bytes(32)
+    assert root == want
+    if n >= 2 * world:
+        assert h > 0 and ne > 1  # really sharded

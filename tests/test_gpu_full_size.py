@@ -184,3 +184,39 @@ def test_c5_full_2p20_deposits(gpu):
                "mk_dev_deposit_trie_append")
     torch.cuda.synchronize()
     assert bytes(root.cpu().numpy()).hex() == g["root"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 8])
+def test_c5_sharded_subtrees_on_one_device(gpu, world):
+    """SURVEY §8e's C5 split at full size on one device: every shard's
+    depth-h subtree (parallel.deposit_subtree_root), the gathered roots as
+    level 0 of the trie above (parallel.deposit_trie_top) = the golden 2^20
+    root; a ragged n (2^20 - 12345) against the one-piece device build."""
+    import torch
+
+    from prysm_amd import device as D
+    from prysm_amd import parallel as P
+
+    g = GOLD["c5"]
+    n, dl, depth = g["n"], g["deposit_len"], g["depth"]
+    data = torch.empty(n * dl, dtype=torch.uint8, device=gpu)
+    D.synth_fill(data, g["seed"])
+    for nn in (n, n - 12_345):
+        tp = P.trie_plan(nn, world, depth)
+        assert tp.height > 0 and tp.nonempty > 1
+        roots = torch.zeros(32 * world, dtype=torch.uint8, device=gpu)
+        for r in range(world):
+            lo, hi = tp.items(r)
+            if hi > lo:
+                P.deposit_subtree_root(data[lo * dl:hi * dl], hi - lo, dl, tp.height, out=roots[32 * r:32 * r + 32])
+        root = P.deposit_trie_top(roots, tp.nonempty, world, depth - tp.height)
+        torch.cuda.synchronize()
+        if nn == n:
+            assert bytes(root.cpu().numpy()).hex() == g["root"]
+        else:
+            lv = torch.empty(D.deposit_trie_levels_bytes(nn, depth), dtype=torch.uint8, device=gpu)
+            want = torch.empty(32, dtype=torch.uint8, device=gpu)
+            D.deposit_trie_build(lv, nn, data, nn, dl, depth, depth, want)
+            torch.cuda.synchronize()
+            assert bytes(root.cpu().numpy()) == bytes(want.cpu().numpy())
