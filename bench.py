@@ -223,7 +223,10 @@ def main():
                     help="N devices from one process through mk_dev_ssz_merkle_hash_multi (the cgo caller's "
                          "form: one shard per device, RCCL all-gather inside the library)")
     args = ap.parse_args()
-    if args.config != "c4":
+    if args.config == "c5" and args.gpus > 1:  # SURVEY §8e's C5 split over N ranks
+        if "WORLD_SIZE" not in os.environ:
+            return launch_ranks(args.gpus, sys.argv[1:])
+    elif args.config != "c4":
         from tools.bench_configs import run_config
 
         return run_config(args)
@@ -240,8 +243,9 @@ def main():
         return 2
     if args.share_device:
         local = 0
+    body = run_c5_ranks if args.config == "c5" else run_ranks
     if world == 1:
-        return run_ranks(args, world, rank, local)
+        return body(args, world, rank, local)
     # N ranks: every failure (a rank that never joins, a collective that
     # times out after parallel.dist_timeout(), a HIP/RCCL error) ends this rank
     # with an error JSON line and a non-zero status instead of a silent hang;
@@ -249,7 +253,7 @@ def main():
     watchdog = Deadline(float(os.environ.get("PRYSM_BENCH_DEADLINE", "900")),
                         lambda: error_line(args, world, rank, "deadline exceeded (PRYSM_BENCH_DEADLINE)"))
     try:
-        return run_ranks(args, world, rank, local)
+        return body(args, world, rank, local)
     except Exception as e:  # noqa: BLE001 -- reported, then the rank fails
         error_line(args, world, rank, f"{type(e).__name__}: {e}")
         return 3
@@ -487,6 +491,101 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
             nt = min(16, len(os.sched_getaffinity(0)))
             out["cpu_baseline_threads"] = cpu_baseline(item_len, args.cpu_sample_log2n, threads=nt)
         print(json.dumps(out), flush=True)
+    if world > 1:
+        st = torch.tensor([status], dtype=torch.int32, device=dev if args.backend == "nccl" else "cpu")
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        status = int(st.item())
+        dist.destroy_process_group()
+    return status
+
+
+def run_c5_ranks(args, world: int, rank: int, local: int) -> int:
+    """BASELINE config 5 over N ranks: the depth-32 deposit
+    trie of 2^20 x 280-B deposits split by subtree (parallel.trie_plan):
+    every rank builds its 2^h-deposit subtree from deposits generated in its
+    HBM, one all-gather of 32 B per rank, rank 0 builds the levels above.
+    value = deposits of all ranks / max-over-ranks time; strong scaling."""
+    import torch
+    import torch.distributed as dist
+
+    from prysm_amd import device as D
+    from prysm_amd import parallel as P
+
+    if world > 1 and args.backend == "gloo":
+        P.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1 and args.backend == "nccl":
+        P.init_process_group("nccl", dev)
+    n, dl, depth = 1 << 20, 280, 32
+    seed = 0x5EED000000000000 + 5
+    tp = P.trie_plan(n, world, depth)
+    lo, hi = tp.items(rank)
+    cnt = hi - lo
+    data = torch.empty(max(cnt * dl, 16), dtype=torch.uint8, device=dev)
+    if cnt:
+        D.synth_fill(data[:cnt * dl], seed, word0=lo * dl // 8)
+    sub_h = tp.height if tp.height else depth
+    lv = torch.empty(D.deposit_trie_levels_bytes(max(cnt, 1), sub_h), dtype=torch.uint8, device=dev)
+    root = torch.zeros(32, dtype=torch.uint8, device=dev)
+    gathered = torch.zeros(32 * world, dtype=torch.uint8, device=dev)
+    top_lv = torch.zeros(D.deposit_trie_levels_bytes(world, max(depth - tp.height, 1)), dtype=torch.uint8,
+                         device=dev)
+    out = torch.zeros(32, dtype=torch.uint8, device=dev)
+    gloo = world > 1 and args.backend == "gloo"
+
+    def step():
+        if cnt:
+            D.deposit_trie_build(lv, cnt, data, cnt, dl, sub_h, sub_h, root)
+        if world == 1 or tp.height == 0:
+            return root
+        if gloo:
+            host = torch.empty(32 * world, dtype=torch.uint8)
+            dist.all_gather_into_tensor(host, root.cpu())
+            gathered.copy_(host)
+        else:
+            dist.all_gather_into_tensor(gathered, root)
+        if rank == 0:
+            top_lv[:32 * tp.nonempty] = gathered[:32 * tp.nonempty]
+            D.deposit_trie_levels(top_lv, world, tp.nonempty, 0, depth - tp.height, depth - tp.height, out)
+            return out
+        return None
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    status = 0
+    if rank == 0:
+        got = bytes(r.cpu().numpy()).hex()
+        try:
+            with open(os.path.join(ROOT, "tests", "golden", "full_size_roots.json")) as f:
+                want = json.load(f)["c5"]["root"]
+        except (OSError, KeyError, ValueError):
+            want = None
+        status = 0 if want is None or got == want else 1
+        sec = t.item() / args.steps
+        print(json.dumps({
+            "metric": "deposit trie build, 2^20 x 280-B deposits, depth 32", "value": n / sec, "unit": "deposits/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": sec * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "u64 (Keccak lanes as u32 pairs)", "data": "synthetic (device SplitMix64, seed 0x5EED..05)",
+            "config": {"workload": "C5 split by subtree: per-rank 2^h-deposit subtrees, 32-B all-gather, rank-0 top",
+                       "n": n, "subtree_height": tp.height, "nonempty": tp.nonempty, "root": got,
+                       "root_matches_golden": None if want is None else got == want,
+                       "backend": str(dist.get_backend()) if world > 1 else None,
+                       "world_size": dist.get_world_size() if world > 1 else 1}}), flush=True)
     if world > 1:
         st = torch.tensor([status], dtype=torch.int32, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
