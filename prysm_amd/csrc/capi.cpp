@@ -421,10 +421,6 @@ int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, 
     const uint64_t grid = ceil_div(n, 256);
     if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0)
         hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
-    else if (MK_REC_DMA && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0)
-        hipLaunchKernelGGL((mk::k_keccak_rec_dma<35>),
-                           dim3(std::min<uint64_t>(ceil_div(n, mk::kRecThreads), mk::kRecDmaGrid)),
-                           dim3(mk::kRecThreads), 0, st, (const uint2*)d_in, n, (uint4*)d_out);
     else if (kRecKernel && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0)
         hipLaunchKernelGGL((mk::k_keccak_rec<35>),
                            dim3(std::min<uint64_t>(ceil_div(n, mk::kRecThreads), mk::kRecGridMax)),
@@ -758,17 +754,6 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
     if (kStructReg && layout && split && nb == 2 && nraw == 0) {
         hipLaunchKernelGGL((mk::k_struct_split<2, 0>), dim3(ceil_div(n, 64)), dim3(256), 0, st, (const uint8_t*)d_rec,
                            n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);
-        HIPCHK(hipGetLastError());
-        return MK_OK;
-    }
-    bool val160 = MK_STRUCT_DMA && layout && nb == 3 && nraw == 6 && vec16 && sp.rec_len == 160;
-    for (uint32_t f = 0; val160 && f < sp.nfields; ++f)  // the validator layout, field for field
-        val160 = sp.off[f] == (f == 0 ? 0u : f == 1 ? 48u : f == 2 ? 80u : 112u + 8u * (f - 3)) &&
-                 sp.len[f] == (f == 0 ? 48u : f < 3 ? 32u : 8u);
-    if (val160) {
-        hipLaunchKernelGGL(mk::k_struct_val_dma, dim3(std::min<uint64_t>(ceil_div(n, mk::kStructThreads),
-                                                                          mk::kStructDmaGrid)),
-                           dim3(mk::kStructThreads), 0, st, (const uint4*)d_rec, n, (uint4*)d_roots);
         HIPCHK(hipGetLastError());
         return MK_OK;
     }

@@ -119,11 +119,10 @@ __device__ __forceinline__ void hash_final(uint4 r0, uint4 r1, uint64_t n, uint4
 }
 
 // ----------------------------------------------------------------------------
-// Fast 256-B window (two Keccak blocks).  The block loop is rolled so the
-// kernel keeps one keccak_f copy in its hot loop (I-cache).
-#ifndef MK_LOAD_ALL
-#define MK_LOAD_ALL 1
-#endif
+// Full 256-B window (two Keccak blocks) for the general leaf paths
+// (first_level_generic, k_spread_leaf neighbours): the whole window is in
+// registers before the first permutation, so each 128-B line is fetched once.
+// The throughput leaf pass uses hash_window256_split below instead.
 #ifndef MK_MIN_WAVES
 #define MK_MIN_WAVES 1
 #endif
@@ -131,9 +130,6 @@ __device__ __forceinline__ void hash_final(uint4 r0, uint4 r1, uint64_t n, uint4
 __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint4& d0, uint4& d1) {
     State s;
     zero(s);
-#if MK_LOAD_ALL
-    // whole window in registers before the first permutation: each 128-B
-    // line is fetched once (no L2 re-fetch of the line shared by both blocks)
     uint4 v[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) v[k] = ld_stream(w + k);
@@ -160,108 +156,19 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
     s.hi[16] ^= 0x80000000u;
     keccak_f_digest(s);
     digest(s, d0, d1);
-    return;
-#endif
-#pragma unroll 1
-    for (int b = 0; b < 2; ++b) {
-        if (b == 0) {
-            uint4 v[9];
-#pragma unroll
-            for (int k = 0; k < 9; ++k) v[k] = ld_stream(w + k);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                s.lo[2 * k] ^= v[k].x;
-                s.hi[2 * k] ^= v[k].y;
-                s.lo[2 * k + 1] ^= v[k].z;
-                s.hi[2 * k + 1] ^= v[k].w;
-            }
-            s.lo[16] ^= v[8].x;
-            s.hi[16] ^= v[8].y;
-        } else {
-            const uint2 t = ld_stream(reinterpret_cast<const uint2*>(w + 8) + 1);
-            uint4 v[7];
-#pragma unroll
-            for (int k = 0; k < 7; ++k) v[k] = ld_stream(w + 9 + k);
-            s.lo[0] ^= t.x;
-            s.hi[0] ^= t.y;
-#pragma unroll
-            for (int k = 0; k < 7; ++k) {
-                s.lo[1 + 2 * k] ^= v[k].x;
-                s.hi[1 + 2 * k] ^= v[k].y;
-                s.lo[2 + 2 * k] ^= v[k].z;
-                s.hi[2 + 2 * k] ^= v[k].w;
-            }
-            s.lo[15] ^= 1u;  // byte 256 = byte 120 of block 1
-            s.hi[16] ^= 0x80000000u;
-        }
-        keccak_f(s);
-    }
-    digest(s, d0, d1);
 }
 
-// MK_STAGE_LDS=1: the same window with its second block parked in this
-// thread's 128-B LDS slot (dword-major across the workgroup:
-// stg[k * kReduceThreads], conflict-free 16-B accesses) for the duration of
-// the first permutation, so the 30 VGPRs it held there are free and the leaf
-// kernel fits 5 waves/SIMD (96 VGPRs, 32 KB LDS per workgroup).
-#ifndef MK_STAGE_LDS
-#define MK_STAGE_LDS 1
-#endif
-#ifndef MK_STAGE_WAVES
-#define MK_STAGE_WAVES 5
-#endif
-
-__device__ __forceinline__ void hash_window256_staged(const uint4* __restrict__ w, uint4* stg, uint4& d0,
-                                                      uint4& d1) {
-    State s;
-    uint4 v[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) v[k] = ld_stream(w + k);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) stg[k * kReduceThreads] = v[8 + k];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        s.lo[2 * k] = v[k].x;
-        s.hi[2 * k] = v[k].y;
-        s.lo[2 * k + 1] = v[k].z;
-        s.hi[2 * k + 1] = v[k].w;
-    }
-    s.lo[16] = v[8].x;
-    s.hi[16] = v[8].y;
-#pragma unroll
-    for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
-    keccak_f(s);
-    uint4 u[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) u[k] = stg[k * kReduceThreads];
-    s.lo[0] ^= u[0].z;
-    s.hi[0] ^= u[0].w;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-        s.lo[1 + 2 * k] ^= u[1 + k].x;
-        s.hi[1 + 2 * k] ^= u[1 + k].y;
-        s.lo[2 + 2 * k] ^= u[1 + k].z;
-        s.hi[2 + 2 * k] ^= u[1 + k].w;
-    }
-    s.lo[15] ^= 1u;
-    s.hi[16] ^= 0x80000000u;
-    keccak_f_digest(s);
-    digest(s, d0, d1);
-}
-
-// MK_LEAF_SPLIT=1: the window without a staging buffer.  Block 1 (bytes
-// 0..135) is loaded straight into the state registers, block 2 only after
-// the first permutation, in two halves, so at most 16 data VGPRs are live
-// beside the state; the thread's held digests live in its own LDS level
-// slots (k_reduce), so the kernel fits MK_LEAF_SPLIT_WAVES waves per SIMD
-// with 16 KB of LDS per workgroup.  The 128-B line shared by both blocks is
-// fetched twice when it leaves L2 in between (infinity-cache hit).  The
-// default since plain loads replaced non-temporal ones: at 6 waves 0.4 %
-// faster than the staged form at 2^28, 1-2 % at 2^25 (profiles/r02zg/README.md),
-// at 5 waves about 1 % more (below).
-#ifndef MK_LEAF_SPLIT
-#define MK_LEAF_SPLIT 1
-#endif
+// The throughput leaf pass's window (MK_LEAF_SPLIT, merkle_kernels.hpp; the
+// only form since round 3).  Block 1 (bytes 0..135) is loaded straight into
+// the state registers, block 2 only after the first permutation, in two
+// halves, so at most 16 data VGPRs are live beside the state; the thread's
+// held digests live in its own LDS level slots (k_reduce), so the kernel
+// fits MK_LEAF_SPLIT_WAVES waves per SIMD with 16 KB of LDS per workgroup.
+// The 128-B line shared by both blocks is fetched twice when it leaves L2 in
+// between (infinity-cache hit).  Against round 2's LDS-staged form (block 2
+// parked in LDS through the first permutation: 1.04x fetch, 32 KB LDS): at
+// 6 waves 0.4 % faster at 2^28, 1-2 % at 2^25 (profiles/r02zg/README.md), at
+// 5 waves about 1 % more (below); the staged form was removed in round 3.
 // 5 waves: 94 VGPRs and no spill, 0.8-1.7 % faster than 6 waves (80 VGPRs,
 // 15 dwords in scratch) and 7 waves (54 spilled) slower still
 // (profiles/r02zi, r02zj).
@@ -424,15 +331,12 @@ __device__ __forceinline__ void reduce_levels_out(const ReduceArgs& a, uint4* ld
 // Non-final passes write 512 >> (levels-2) nodes per workgroup; the final
 // pass (one workgroup) reduces to the root and applies the length mix-in.
 template <bool LEAF, bool FAST, int NI>
-__global__ __launch_bounds__(kReduceThreads, (MK_LEAF_SPLIT && LEAF && FAST) ? MK_LEAF_SPLIT_WAVES
-                                             : (MK_STAGE_LDS && LEAF && FAST) ? MK_STAGE_WAVES : MK_MIN_WAVES) void k_reduce(
-    ReduceArgs a) {
+__global__ __launch_bounds__(kReduceThreads, (MK_LEAF_SPLIT && LEAF && FAST) ? MK_LEAF_SPLIT_WAVES : MK_MIN_WAVES) void
+k_reduce(ReduceArgs a) {
     constexpr uint64_t kSpan1 = 2 * NI * kReduceThreads;  // first-level nodes per workgroup
     constexpr uint64_t kSpan2 = kSpan1 / 2;
     constexpr bool kSplit = MK_LEAF_SPLIT && LEAF && FAST;
-    constexpr bool kStaged = !kSplit && MK_STAGE_LDS && LEAF && FAST;
-    constexpr uint64_t kLdsU4 = kStaged && 8 * kReduceThreads > 2 * kSpan2 ? 8 * kReduceThreads : 2 * kSpan2;
-    __shared__ uint4 lds[kLdsU4];
+    __shared__ uint4 lds[2 * kSpan2];
     const uint32_t tid = threadIdx.x;
     const uint64_t wg = a.wg_base + blockIdx.x;
     // a.half_from > 0 (FAST split leaf passes, MK_HALF_TAIL): workgroups from
@@ -467,31 +371,6 @@ __global__ __launch_bounds__(kReduceThreads, (MK_LEAF_SPLIT && LEAF && FAST) ? M
             hash_pair(l0, l1, r0, r1, false, d0, d1);
             lds[2 * q] = d0;
             lds[2 * q + 1] = d1;
-        }
-    } else if constexpr (kStaged) {
-        // The staging slots alias the level buffer: every pair node stays in
-        // registers until all threads are done with their slots.
-        static_assert(NI == 1 || NI == 2, "staged leaf pass holds at most 2 pair nodes");
-        uint4 e0 = make_uint4(0, 0, 0, 0), e1 = e0, d0, d1;
-#pragma unroll 1
-        for (int i = 0; i < NI; ++i) {
-            const uint32_t q = i * kReduceThreads + tid;
-            const uint4* w = reinterpret_cast<const uint4*>(a.items) + (lo1 + 2 * (uint64_t)q) * 16;
-            uint4 l0, l1, r0, r1;
-            hash_window256_staged(w, lds + tid, l0, l1);
-            hash_window256_staged(w + 16, lds + tid, r0, r1);
-            hash_pair(l0, l1, r0, r1, false, d0, d1);
-            if (i == 0) {
-                e0 = d0;
-                e1 = d1;
-            }
-        }
-        __syncthreads();
-        lds[2 * tid] = e0;
-        lds[2 * tid + 1] = e1;
-        if (NI == 2) {
-            lds[2 * (kReduceThreads + tid)] = d0;
-            lds[2 * (kReduceThreads + tid) + 1] = d1;
         }
     } else if constexpr (FAST) {
         // Full workgroup of full windows / complete node pairs (host-checked):
@@ -1734,100 +1613,6 @@ __global__ __launch_bounds__(256) void k_struct_split(const uint8_t* __restrict_
 template __global__ void k_struct_split<3, 6>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
 template __global__ void k_struct_split<2, 0>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
 
-// The validator layout (160-B records, 16-B aligned: Pubkey 48 B @0,
-// WithdrawalCredentialsHash32 32 B @48, RandaoCommitmentHash32 32 B @80, six
-// uint64 @112; SURVEY.md §8d, the synthetic pb.Validator mirror) with every
-// record moved into LDS by DMA (global_load_lds_dwordx4: 10 aligned 16-B
-// units per record, lane l's unit k at B[k][l], conflict-free ds_read_b128)
-// and the next record's DMA in flight during this record's two struct
-// permutations (persistent grid-stride threads).  Field digest f overwrites
-// the units of field f once they are consumed (d0 -> units 1-2, d1 -> 3-4,
-// d2 -> 5-6), so the struct message K(d0 || d1 || d2 || le64 x 6) is units
-// 1..9 as they stand (hash.go:141-159): no separate digest column.
-// 40 KB of LDS per 256-thread workgroup: 4 workgroups (4 waves/SIMD) per CU.
-__global__ __launch_bounds__(kStructThreads) void k_struct_val_dma(const uint4* __restrict__ rec, uint64_t n,
-                                                                   uint4* __restrict__ roots) {
-    __shared__ uint4 buf[kStructThreads / 64][10][64];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    uint4(*B)[64] = buf[wv];
-    const uint64_t stride = (uint64_t)gridDim.x * kStructThreads;
-    auto prefetch = [&](uint64_t r) {
-        const uint4* u = rec + r * 10;
-#pragma unroll
-        for (int k = 0; k < 10; ++k)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(u + k),
-                                             (__attribute__((address_space(3))) void*)(&B[k][0]), 16, 0, 0);
-    };
-    // Keccak(le32(4*nw) || w[0..nw)) for nw = 12 (48 B) or 8 (32 B), one block
-    auto field = [&](int u0, int nunits) {
-        uint32_t w[12];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            if (k < nunits) {
-                const uint4 t = B[u0 + k][lane];
-                w[4 * k] = t.x;
-                w[4 * k + 1] = t.y;
-                w[4 * k + 2] = t.z;
-                w[4 * k + 3] = t.w;
-            }
-        }
-        const int nw = 4 * nunits;
-        State s;
-#pragma unroll
-        for (int q = 0; q < 34; ++q) {  // message dword q: 0 = le32(len), 1..nw = field, nw+1 = pad
-            uint32_t v = q == 0 ? (uint32_t)(4 * nw) : (q <= nw ? w[q - 1] : 0u);
-            if (q == nw + 1) v = 1u;
-            if (q & 1)
-                s.hi[q >> 1] = v;
-            else
-                s.lo[q >> 1] = v;
-        }
-#pragma unroll
-        for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
-        s.hi[16] ^= 0x80000000u;
-        keccak_f_digest(s);
-        return s;
-    };
-    auto put = [&](const State& s, int u) {  // the digest over units u, u+1 (their bytes are consumed)
-        B[u][lane] = make_uint4(s.lo[0], s.hi[0], s.lo[1], s.hi[1]);
-        B[u + 1][lane] = make_uint4(s.lo[2], s.hi[2], s.lo[3], s.hi[3]);
-    };
-    uint64_t i = (uint64_t)blockIdx.x * kStructThreads + threadIdx.x;
-    if (i < n) prefetch(i);
-#pragma unroll 1
-    for (; i < n; i += stride) {
-        put(field(0, 3), 1);  // Pubkey: units 0-2
-        put(field(3, 2), 3);  // WithdrawalCredentialsHash32: units 3-4
-        put(field(5, 2), 5);  // RandaoCommitmentHash32: units 5-6
-        State s;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {  // block 1: message dwords 0..31 = units 1..8
-            const uint4 t = B[1 + k][lane];
-            s.lo[2 * k] = t.x;
-            s.hi[2 * k] = t.y;
-            s.lo[2 * k + 1] = t.z;
-            s.hi[2 * k + 1] = t.w;
-        }
-        const uint4 t9 = B[9][lane];
-        s.lo[16] = t9.x;  // message dwords 32, 33
-        s.hi[16] = t9.y;
-#pragma unroll
-        for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the record's units are read: the slots are free
-        if (i + stride < n) prefetch(i + stride);
-        keccak_f(s);
-        s.lo[0] ^= t9.z;  // message dwords 34, 35 = block 2 bytes 0..7
-        s.hi[0] ^= t9.w;
-        s.lo[1] ^= 1u;  // domain pad at message byte 144 = block 2 byte 8
-        s.hi[16] ^= 0x80000000u;
-        keccak_f_digest(s);
-        uint4 d0, d1;
-        digest(s, d0, d1);
-        roots[2 * i] = d0;
-        roots[2 * i + 1] = d1;
-    }
-}
-
 // ----------------------------------------------------------------------------
 // n messages of msg_len bytes, msg_len % 8 == 0, 8-byte aligned: whole-word
 // loads only (deposit leaves: 280 B = 35 words = 3 blocks).
@@ -1956,93 +1741,6 @@ __global__ __launch_bounds__(kRecThreads, MK_REC_WAVES) void k_keccak_rec(const 
     }
 }
 template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
-
-// The same records with the blocks prefetched into LDS by DMA
-// (global_load_lds_dwordx4: no VGPRs held while a load is in flight), so
-// each block's load latency hides behind the previous permutation:
-// persistent grid-stride threads, and while record i's last two
-// permutations run, record i+stride's first block is already on its way.
-// A full 17-word block (136 B at an 8-B aligned address) is fetched as the
-// 9 aligned 16-B units that cover it (lane l's unit k lands at
-// buf[k][l]: conflict-free ds_read_b128) and the words are selected by the
-// record's 8-B phase.  A short last block (NW % 17 words, 1 for the 35-word
-// deposit) is one plain load issued early.  36 KB of LDS per 256-thread
-// workgroup.
-template <int NW>
-__global__ __launch_bounds__(kRecThreads) void k_keccak_rec_dma(const uint2* __restrict__ in, uint64_t n,
-                                                                uint4* __restrict__ out) {
-    static_assert(NW / 17 == 2 && NW % 17 > 0 && NW % 17 <= 2, "two full blocks and a short one");
-    constexpr int kTail = NW % 17;  // words of the short third block
-    __shared__ uint4 buf[kRecThreads / 64][9][64];
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    uint4(*B)[64] = buf[wv];
-    const uint64_t stride = (uint64_t)gridDim.x * kRecThreads;
-    auto prefetch = [&](uint64_t rec, int blk) {
-        const uintptr_t a = reinterpret_cast<uintptr_t>(in + rec * NW + 17 * blk);
-        const uint4* u = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
-#pragma unroll
-        for (int k = 0; k < 9; ++k)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(u + k),
-                                             (__attribute__((address_space(3))) void*)(&B[k][0]), 16, 0, 0);
-    };
-    // block words from the staged units: word w = unit (w + odd) / 2, half (w + odd) % 2
-    auto absorb = [&](State& s, uint32_t odd, bool first) {
-        const uint32_t msk = 0u - odd;
-        uint2 e[18];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const uint4 t = B[k][lane];
-            e[2 * k] = make_uint2(t.x, t.y);
-            e[2 * k + 1] = make_uint2(t.z, t.w);
-        }
-#pragma unroll
-        for (int w = 0; w < 17; ++w) {
-            const uint32_t lo = __builtin_amdgcn_bitop3_b32(e[w].x, e[w + 1].x, msk, 0xD8);
-            const uint32_t hi = __builtin_amdgcn_bitop3_b32(e[w].y, e[w + 1].y, msk, 0xD8);
-            if (first) {
-                s.lo[w] = lo;
-                s.hi[w] = hi;
-            } else {
-                s.lo[w] ^= lo;
-                s.hi[w] ^= hi;
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the next DMA reuses the slots
-    };
-    uint64_t i = (uint64_t)blockIdx.x * kRecThreads + threadIdx.x;
-    if (i < n) prefetch(i, 0);
-#pragma unroll 1
-    for (; i < n; i += stride) {
-        const uint2* p = in + i * NW;
-        const uint32_t odd0 = (uint32_t)((reinterpret_cast<uintptr_t>(p) >> 3) & 1u);
-        const uint32_t odd1 = (uint32_t)((reinterpret_cast<uintptr_t>(p + 17) >> 3) & 1u);
-        uint2 tail[kTail];
-#pragma unroll
-        for (int k = 0; k < kTail; ++k) tail[k] = p[34 + k];
-        State s;
-        absorb(s, odd0, true);
-#pragma unroll
-        for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
-        prefetch(i, 1);
-        keccak_f(s);
-        absorb(s, odd1, false);
-        if (i + stride < n) prefetch(i + stride, 0);
-        keccak_f(s);
-#pragma unroll
-        for (int k = 0; k < kTail; ++k) {
-            s.lo[k] ^= tail[k].x;
-            s.hi[k] ^= tail[k].y;
-        }
-        s.lo[kTail] ^= 1u;  // domain pad byte right after the message
-        s.hi[16] ^= 0x80000000u;
-        keccak_f_digest(s);
-        uint4 d0, d1;
-        digest(s, d0, d1);
-        out[2 * i] = d0;
-        out[2 * i + 1] = d1;
-    }
-}
-template __global__ void k_keccak_rec_dma<35>(const uint2*, uint64_t, uint4*);
 
 // ----------------------------------------------------------------------------
 // Deposit trie level: node j = K(in[2j] || (2j+1 < cin ? in[2j+1] : 0^32)),

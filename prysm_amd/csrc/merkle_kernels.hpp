@@ -41,14 +41,6 @@ template <int NB, int NRAW>
 __global__ void k_struct_reg(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
 template <int NB, int NRAW>
 __global__ void k_struct_split(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
-__global__ void k_struct_val_dma(const uint4* rec, uint64_t n, uint4* roots);
-#ifndef MK_STRUCT_DMA
-#define MK_STRUCT_DMA 0
-#endif
-#ifndef MK_STRUCT_DMA_GRID
-#define MK_STRUCT_DMA_GRID 1024
-#endif
-constexpr uint32_t kStructDmaGrid = MK_STRUCT_DMA_GRID;  // k_struct_val_dma: persistent grid
 #ifndef MK_STRUCT_SPLIT_MAX_N
 #define MK_STRUCT_SPLIT_MAX_N 32768
 #endif
@@ -65,15 +57,6 @@ __global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
 __global__ void k_keccak_words(const uint2* in, uint64_t n, uint32_t nwords, uint4* out);
 template <int NW>
 __global__ void k_keccak_rec(const uint2* in, uint64_t n, uint4* out);
-template <int NW>
-__global__ void k_keccak_rec_dma(const uint2* in, uint64_t n, uint4* out);
-#ifndef MK_REC_DMA
-#define MK_REC_DMA 0
-#endif
-#ifndef MK_REC_DMA_GRID
-#define MK_REC_DMA_GRID 1024
-#endif
-constexpr uint32_t kRecDmaGrid = MK_REC_DMA_GRID;  // k_keccak_rec_dma: persistent grid (resident workgroups)
 
 #ifndef MK_REC_THREADS
 #define MK_REC_THREADS 256
