@@ -114,7 +114,7 @@ struct SmallStage {
 struct DevCtx {
     std::mutex mu;  // host-buffer entry points: in/out/ws/aux and the big staging
     hipStream_t stream = nullptr;
-    DevBuf in, out, ws, aux, in2;
+    DevBuf in, out, ws, aux, dig;  // dig: element digests of the multi-shard TreeHash path
     // side stream + events: the ragged last workgroup of a pass runs
     // concurrently with the pass's full workgroups (fork/join on events)
     std::mutex side_mu;
@@ -538,6 +538,18 @@ int make_elem_plan(uint64_t n, uint32_t elem_len, bool aligned16, ElemPlan& e) {
     return MK_OK;
 }
 
+int launch_elem_digests(const void* d_elems, uint64_t n, uint32_t elem_len, void* d_dig, hipStream_t st) {
+    if (n == 0) return MK_OK;
+    if (elem_len == 32 && ((uintptr_t)d_elems % 16) == 0)
+        hipLaunchKernelGGL(mk::k_elem_digests<true>, dim3(ceil_div(n, 256)), dim3(256), 0, st,
+                           (const uint8_t*)d_elems, n, elem_len, (uint4*)d_dig);
+    else
+        hipLaunchKernelGGL(mk::k_elem_digests<false>, dim3(ceil_div(n, 256)), dim3(256), 0, st,
+                           (const uint8_t*)d_elems, n, elem_len, (uint4*)d_dig);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
 int dev_tree_hash_elems(const void* d_elems, uint64_t n, uint32_t elem_len, void* d_out32, void* d_ws,
                         uint64_t ws_bytes, hipStream_t st) {
     if (!d_out32 || (n && elem_len && !d_elems)) return fail(MK_EINVAL, "null pointer");
@@ -550,7 +562,6 @@ int dev_tree_hash_elems(const void* d_elems, uint64_t n, uint32_t elem_len, void
     if (e.fused) return launch_plan(e.p, (const uint8_t*)d_elems, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st);
     uint8_t* dig = (uint8_t*)d_ws;
     if (n) {
-        const uint32_t fast32 = (elem_len == 32 && ((uintptr_t)d_elems % 16) == 0) ? 1u : 0u;
         ProfRec rec{};
         const bool prof = prof_on();
         if (prof) {
@@ -558,13 +569,7 @@ int dev_tree_hash_elems(const void* d_elems, uint64_t n, uint32_t elem_len, void
             HIPCHK(hipEventCreate(&rec.b));
             HIPCHK(hipEventRecord(rec.a, st));
         }
-        if (fast32)
-            hipLaunchKernelGGL(mk::k_elem_digests<true>, dim3(ceil_div(n, 256)), dim3(256), 0, st,
-                               (const uint8_t*)d_elems, n, elem_len, (uint4*)dig);
-        else
-            hipLaunchKernelGGL(mk::k_elem_digests<false>, dim3(ceil_div(n, 256)), dim3(256), 0, st,
-                               (const uint8_t*)d_elems, n, elem_len, (uint4*)dig);
-        HIPCHK(hipGetLastError());
+        TRY(launch_elem_digests(d_elems, n, elem_len, dig, st));
         if (prof) {
             HIPCHK(hipEventRecord(rec.b, st));
             rec.perms = (double)n * (double)mk::perms_for_len((uint64_t)elem_len + 4);
@@ -576,7 +581,7 @@ int dev_tree_hash_elems(const void* d_elems, uint64_t n, uint32_t elem_len, void
     return launch_plan(e.p, dig, (uint8_t*)d_out32, dig + e.dig_bytes, ws_bytes - e.dig_bytes, st);
 }
 
-int host_tree_hash_elems(const uint8_t* elems, uint64_t n, uint32_t elem_len, uint8_t* out) {
+int host_tree_hash_elems_plain(const uint8_t* elems, uint64_t n, uint32_t elem_len, uint8_t* out) {
     if (!out || (n && elem_len && !elems)) return fail(MK_EINVAL, "null pointer");
     if (elem_len && n > (UINT64_MAX / 4) / elem_len) return fail(MK_EINVAL, "n * elem_len overflows");
     TRY(bind_call());
@@ -616,7 +621,8 @@ int host_merkle_hash_plain(const uint8_t* items, uint64_t n, uint32_t item_len, 
 }
 
 int host_merkle_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int nshards, const int* devs_in,
-                      uint8_t* out);
+                      uint8_t* out, uint32_t elem_len = 0);
+int host_tree_hash_elems_plain(const uint8_t* elems, uint64_t n, uint32_t elem_len, uint8_t* out);
 
 // merkleHash of a host buffer (the cgo TreeHash path).  A large buffer goes
 // through the sharded path with its shards on this one device: shard i+1
@@ -638,6 +644,24 @@ int host_merkle_hash(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_
         return host_merkle_multi(items, n, item_len, ns, devs.data(), out);
     }
     return host_merkle_hash_plain(items, n, item_len, out);
+}
+
+// TreeHash of a host list of byte strings (the cgo path): like
+// host_merkle_hash, a buffer of at least 2^MK_HOST_OVERLAP_MIN_LOG2 bytes goes
+// through the sharded path on its one device, so shard i+1's elements cross
+// PCIe while shard i is hashed (element digests, then the digest subtree).
+int host_tree_hash_elems(const uint8_t* elems, uint64_t n, uint32_t elem_len, uint8_t* out) {
+    if (!out || (n && elem_len && !elems)) return fail(MK_EINVAL, "null pointer");
+    if (elem_len && n > (UINT64_MAX / 4) / elem_len) return fail(MK_EINVAL, "n * elem_len overflows");
+    const uint64_t inb = n * (uint64_t)elem_len;
+    if (MK_HOST_OVERLAP_MIN_LOG2 < 64 && elem_len && inb >= (1ull << (MK_HOST_OVERLAP_MIN_LOG2 & 63))) {
+        TRY(bind_call());
+        const int d = t_bound;
+        const int ns = (int)std::min<uint64_t>(8, std::max<uint64_t>(2, inb >> 26));  // >= 64 MB per shard
+        std::vector<int> devs(ns, d);
+        return host_merkle_multi(elems, n, 32, ns, devs.data(), out, elem_len);
+    }
+    return host_tree_hash_elems_plain(elems, n, elem_len, out);
 }
 
 // ---- many lists ------------------------------------------------------------------------
@@ -1123,13 +1147,20 @@ struct MultiJob {
 // Worker of mk_ssz_merkle_hash_multi for one device: its shards are uploaded
 // into two alternating regions on the copy stream; each shard's passes run on
 // the compute stream once its upload landed, while the next shard uploads.
+// elem_len > 0 (the TreeHash-of-byte-strings path): `items` are elements of
+// elem_len bytes and the tree's 32-B items are their digests
+// K(le32(elem_len) || element); a shard's elements are uploaded, hashed into
+// the matching digest region (k_elem_digests) and reduced from there.
 int multi_device_worker(const MultiJob& job, const uint8_t* items, const std::vector<uint64_t>& begin,
-                        uint32_t item_len, uint32_t h, uint32_t k, size_t block) {
+                        uint32_t item_len, uint32_t h, uint32_t k, size_t block, uint32_t elem_len = 0) {
     TRY(bind_dev(job.dev));
     DevCtx* c = ctx();
-    const size_t region = (size_t)((1ull << h) * mk::chunk_bytes(item_len));
+    const size_t tree_region = (size_t)((1ull << h) * mk::chunk_bytes(item_len));  // tree items of a shard
+    const size_t per_shard_items = tree_region / item_len;
+    const size_t region = elem_len ? per_shard_items * elem_len : tree_region;     // uploaded bytes of a shard
     const int nreg = job.shards.size() > 1 ? 2 : 1;
-    TRY(grow(c->in, region * nreg));
+    TRY(grow(c->in, std::max<size_t>(region, 16) * nreg));
+    if (elem_len) TRY(grow(c->dig, tree_region * nreg));
     TRY(grow(c->out, block * (begin.size() - 1) + 32));
     Plan p;
     uint64_t wsb = 256;
@@ -1145,11 +1176,18 @@ int multi_device_worker(const MultiJob& job, const uint8_t* items, const std::ve
         const int r = (int)(i % 2);
         uint8_t* dreg = (uint8_t*)c->in.p + region * r;
         const uint64_t sn = begin[s + 1] - begin[s];
+        const uint32_t up_len = elem_len ? elem_len : item_len;
         if (c->region_used[r]) HIPCHK(hipStreamWaitEvent(c->copy, c->region_ev[r], 0));  // its last shard is done
-        TRY(staged_upload(c, dreg, items + begin[s] * item_len, sn * (size_t)item_len));
+        TRY(staged_upload(c, dreg, items + begin[s] * up_len, sn * (size_t)up_len));
         HIPCHK(hipEventRecord(c->h2d, c->copy));
         HIPCHK(hipStreamWaitEvent(c->stream, c->h2d, 0));
-        TRY(launch_shard(dreg, sn, item_len, h, k, (uint8_t*)c->out.p + block * s, c->ws, c->stream));
+        const uint8_t* tree_items = dreg;
+        if (elem_len) {
+            uint8_t* dg = (uint8_t*)c->dig.p + tree_region * r;
+            TRY(launch_elem_digests(dreg, sn, elem_len, dg, c->stream));
+            tree_items = dg;
+        }
+        TRY(launch_shard(tree_items, sn, item_len, h, k, (uint8_t*)c->out.p + block * s, c->ws, c->stream));
         HIPCHK(hipEventRecord(c->region_ev[r], c->stream));
         c->region_used[r] = true;
     }
@@ -1157,8 +1195,9 @@ int multi_device_worker(const MultiJob& job, const uint8_t* items, const std::ve
 }
 
 int host_merkle_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int nshards, const int* devs_in,
-                      uint8_t* out) {
+                      uint8_t* out, uint32_t elem_len) {
     if (nshards <= 0) return fail(MK_EINVAL, "nshards %d <= 0", nshards);
+    if (elem_len && item_len != 32) return fail(MK_EINVAL, "element digests are 32-B tree items");
     if (!out || (n && item_len && !items)) return fail(MK_EINVAL, "null pointer");
     const int nvis = probe_devices();
     if (nvis <= 0) return fail(MK_ENODEV, "no gfx950 device visible");
@@ -1175,7 +1214,8 @@ int host_merkle_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int n
         mk_call local{};
         local.device = devs[0];
         mk_call* prev = mk::swap_call(&local);
-        const int rc = host_merkle_hash_plain(items, n, item_len, out);
+        const int rc = elem_len ? host_tree_hash_elems_plain(items, n, elem_len, out)
+                                : host_merkle_hash_plain(items, n, item_len, out);
         mk::swap_call(prev);
         return rc ? fail(rc, "%s", local.err) : MK_OK;
     }
@@ -1212,7 +1252,7 @@ int host_merkle_multi(const uint8_t* items, uint64_t n, uint32_t item_len, int n
             mk_call local{};
             local.device = jobs[j].dev;
             mk::swap_call(&local);
-            rcs[j] = multi_device_worker(jobs[j], items, begin, item_len, h, k, block);
+            rcs[j] = multi_device_worker(jobs[j], items, begin, item_len, h, k, block, elem_len);
             if (rcs[j] == MK_OK && !one_each && hipStreamSynchronize(g_ctx[jobs[j].dev]->stream) != hipSuccess)
                 rcs[j] = fail(MK_EHIP, "hipStreamSynchronize failed on device %d", jobs[j].dev);
             errs[j] = local.err;

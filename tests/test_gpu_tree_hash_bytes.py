@@ -138,3 +138,17 @@ def test_tree_hash_2p28_golden(gpu):
     out = D.tree_hash_bytes_list(items, n, L)
     torch.cuda.synchronize()
     assert bytes(out.cpu().numpy()).hex() == g["root"]
+
+
+@pytest.mark.parametrize("n,L", [((1 << 23) + 5, 32), (6_291_459, 48), ((1 << 21) + 1, 133)])
+def test_tree_hash_host_overlap_path(gpu, n, L):
+    """A host list of at least 2^28 bytes (the cgo TreeHash path) is hashed
+    in shards on its one device: shard i+1's elements cross PCIe while shard
+    i's digests and subtree are computed (multi_device_worker with elem_len)."""
+    from oracle import oracle as O
+    from prysm_amd import ssz
+
+    assert n * L >= 1 << 28
+    items = O.splitmix_bytes(n * L, SEED + L + 0x100)
+    want = O.tree_hash_bytes_list(items, n, L, nthreads=16)
+    assert ssz.tree_hash_bytes_list(items, n, L) == want

@@ -16,6 +16,7 @@
 #                           for spaces (e.g. ab:--trie+--log2n+20:main+rec2)
 #   rankstep:LOG2N:WORLD    tools/rank_step_probe.py (one rank's pipelined step, 3 sets)
 #   rehearse8               tools/rehearse8.sh (8 gloo ranks sharing the GPU, golden root)
+#   e2e:LOG2N:MODE          tools/e2e_host.py (host-buffer call incl. PCIe; MODE "tree" or empty)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -55,6 +56,10 @@ for step in "$@"; do
     rehearse8)
       bash tools/rehearse8.sh > $O/rehearse8.log 2>&1 || { tail -20 $O/rehearse8.log; exit 1; }
       cp gpurun_out/rehearse8_summary.json $O/ && echo "rehearse8 ok" ;;
+    e2e)
+      timeout -k 10 300 python tools/e2e_host.py $a $b > $O/e2e_${a}_$b.json 2> $O/e2e_${a}_$b.err \
+        || { tail -5 $O/e2e_${a}_$b.err; exit 1; }
+      cat $O/e2e_${a}_$b.json ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
