@@ -378,26 +378,38 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                 HIPCHK(hipGetLastError());
                 if (c) HIPCHK(hipEventRecord(c->join, c->side));
             }
-            if (ps.nfast) {
+            uint64_t fast_base = 0;
+            if (ps.nlock && !a.elem_len) {  // phase-locked leaf workgroups first: 4 spans each, levels == 3
                 a.wg_base = 0;
+                if (MK_LOCK_STAGE)
+                    hipLaunchKernelGGL(mk::k_leaf_lock_st, dim3(std::min<uint64_t>(ps.nlock, MK_LOCK_GRID)),
+                                       dim3(mk::kLockThreads), 0, st, a, ps.nlock);
+                else
+                    hipLaunchKernelGGL(mk::k_leaf_lock, dim3(ps.nlock), dim3(mk::kLockThreads), 0, st, a);
+                HIPCHK(hipGetLastError());
+                fast_base = ps.nlock * 4;
+            }
+            if (ps.nfast > fast_base) {
+                a.wg_base = fast_base;
+                const uint64_t nfast = ps.nfast - fast_base;
                 // half-span tail (MK_HALF_TAIL): the last T full spans as 2T
                 // half-length workgroups at the end of the same grid
                 const uint64_t T = (MK_HALF_TAIL > 0 && mk::kLeafSplit && ps.leaf && !a.elem_len && ps.ni == 2 &&
-                                    ps.nfast >= 4ull * MK_HALF_TAIL && ps.nfast <= MK_HALF_TAIL_MAX)
+                                    !ps.nlock && nfast >= 4ull * MK_HALF_TAIL && nfast <= MK_HALF_TAIL_MAX)
                                        ? (uint64_t)MK_HALF_TAIL
                                        : 0;
                 if (T) {
-                    a.half_from = ps.nfast - T;
-                    hipLaunchKernelGGL((mk::k_reduce<true, true, 2>), dim3(ps.nfast + T), dim3(kReduceThreads), 0, st,
+                    a.half_from = nfast - T;
+                    hipLaunchKernelGGL((mk::k_reduce<true, true, 2>), dim3(nfast + T), dim3(kReduceThreads), 0, st,
                                        a);
                 } else if (ps.leaf && a.elem_len)
-                    hipLaunchKernelGGL((mk::k_reduce_elem<true>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+                    hipLaunchKernelGGL((mk::k_reduce_elem<true>), dim3(nfast), dim3(kReduceThreads), 0, st, a);
                 else if (ps.leaf && ps.ni == 1)
-                    hipLaunchKernelGGL((mk::k_reduce<true, true, 1>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+                    hipLaunchKernelGGL((mk::k_reduce<true, true, 1>), dim3(nfast), dim3(kReduceThreads), 0, st, a);
                 else if (ps.leaf)
-                    hipLaunchKernelGGL((mk::k_reduce<true, true, 2>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+                    hipLaunchKernelGGL((mk::k_reduce<true, true, 2>), dim3(nfast), dim3(kReduceThreads), 0, st, a);
                 else
-                    hipLaunchKernelGGL((mk::k_reduce<false, true, 2>), dim3(ps.nfast), dim3(kReduceThreads), 0, st, a);
+                    hipLaunchKernelGGL((mk::k_reduce<false, true, 2>), dim3(nfast), dim3(kReduceThreads), 0, st, a);
                 HIPCHK(hipGetLastError());
             }
             if (c) HIPCHK(hipStreamWaitEvent(st, c->join, 0));

@@ -168,6 +168,19 @@ __device__ __forceinline__ void arho_all(const State& a, uint32_t (&blo)[25], ui
     (arho<Is>(a, blo, bhi), ...);
 }
 
+// BAR (phase-locked rounds, k_leaf_lock): an s_barrier between rho and chi.
+// In a 1024-thread workgroup (4 waves per SIMD, all of one workgroup) it
+// starts every round's chi with the 4 waves of each SIMD on the same
+// instruction.  The round's two long full-rate runs (chi + the next
+// round's parity, 72; theta apply, 50) then issue in pairs across waves at
+// ~2.2 cycles per wave instruction, and the whole round at ~2.8 against 3.5-3.7
+// free running (tools/replay_probe.py, profiles/r03i: the compiled round's
+// exact text 56.2 vs 42.7 T ops/s).  The barrier's position is what matters:
+// after iota (the round's end) the same stream runs at 3.5, before rho at 4.45.
+#ifndef MK_LOCK_BARS
+#define MK_LOCK_BARS 1
+#endif
+template <bool BAR = false>
 __device__ __forceinline__ void round_asm(State& s, uint32_t rclo, uint32_t rchi) {
     uint32_t clo[5], chi_[5];
 #pragma unroll
@@ -183,6 +196,7 @@ __device__ __forceinline__ void round_asm(State& s, uint32_t rclo, uint32_t rchi
     uint32_t rlo[5], rhi[5];
 #pragma unroll
     for (int x = 0; x < 5; ++x) arot<1>(clo[x], chi_[x], rlo[x], rhi[x]);
+    if constexpr (BAR && MK_LOCK_BARS >= 2) __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int i = 0; i < 25; ++i) {
         const int x = i % 5;
@@ -191,6 +205,7 @@ __device__ __forceinline__ void round_asm(State& s, uint32_t rclo, uint32_t rchi
     }
     uint32_t blo[25], bhi[25];
     arho_all(s, blo, bhi, std::make_integer_sequence<int, 25>{});
+    if constexpr (BAR) __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int y = 0; y < 5; ++y) {
 #pragma unroll
@@ -319,6 +334,21 @@ __device__ __forceinline__ void keccak_f_digest(State& s) {
 #else
     keccak_f(s);
 #endif
+}
+
+// Phase-locked permutations (round_asm<true>): every wave of the workgroup
+// must run the same number of them -- each round holds an s_barrier.
+__device__ __forceinline__ void keccak_f_lock(State& s) {
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < 24; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+}
+__device__ __forceinline__ void keccak_f_digest_lock(State& s) {
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < 22; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    round_asm<true>(s, kRcLo[22], kRcHi[22]);
+    last_round_digest(s, kRcLo[23], kRcHi[23]);
+    asm volatile("" : "+v"(s.lo[0]), "+v"(s.hi[0]), "+v"(s.lo[1]), "+v"(s.hi[1]), "+v"(s.lo[2]), "+v"(s.hi[2]),
+                 "+v"(s.lo[3]), "+v"(s.hi[3]));
 }
 
 // ---- absorb helpers --------------------------------------------------------

@@ -175,6 +175,7 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
 #ifndef MK_LEAF_SPLIT_WAVES
 #define MK_LEAF_SPLIT_WAVES 5
 #endif
+template <bool BAR = false>
 __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w, uint4& d0, uint4& d1) {
     State s;
     uint4 v[9];
@@ -192,7 +193,10 @@ __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w
     const uint32_t t0 = v[8].z, t1 = v[8].w;
 #pragma unroll
     for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
-    keccak_f(s);
+    if constexpr (BAR)
+        keccak_f_lock(s);
+    else
+        keccak_f(s);
     asm volatile("" ::: "memory");  // block 2 loads stay after the permutation
     s.lo[0] ^= t0;
     s.hi[0] ^= t1;
@@ -222,7 +226,25 @@ __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w
     }
     s.lo[15] ^= 1u;  // byte 256 = byte 120 of block 1
     s.hi[16] ^= 0x80000000u;
-    keccak_f_digest(s);
+    if constexpr (BAR)
+        keccak_f_digest_lock(s);
+    else
+        keccak_f_digest(s);
+    digest(s, d0, d1);
+}
+
+// K(L || R) of two 32-B nodes with phase-locked rounds (k_leaf_lock).
+__device__ __forceinline__ void hash_node_lock(uint4 l0, uint4 l1, uint4 r0, uint4 r1, uint4& d0, uint4& d1) {
+    State s;
+    s.lo[0] = l0.x; s.hi[0] = l0.y; s.lo[1] = l0.z; s.hi[1] = l0.w;
+    s.lo[2] = l1.x; s.hi[2] = l1.y; s.lo[3] = l1.z; s.hi[3] = l1.w;
+    s.lo[4] = r0.x; s.hi[4] = r0.y; s.lo[5] = r0.z; s.hi[5] = r0.w;
+    s.lo[6] = r1.x; s.hi[6] = r1.y; s.lo[7] = r1.z; s.hi[7] = r1.w;
+#pragma unroll
+    for (int k = 8; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+    s.lo[8] = 1u;  // byte 64
+    s.hi[16] = 0x80000000u;
+    keccak_f_digest_lock(s);
     digest(s, d0, d1);
 }
 
@@ -425,6 +447,118 @@ k_reduce(ReduceArgs a) {
     __syncthreads();
 
     reduce_levels_out<NI>(a, lds, tid, lo1, c2, m2, pair);
+}
+
+// ----------------------------------------------------------------------------
+// Phase-locked leaf pass (MK_LEAF_LOCK): 1024 threads, one workgroup per CU,
+// so the 4 waves of each SIMD belong to one workgroup and the s_barrier in
+// every Keccak round (round_asm<true>, keccak_dev.hpp) keeps them on the same
+// instruction: the round issues at ~2.8 cycles per wave instruction instead of
+// the ~3.5 of free-running waves.  Every thread hashes 4
+// consecutive full windows, folds them in registers into one node three
+// levels above the chunks (4 x 2 + 2 + 1 = 11 permutations, all locked) and
+// writes it: workgroup g covers windows [4096 g, 4096 g + 4096) of the pass,
+// i.e. the spans of k_reduce workgroups 4g..4g+3 run with a.levels == 3, and
+// writes their output nodes [1024 g, 1024 g + 1024).  No LDS, no divergence:
+// every wave runs the same number of barriers (the host launches only full
+// workgroups of full windows).
+__global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock(ReduceArgs a) {
+    const uint64_t node = (uint64_t)blockIdx.x * kLockThreads + threadIdx.x;
+    const uint4* w = reinterpret_cast<const uint4*>(a.items) + node * 64;
+    uint4 l0, l1, r0, r1, p0, p1;
+    hash_window256_split<true>(w, l0, l1);
+    hash_window256_split<true>(w + 16, r0, r1);
+    hash_node_lock(l0, l1, r0, r1, p0, p1);
+    hash_window256_split<true>(w + 32, l0, l1);
+    hash_window256_split<true>(w + 48, r0, r1);
+    hash_node_lock(l0, l1, r0, r1, l0, l1);
+    hash_node_lock(p0, p1, l0, l1, r0, r1);
+    uint4* out = reinterpret_cast<uint4*>(a.out);
+    out[2 * node] = r0;
+    out[2 * node + 1] = r1;
+}
+
+// The same pass with the windows staged in LDS by DMA (global_load_lds_dwordx4,
+// no VGPRs held while a load is in flight) and a persistent grid: while a
+// window's first permutation runs, its block 2 is on its way into the wave's
+// LDS slots, and while its second runs, the next window's block 1.  A locked
+// workgroup has no other workgroup on its CU to cover a load wait, so every
+// wait not hidden this way stalls all 16 waves at once.  144 KB of LDS:
+// 9 x 1 KB per wave (lane l's 16-B unit k at B[k][l], conflict-free).
+__device__ __forceinline__ void lock_dma(uint4 (*B)[64], const uint4* src, int nk) {
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+        if (k < nk)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + k),
+                                             (__attribute__((address_space(3))) void*)(&B[k][0]), 16, 0, 0);
+}
+
+// Window w whose block 1 (w[0..8]) is in B (DMA issued earlier); issues the
+// DMA of `next`'s block 1 (when non-null) once block 2 has been read.
+__device__ __forceinline__ void hash_window_st(uint4 (*B)[64], uint32_t lane, const uint4* __restrict__ w,
+                                               const uint4* __restrict__ next, uint4& d0, uint4& d1) {
+    State s;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 1 has landed
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint4 v = B[k][lane];
+        s.lo[2 * k] = v.x;
+        s.hi[2 * k] = v.y;
+        s.lo[2 * k + 1] = v.z;
+        s.hi[2 * k + 1] = v.w;
+    }
+    const uint4 v8 = B[8][lane];
+    s.lo[16] = v8.x;
+    s.hi[16] = v8.y;
+#pragma unroll
+    for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots read: block 2 may overwrite them
+    lock_dma(B, w + 9, 7);
+    keccak_f_lock(s);
+    s.lo[0] ^= v8.z;
+    s.hi[0] ^= v8.w;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 2 has landed
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const uint4 u = B[k][lane];
+        s.lo[1 + 2 * k] ^= u.x;
+        s.hi[1 + 2 * k] ^= u.y;
+        s.lo[2 + 2 * k] ^= u.z;
+        s.hi[2 + 2 * k] ^= u.w;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (next) lock_dma(B, next, 9);
+    s.lo[15] ^= 1u;  // byte 256 = byte 120 of block 1
+    s.hi[16] ^= 0x80000000u;
+    keccak_f_digest_lock(s);
+    digest(s, d0, d1);
+}
+
+__global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock_st(ReduceArgs a, uint64_t ngroups) {
+    __shared__ uint4 buf[kLockThreads / 64][9][64];
+    const uint32_t lane = threadIdx.x & 63u;
+    uint4(*B)[64] = buf[threadIdx.x >> 6];
+    const uint4* items = reinterpret_cast<const uint4*>(a.items);
+    uint4* out = reinterpret_cast<uint4*>(a.out);
+    uint64_t g = blockIdx.x;
+    if (g < ngroups) lock_dma(B, items + (g * kLockThreads + threadIdx.x) * 64, 9);
+#pragma unroll 1
+    for (; g < ngroups; g += gridDim.x) {
+        const uint64_t node = g * kLockThreads + threadIdx.x;
+        const uint4* w = items + node * 64;
+        const uint64_t gn = g + gridDim.x;
+        const uint4* wn = gn < ngroups ? items + (gn * kLockThreads + threadIdx.x) * 64 : nullptr;
+        uint4 l0, l1, r0, r1, p0, p1;
+        hash_window_st(B, lane, w, w + 16, l0, l1);
+        hash_window_st(B, lane, w + 16, w + 32, r0, r1);
+        hash_node_lock(l0, l1, r0, r1, p0, p1);
+        hash_window_st(B, lane, w + 32, w + 48, l0, l1);
+        hash_window_st(B, lane, w + 48, wn, r0, r1);
+        hash_node_lock(l0, l1, r0, r1, l0, l1);
+        hash_node_lock(p0, p1, l0, l1, r0, r1);
+        out[2 * node] = r0;
+        out[2 * node + 1] = r1;
+    }
 }
 
 template __global__ void k_reduce<true, true, 2>(ReduceArgs);

@@ -30,6 +30,18 @@ struct StructSpec {                 // flat fixed-layout record (hash.go:141-159
 constexpr bool kLeafSplit = MK_LEAF_SPLIT != 0;
 template <bool LEAF, bool FAST, int NI>
 __global__ void k_reduce(ReduceArgs a);
+// Phase-locked leaf pass (merkle_kernels.hip): 4096 full windows per
+// workgroup -> 1024 nodes three levels above the chunks.
+constexpr uint32_t kLockThreads = 1024;
+constexpr uint64_t kLockWindows = 4 * kLockThreads;
+__global__ void k_leaf_lock(ReduceArgs a);
+__global__ void k_leaf_lock_st(ReduceArgs a, uint64_t ngroups);  // LDS-DMA staged, persistent (grid <= ngroups)
+#ifndef MK_LOCK_STAGE
+#define MK_LOCK_STAGE 1
+#endif
+#ifndef MK_LOCK_GRID
+#define MK_LOCK_GRID 256
+#endif
 template <bool FAST>
 __global__ void k_reduce_elem(ReduceArgs a);
 template <bool FAST32>

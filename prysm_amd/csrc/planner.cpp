@@ -89,6 +89,20 @@ constexpr uint32_t kW3MaxNt = MK_W3_MAX_NT < kMidThreads ? MK_W3_MAX_NT : kMidTh
 #endif
 constexpr uint64_t kSpreadLeafMaxC1 = MK_SPREAD_LEAF_MAX_LOG2 < 0 ? 0 : 1ull << MK_SPREAD_LEAF_MAX_LOG2;
 constexpr uint64_t kSpreadSpan = 16;  // windows per k_spread_leaf workgroup
+// Phase-locked leaf pass (k_leaf_lock, merkle_kernels.hip): wide leaf passes
+// of full 256-B windows fold 3 levels (windows -> node pairs -> one node per
+// 4 windows) in 1024-thread workgroups whose Keccak rounds hold an s_barrier;
+// the next (node) pass takes the levels the leaf pass used to fuse in LDS.
+#ifndef MK_LEAF_LOCK
+#define MK_LEAF_LOCK 0
+#endif
+constexpr bool kLeafLock = MK_LEAF_LOCK != 0;
+#ifndef MK_LEAF_LOCK_MIN_LOG2
+#define MK_LEAF_LOCK_MIN_LOG2 20
+#endif
+constexpr uint64_t kLeafLockMinC1 = 1ull << MK_LEAF_LOCK_MIN_LOG2;  // windows (first-level nodes)
+constexpr uint32_t kLockLevels = 3;
+constexpr uint64_t kLockSpans = 4;  // k_reduce spans (1024 windows) per k_leaf_lock workgroup
 
 uint32_t ilog2(uint64_t v) {
     uint32_t l = 0;
@@ -194,6 +208,10 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         const uint32_t max_lv = sp ? 1 + ilog2(kSpreadSpan)
                               : w3 ? 1 + ilog2(nt / 2) : wave ? kWave2Levels : kMaxPassLevels;
         uint32_t lv = final_pass ? remaining : std::min<uint32_t>(max_lv, remaining);
+        const bool lock = kLeafLock && leaf && !wave && !final_pass && !leaf_ni1 && ni == 2 &&
+                          a.c1_full >= kLeafLockMinC1 && remaining > kLockLevels &&
+                          a.c1_full / span >= kLockSpans;
+        if (lock) lv = kLockLevels;
         for (uint32_t l = 1; l < lv; ++l) {  // fused levels above the first
             if (c <= 1 && !pad_at_one) break;
             perms += (double)(c / 2) + (c % 2 ? 2.0 : 0.0);
@@ -212,6 +230,7 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         ps.nwg = ceil_div(c1, span);
         ps.nfast = wave ? 0 : std::min<uint64_t>(ps.nwg, a.c1_full / span);
         ps.ni = ni;
+        ps.nlock = lock ? ps.nfast / kLockSpans : 0;
         ps.in_ws = in_slot;
         if (final_pass) {
             if (!subtree) {

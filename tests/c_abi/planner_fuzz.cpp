@@ -27,6 +27,8 @@ using namespace mk;
 
 // Replays a plan's node counts: pass p turns cin into c1 = ceil(cin/2)
 // (1 when cin == 1 and no pad_at_one), then `levels - 1` more halvings.
+static uint64_t g_lock_passes = 0;
+
 static uint64_t replay(const Plan& p, uint64_t nchunks, bool pad) {
     uint64_t c = nchunks;
     for (size_t i = 0; i < p.passes.size(); ++i) {
@@ -42,6 +44,11 @@ static uint64_t replay(const Plan& p, uint64_t nchunks, bool pad) {
             c = ceil_div(c, 2);
         }
         if (ps.out_ws >= 0) REQUIRE(p.slot_nodes[ps.out_ws] >= c);
+        if (ps.nlock) {  // k_leaf_lock: whole groups of 4 full spans, exactly 3 levels, never the final pass
+            ++g_lock_passes;
+            REQUIRE(ps.leaf && !ps.wave && !ps.sp && ps.ni == 2 && !ps.a.finalize && ps.a.levels == 3);
+            REQUIRE(4 * ps.nlock <= ps.nfast && ps.nfast * 2 * ps.ni * kReduceThreads <= ps.a.c1_full);
+        }
         REQUIRE(ps.nfast <= ps.nwg);
         REQUIRE(ps.nwg >= 1);
     }
@@ -157,6 +164,7 @@ int main(int argc, char** argv) {
     uint32_t h, ne;
     uint64_t b[2];
     REQUIRE(shard_plan(5, 32, 0, &h, &ne, b) == MK_EINVAL);
-    std::fprintf(stderr, "planner fuzz: %d cases clean\n", cases);
+    std::fprintf(stderr, "planner fuzz: %d cases clean (%llu phase-locked leaf passes)\n", cases,
+                 (unsigned long long)g_lock_passes);
     return 0;
 }

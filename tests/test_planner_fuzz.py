@@ -14,12 +14,15 @@ from tests.test_distributed import _plan_cpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.fixture(scope="module")
-def fuzz_exe(tmp_path_factory):
-    out = str(tmp_path_factory.mktemp("fuzz") / "planner_fuzz")
+# the default build, and one with the phase-locked leaf pass (k_leaf_lock)
+# enabled down to 2^12 windows so the fuzz sizes reach it
+@pytest.fixture(scope="module", params=[(), ("-DMK_LEAF_LOCK=1", "-DMK_LEAF_LOCK_MIN_LOG2=12")],
+                ids=["default", "leaf_lock"])
+def fuzz_exe(tmp_path_factory, request):
+    out = str(tmp_path_factory.mktemp("fuzz") / ("planner_fuzz_" + ("leaf_lock" if request.param else "default")))
     csrc = os.path.join(ROOT, "prysm_amd", "csrc")
     subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
-                    "-fno-omit-frame-pointer", "-I" + csrc, "-I" + os.path.join(ROOT, "include"),
+                    "-fno-omit-frame-pointer", *request.param, "-I" + csrc, "-I" + os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "c_abi", "planner_fuzz.cpp"), os.path.join(csrc, "planner.cpp"),
                     "-o", out], check=True)
     return out
@@ -31,6 +34,8 @@ def test_planner_fuzz_sanitized(fuzz_exe, seed):
     r = subprocess.run([fuzz_exe, str(seed), "400"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     assert "cases clean" in r.stderr
+    if "leaf_lock" in fuzz_exe:
+        assert " 0 phase-locked" not in r.stderr, r.stderr[-300:]
     nshard = nfront = 0
     for line in r.stdout.splitlines():
         f = line.split()
