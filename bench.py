@@ -79,23 +79,38 @@ def cpu_baseline(item_len: int, log2n_sample: int, threads: int = 1):
                       f"(same SplitMix64 stream), {threads} thread{'s' if threads > 1 else ''}, {dt:.1f} s"}
 
 
-def load_pmc():
+def leaf_kernel():
+    """(kernel-name substring, description) of the C4 leaf pass this library
+    build runs (mk_version carries the compile-time knobs)."""
+    from prysm_amd import _lib
+
+    v = _lib.load().mk_version().decode()
+    if "leaf_lock=1" in v:
+        return ("k_leaf_lock_sc" if "lock_stage=2" in v else "k_leaf_lock",
+                "k_leaf_lock_sc (phase-locked leaf pass: 1024-thread workgroups, s_barrier in every Keccak round; "
+                "4 windows -> 1 node per thread, 3 levels; coalesced LDS-DMA staging)")
+    return "k_reduce<true, true, 2>", "k_reduce<LEAF, FAST, 2> (leaf pass: 256-B windows + 4 fused levels)"
+
+
+def load_pmc(kernel):
     """HBM bytes per leaf-kernel launch and the effective clock under that
-    load from the newest committed rocprofv3 PMC summary (profiles/*_pmc.json,
-    tools/pmc_summary.py), with the file they come from.  These are NOT
-    measured by this run (PMC counters need their own rocprofv3 pass)."""
+    load from the newest committed rocprofv3 PMC summary of this leaf kernel
+    (profiles/*_pmc.json, tools/pmc_summary.py), with the file they come
+    from.  These are NOT measured by this run (PMC counters need their own
+    rocprofv3 pass)."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
-    if not files:
-        return None, None, None
-    try:
-        with open(files[-1]) as f:
-            d = json.load(f)
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except Exception:
+            continue
+        if d.get("kernel", "k_reduce<true, true, 2>") != kernel:
+            continue
         return (d.get("hbm_bytes_per_leaf_launch"), d.get("effective_clock_GHz"),
-                os.path.relpath(files[-1], ROOT) + f" ({d.get('box', 'builder lease')}, not this run)")
-    except Exception:
-        return None, None, None
+                os.path.relpath(path, ROOT) + f" ({d.get('box', 'builder lease')}, not this run)")
+    return None, None, None
 
 
 class ClockSampler:
@@ -440,7 +455,8 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
         hashes_per_launch = leaf_hashes / max(leaf_launches, 1)
         ops_per_launch = perms_per_launch * INT_OPS_PER_PERM - hashes_per_launch * INT_OPS_SAVED_PER_HASH
         achieved = ops_per_launch / avg_leaf_s if avg_leaf_s > 0 else 0.0
-        traffic, clk, pmc_src = load_pmc() if world == 1 and args.log2n == 28 else (None, None, None)
+        kname, kdesc = leaf_kernel()
+        traffic, clk, pmc_src = load_pmc(kname) if world == 1 and args.log2n == 28 else (None, None, None)
         out = {
             "metric": "tree-hash leaves/sec @2^28 chunks (ssz.merkleHash, 32-B leaves)",
             "value": value,
@@ -464,7 +480,7 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
                        "per_rank_ms_per_step_and_leaf_ms": per_rank},
             "roofline": {
                 "bound": "valu-int",
-                "kernel": "k_reduce<LEAF, FAST, 2> (leaf pass: 256-B windows + 4 fused levels)",
+                "kernel": kdesc,
                 "achieved": achieved / 1e12,
                 "peak": PEAK_INT_OPS / 1e12,
                 "unit": "Tops/s (int32 VALU)",

@@ -381,11 +381,13 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
             uint64_t fast_base = 0;
             if (ps.nlock && !a.elem_len) {  // phase-locked leaf workgroups first: 4 spans each, levels == 3
                 a.wg_base = 0;
-                if (MK_LOCK_STAGE)
-                    hipLaunchKernelGGL(mk::k_leaf_lock_st, dim3(std::min<uint64_t>(ps.nlock, MK_LOCK_GRID)),
+                // persistent grid (one 1024-thread workgroup per CU); k_leaf_lock (MK_LOCK_STAGE=0)
+                // takes one group per workgroup
+                if (MK_LOCK_STAGE == 2)
+                    hipLaunchKernelGGL(mk::k_leaf_lock_sc, dim3(std::min<uint64_t>(ps.nlock, MK_LOCK_GRID)),
                                        dim3(mk::kLockThreads), 0, st, a, ps.nlock);
                 else
-                    hipLaunchKernelGGL(mk::k_leaf_lock, dim3(ps.nlock), dim3(mk::kLockThreads), 0, st, a);
+                    hipLaunchKernelGGL(mk::k_leaf_lock, dim3(ps.nlock), dim3(mk::kLockThreads), 0, st, a, ps.nlock);
                 HIPCHK(hipGetLastError());
                 fast_base = ps.nlock * 4;
             }
@@ -1393,7 +1395,12 @@ struct mk_trie {
 // =============================================================================
 extern "C" {
 
-const char* mk_version(void) { return "prysm_merkle 0.2 (gfx950)"; }
+#define MK_STR2(x) #x
+#define MK_STR(x) MK_STR2(x)
+const char* mk_version(void) {
+    return "prysm_merkle 0.3 (gfx950; leaf_lock=" MK_STR(MK_LEAF_LOCK) " lock_stage=" MK_STR(MK_LOCK_STAGE)
+           " lock_bars=" MK_STR(MK_LOCK_BARS) ")";
+}
 
 const char* mk_strerror(int code) {
     switch (code) {

@@ -178,7 +178,7 @@ __device__ __forceinline__ void arho_all(const State& a, uint32_t (&blo)[25], ui
 // exact text 56.2 vs 42.7 T ops/s).  The barrier's position is what matters:
 // after iota (the round's end) the same stream runs at 3.5, before rho at 4.45.
 #ifndef MK_LOCK_BARS
-#define MK_LOCK_BARS 1
+#define MK_LOCK_BARS 2  // 1: before chi; 2: also before theta apply (57.2 vs 51.9 T register-resident)
 #endif
 template <bool BAR = false>
 __device__ __forceinline__ void round_asm(State& s, uint32_t rclo, uint32_t rchi) {

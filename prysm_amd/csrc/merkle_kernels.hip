@@ -461,10 +461,15 @@ k_reduce(ReduceArgs a) {
 // i.e. the spans of k_reduce workgroups 4g..4g+3 run with a.levels == 3, and
 // writes their output nodes [1024 g, 1024 g + 1024).  No LDS, no divergence:
 // every wave runs the same number of barriers (the host launches only full
-// workgroups of full windows).
-__global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock(ReduceArgs a) {
-    const uint64_t node = (uint64_t)blockIdx.x * kLockThreads + threadIdx.x;
-    const uint4* w = reinterpret_cast<const uint4*>(a.items) + node * 64;
+// workgroups of full windows).  This direct-load form (MK_LOCK_STAGE=0) is
+// kept as the A/B reference of the staged default k_leaf_lock_sc below:
+// 2^28 leaf pass 8.54 vs 8.25 ms in one process (profiles/r03i/ab_lock4_28.jsonl).
+#ifndef MK_LOCK_NOLOAD
+#define MK_LOCK_NOLOAD 0  // probe only: windows read from a 16 MB wrap of the input (wrong roots)
+#endif
+__device__ __forceinline__ uint64_t lock_src(uint64_t node) { return MK_LOCK_NOLOAD ? (node & 0x3FFFull) : node; }
+__device__ __forceinline__ void leaf_lock_group(const ReduceArgs& a, uint64_t node) {
+    const uint4* w = reinterpret_cast<const uint4*>(a.items) + lock_src(node) * 64;
     uint4 l0, l1, r0, r1, p0, p1;
     hash_window256_split<true>(w, l0, l1);
     hash_window256_split<true>(w + 16, r0, r1);
@@ -477,85 +482,105 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock(ReduceArgs a) {
     out[2 * node] = r0;
     out[2 * node + 1] = r1;
 }
-
-// The same pass with the windows staged in LDS by DMA (global_load_lds_dwordx4,
-// no VGPRs held while a load is in flight) and a persistent grid: while a
-// window's first permutation runs, its block 2 is on its way into the wave's
-// LDS slots, and while its second runs, the next window's block 1.  A locked
-// workgroup has no other workgroup on its CU to cover a load wait, so every
-// wait not hidden this way stalls all 16 waves at once.  144 KB of LDS:
-// 9 x 1 KB per wave (lane l's 16-B unit k at B[k][l], conflict-free).
-__device__ __forceinline__ void lock_dma(uint4 (*B)[64], const uint4* src, int nk) {
-#pragma unroll
-    for (int k = 0; k < 9; ++k)
-        if (k < nk)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + k),
-                                             (__attribute__((address_space(3))) void*)(&B[k][0]), 16, 0, 0);
+// grid = ngroups (one group of 1024 nodes per workgroup), or fewer workgroups
+// looping over the groups (persistent)
+__global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock(ReduceArgs a, uint64_t ngroups) {
+#pragma unroll 1
+    for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) leaf_lock_group(a, g * kLockThreads + threadIdx.x);
 }
 
-// Window w whose block 1 (w[0..8]) is in B (DMA issued earlier); issues the
-// DMA of `next`'s block 1 (when non-null) once block 2 has been read.
-__device__ __forceinline__ void hash_window_st(uint4 (*B)[64], uint32_t lane, const uint4* __restrict__ w,
-                                               const uint4* __restrict__ next, uint4& d0, uint4& d1) {
+// The default form (MK_LOCK_STAGE=2): the windows staged in LDS by COALESCED
+// DMA (global_load_lds_dwordx4: no VGPRs held while a load is in flight) on a
+// persistent grid.  In k_leaf_lock every wave waits for its window loads,
+// and a locked workgroup has no other workgroup on its CU to cover the wait;
+// its per-lane 16-B loads of lanes 1 KB apart also touch 64 lines per
+// instruction and every line 8 times.  Here phase A of window j (units
+// 0..8 = block 1) lands in the wave's 9 KB of LDS during the previous
+// window's second permutation and phase B (units 9..15) during this window's
+// first, and the 576 (phase A: units
+// 0..8) or 448 (phase B: units 9..15) 16-B units of the step are flattened
+// window-major (U = 9 m + u or 7 m + u - 9), so consecutive lanes of a DMA
+// instruction read consecutive units of one window (~15 lines per
+// instruction, each line once), and the LDS image is that flat order: lane m
+// reads its unit u at row 9 m + u (or 7 m + u - 9) -- an odd stride, so the
+// 16-B reads of any 16 consecutive lanes hit distinct bank quads.
+template <int NU, int U0>
+__device__ __forceinline__ void lock_dma_c(uint4* Bw, const uint4* __restrict__ Rj, uint32_t lane) {
+    // launder the lane index so the per-lane offsets are recomputed here (a
+    // few VALU per DMA) instead of being hoisted and held in 16+ VGPRs
+    asm volatile("" : "+v"(lane));
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        const uint32_t U = 64u * i + lane;
+        const uint32_t m = U / NU, u = U - m * NU;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Rj + m * 64 + U0 + u),
+                                         (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void hash_window_sc(uint4* Bw, uint32_t lane, const uint4* __restrict__ Rj,
+                                               const uint4* __restrict__ Rnext, uint4& d0, uint4& d1) {
     State s;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 1 has landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phase A has landed
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        const uint4 v = B[k][lane];
+        const uint4 v = Bw[9 * lane + k];
         s.lo[2 * k] = v.x;
         s.hi[2 * k] = v.y;
         s.lo[2 * k + 1] = v.z;
         s.hi[2 * k + 1] = v.w;
     }
-    const uint4 v8 = B[8][lane];
+    const uint4 v8 = Bw[9 * lane + 8];
     s.lo[16] = v8.x;
     s.hi[16] = v8.y;
 #pragma unroll
     for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slots read: block 2 may overwrite them
-    lock_dma(B, w + 9, 7);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: phase B may overwrite them
+    lock_dma_c<7, 9>(Bw, Rj, lane);
     keccak_f_lock(s);
     s.lo[0] ^= v8.z;
     s.hi[0] ^= v8.w;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 2 has landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phase B has landed
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-        const uint4 u = B[k][lane];
+        const uint4 u = Bw[7 * lane + k];
         s.lo[1 + 2 * k] ^= u.x;
         s.hi[1 + 2 * k] ^= u.y;
         s.lo[2 + 2 * k] ^= u.z;
         s.hi[2 + 2 * k] ^= u.w;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (next) lock_dma(B, next, 9);
-    s.lo[15] ^= 1u;  // byte 256 = byte 120 of block 1
+    if (Rnext) lock_dma_c<9, 0>(Bw, Rnext, lane);
+    s.lo[15] ^= 1u;
     s.hi[16] ^= 0x80000000u;
     keccak_f_digest_lock(s);
     digest(s, d0, d1);
 }
 
-__global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock_st(ReduceArgs a, uint64_t ngroups) {
-    __shared__ uint4 buf[kLockThreads / 64][9][64];
-    const uint32_t lane = threadIdx.x & 63u;
-    uint4(*B)[64] = buf[threadIdx.x >> 6];
+__global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock_sc(ReduceArgs a, uint64_t ngroups) {
+    __shared__ uint4 buf[kLockThreads / 64][9 * 64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint4* Bw = buf[wave];
     const uint4* items = reinterpret_cast<const uint4*>(a.items);
     uint4* out = reinterpret_cast<uint4*>(a.out);
+    // the wave's 64 nodes = 256 consecutive windows (64 KB); lane m's windows at m * 64 uint4
+    auto region = [&](uint64_t g) { return items + lock_src(g * kLockThreads + 64 * wave) * 64; };
     uint64_t g = blockIdx.x;
-    if (g < ngroups) lock_dma(B, items + (g * kLockThreads + threadIdx.x) * 64, 9);
+    if (g < ngroups) lock_dma_c<9, 0>(Bw, region(g), lane);
 #pragma unroll 1
     for (; g < ngroups; g += gridDim.x) {
-        const uint64_t node = g * kLockThreads + threadIdx.x;
-        const uint4* w = items + node * 64;
+        const uint4* R = region(g);
         const uint64_t gn = g + gridDim.x;
-        const uint4* wn = gn < ngroups ? items + (gn * kLockThreads + threadIdx.x) * 64 : nullptr;
+        const uint4* Rn = gn < ngroups ? region(gn) : nullptr;
         uint4 l0, l1, r0, r1, p0, p1;
-        hash_window_st(B, lane, w, w + 16, l0, l1);
-        hash_window_st(B, lane, w + 16, w + 32, r0, r1);
+        hash_window_sc(Bw, lane, R, R + 16, l0, l1);
+        hash_window_sc(Bw, lane, R + 16, R + 32, r0, r1);
         hash_node_lock(l0, l1, r0, r1, p0, p1);
-        hash_window_st(B, lane, w + 32, w + 48, l0, l1);
-        hash_window_st(B, lane, w + 48, wn, r0, r1);
+        hash_window_sc(Bw, lane, R + 32, R + 48, l0, l1);
+        hash_window_sc(Bw, lane, R + 48, Rn, r0, r1);
         hash_node_lock(l0, l1, r0, r1, l0, l1);
         hash_node_lock(p0, p1, l0, l1, r0, r1);
+        const uint64_t node = g * kLockThreads + threadIdx.x;
         out[2 * node] = r0;
         out[2 * node + 1] = r1;
     }

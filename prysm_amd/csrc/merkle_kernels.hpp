@@ -34,10 +34,10 @@ __global__ void k_reduce(ReduceArgs a);
 // workgroup -> 1024 nodes three levels above the chunks.
 constexpr uint32_t kLockThreads = 1024;
 constexpr uint64_t kLockWindows = 4 * kLockThreads;
-__global__ void k_leaf_lock(ReduceArgs a);
-__global__ void k_leaf_lock_st(ReduceArgs a, uint64_t ngroups);  // LDS-DMA staged, persistent (grid <= ngroups)
+__global__ void k_leaf_lock(ReduceArgs a, uint64_t ngroups);
+__global__ void k_leaf_lock_sc(ReduceArgs a, uint64_t ngroups);  // coalesced LDS-DMA staging, persistent grid
 #ifndef MK_LOCK_STAGE
-#define MK_LOCK_STAGE 1
+#define MK_LOCK_STAGE 2  // 0: k_leaf_lock (direct per-lane loads), 2: k_leaf_lock_sc (coalesced LDS-DMA)
 #endif
 #ifndef MK_LOCK_GRID
 #define MK_LOCK_GRID 256

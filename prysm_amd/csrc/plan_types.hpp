@@ -14,6 +14,14 @@ constexpr uint32_t kWaveThreads = 64;                // k_wave2: one wave per wo
 constexpr uint32_t kWave2Span = kWaveThreads / 2;    // two lanes per state: 32 nodes per wave
 constexpr uint32_t kWave2Levels = 6;                 // first level + 5 in-wave levels (32 -> 1)
 constexpr uint32_t kMidThreads = 1024;               // largest k_wave3: 16 waves, 512 lane pairs, 10 levels
+// Wide leaf passes of full windows run the phase-locked k_leaf_lock_sc
+// (merkle_kernels.hip, planner.cpp) instead of k_reduce's fused form.
+#ifndef MK_LEAF_LOCK
+#define MK_LEAF_LOCK 1
+#endif
+#ifndef MK_LOCK_BARS
+#define MK_LOCK_BARS 2  // s_barriers per locked Keccak round (keccak_dev.hpp round_asm)
+#endif
 
 struct ReduceArgs {
     const uint8_t* items;  // LEAF: item bytes; NODE: 32-B input nodes

@@ -93,10 +93,7 @@ constexpr uint64_t kSpreadSpan = 16;  // windows per k_spread_leaf workgroup
 // of full 256-B windows fold 3 levels (windows -> node pairs -> one node per
 // 4 windows) in 1024-thread workgroups whose Keccak rounds hold an s_barrier;
 // the next (node) pass takes the levels the leaf pass used to fuse in LDS.
-#ifndef MK_LEAF_LOCK
-#define MK_LEAF_LOCK 0
-#endif
-constexpr bool kLeafLock = MK_LEAF_LOCK != 0;
+constexpr bool kLeafLock = MK_LEAF_LOCK != 0;  // plan_types.hpp
 #ifndef MK_LEAF_LOCK_MIN_LOG2
 #define MK_LEAF_LOCK_MIN_LOG2 20
 #endif

@@ -83,9 +83,12 @@ def test_shard_plan_properties(lib, n, item_len, world):
 def test_workspace_sizing(lib):
     assert lib.mk_ssz_merkle_workspace_bytes(0, 32) >= 32
     ws = lib.mk_ssz_merkle_workspace_bytes(1 << 28, 32)
-    # pass outputs: 2^21 + 2^16 nodes of 32 B
-    assert ws >= 32 * ((1 << 21) + (1 << 16))
-    assert ws < 80 << 20
+    if b"leaf_lock=1" in lib.mk_version():
+        # phase-locked leaf pass (3 levels): pass outputs 2^23 + 2^18 nodes of 32 B
+        assert 32 * ((1 << 23) + (1 << 18)) <= ws < 300 << 20
+    else:
+        # fused leaf pass (5 levels): pass outputs 2^21 + 2^16 nodes of 32 B
+        assert 32 * ((1 << 21) + (1 << 16)) <= ws < 80 << 20
     assert lib.mk_ssz_merkle_workspace_bytes(10, 0) == 0  # item_len 0 is invalid
     assert lib.mk_deposit_trie_levels_bytes(0, 32) == 0
     assert lib.mk_deposit_trie_levels_bytes(5, 2) == 32 * (5 + 3 + 2)

@@ -130,6 +130,10 @@ __global__ __launch_bounds__(NT) void k_perm(uint32_t* out, int iters) {
     }
 #pragma unroll 1
     for (int k = 0; k < iters; ++k) {
+        if constexpr (ASM == 9) {  // the phase-locked permutation of k_leaf_lock (round_asm<true>)
+            mk::keccak_f_lock(s);
+            continue;
+        }
 #pragma unroll 2
         for (int r = 0; r < 24; ++r) {
             if constexpr (ASM == 1)
@@ -198,6 +202,11 @@ int main() {
     run<256, 1, 0>("asm_free_again", 1024, it, out, ref);
     run<256, 2, 0>("asm_rowwise_free_again", 1024, it, out, ref);
     run<256, 3, 0>("asm_rotchi_rows_free_again", 1024, it, out, ref);
+    if (getenv("PROBE_KLOCK")) {  // keccak_f_lock as compiled (MK_LOCK_BARS, MK_ROUND_UNROLL)
+        run<1024, 9, 0>("keccak_f_lock_wg1024", 256, it, out, ref);
+        run<256, 0, 0>("compiled_free", 1024, it, out, ref);
+        run<1024, 9, 0>("keccak_f_lock_wg1024_again", 256, it, out, ref);
+    }
     if (getenv("PROBE_LOCK")) {
         run<1024, 0, 1>("compiled_lock1", 256, it, out, ref);
         run<1024, 1, 1>("asm_lock1", 256, it, out, ref);

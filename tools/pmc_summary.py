@@ -25,7 +25,7 @@ def counters(d):
 def main(d):
     import socket
 
-    res = {"dir": d, "box": f"GPU box {socket.gethostname()}"}
+    res = {"dir": d, "box": f"GPU box {socket.gethostname()}", "kernel": LEAF}
     stats = glob.glob(os.path.join(d, "stats", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         res["kernel_stats"] = [
