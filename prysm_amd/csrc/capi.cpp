@@ -433,18 +433,35 @@ int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, 
     if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
     if (!d_out || (!d_in && msg_len)) return fail(MK_EINVAL, "null pointer");
     const uint64_t grid = ceil_div(n, 256);
-    if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0)
-        hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
-    else if (kRecKernel && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0)
-        hipLaunchKernelGGL((mk::k_keccak_rec<35>),
-                           dim3(std::min<uint64_t>(ceil_div(n, mk::kRecThreads), mk::kRecGridMax)),
-                           dim3(mk::kRecThreads), 0, st, (const uint2*)d_in, n, (uint4*)d_out);
-    else if (msg_len % 8 == 0 && msg_len > 0 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0)
+    if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0) {
+        // phase-locked whole groups of 1024 messages first, the rest one per thread
+        const uint64_t ng = (MK_K64_LOCK && n >= (1u << 18)) ? n / mk::kLockThreads : 0;
+        if (ng)
+            hipLaunchKernelGGL(mk::k_keccak64_lock, dim3(std::min<uint64_t>(ng, MK_LOCK_GRID)), dim3(mk::kLockThreads),
+                               0, st, (const uint4*)d_in, ng, (uint4*)d_out);
+        const uint64_t done = ng * mk::kLockThreads, rest = n - done;
+        if (rest)
+            hipLaunchKernelGGL(mk::k_keccak64, dim3(ceil_div(rest, 256)), dim3(256), 0, st,
+                               (const uint4*)d_in + 4 * done, rest, (uint4*)d_out + 2 * done);
+    } else if (kRecKernel && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0) {
+        // phase-locked records first (whole groups of 1024), the rest grid-stride
+        const uint64_t ng = (MK_REC_LOCK && n >= MK_REC_LOCK_MIN) ? n / mk::kLockThreads : 0;
+        if (ng)
+            hipLaunchKernelGGL((mk::k_keccak_rec_lock<35>), dim3(std::min<uint64_t>(ng, MK_LOCK_GRID)),
+                               dim3(mk::kLockThreads), 0, st, (const uint2*)d_in, ng, (uint4*)d_out);
+        const uint64_t done = ng * mk::kLockThreads, rest = n - done;
+        if (rest)
+            hipLaunchKernelGGL((mk::k_keccak_rec<35>),
+                               dim3(std::min<uint64_t>(ceil_div(rest, mk::kRecThreads), mk::kRecGridMax)),
+                               dim3(mk::kRecThreads), 0, st, (const uint2*)d_in + done * 35, rest,
+                               (uint4*)d_out + 2 * done);
+    } else if (msg_len % 8 == 0 && msg_len > 0 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0) {
         hipLaunchKernelGGL(mk::k_keccak_words, dim3(grid), dim3(256), 0, st, (const uint2*)d_in, n, msg_len / 8,
                            (uint4*)d_out);
-    else
+    } else {
         hipLaunchKernelGGL(mk::k_keccak_fixed, dim3(grid), dim3(256), 0, st, (const uint8_t*)d_in, n, msg_len,
                            (uint4*)d_out);
+    }
     HIPCHK(hipGetLastError());
     return MK_OK;
 }
@@ -757,6 +774,21 @@ int make_spec(const mk_field* fields, uint32_t nfields, uint32_t record_len, mk:
     return MK_OK;
 }
 
+// k_struct_lock's compile-time layout: the SURVEY §8d ValidatorRecord
+// (3 bytes fields, 6 uint64, 160-B records)
+bool validator_layout(const mk::StructSpec& sp) {
+    static const uint32_t off[9] = {0, 48, 80, 112, 120, 128, 136, 144, 152};
+    static const uint32_t len[9] = {48, 32, 32, 8, 8, 8, 8, 8, 8};
+    if (sp.nfields != 9 || sp.rec_len != 160 || sp.msg_len != 144) return false;
+    for (uint32_t f = 0; f < 9; ++f) {
+        const bool bytes = f < 3;
+        if (sp.kind[f] != (bytes ? MK_FIELD_BYTES : MK_FIELD_RAW) || sp.off[f] != off[f] || sp.len[f] != len[f] ||
+            sp.out_off[f] != (bytes ? 32 * f : 96 + 8 * (f - 3)))
+            return false;
+    }
+    return true;
+}
+
 // roots of n records into d_roots (n x 32); d_msg holds n x msg_len bytes
 int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp, void* d_msg, void* d_roots,
                         hipStream_t st) {
@@ -796,8 +828,19 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
         return MK_OK;
     }
     if (kStructReg && layout && nb == 3 && nraw == 6) {
-        hipLaunchKernelGGL((mk::k_struct_reg<3, 6>), dim3(ceil_div(n, mk::kStructThreads)), dim3(mk::kStructThreads),
-                           0, st, (const uint8_t*)d_rec, n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);
+        // phase-locked whole groups of 1024 records first (16-B aligned records of <= 160 B)
+        const uint64_t ng = (MK_STRUCT_LOCK && vec16 && validator_layout(sp) && n >= (1u << 18)) ? n / mk::kLockThreads
+                                                                                                  : 0;
+        if (ng) {
+            hipLaunchKernelGGL(mk::k_struct_lock, dim3(std::min<uint64_t>(ng, MK_LOCK_GRID)), dim3(mk::kLockThreads),
+                               0, st, (const uint8_t*)d_rec, ng, (uint4*)d_roots);
+            HIPCHK(hipGetLastError());
+        }
+        const uint64_t done = ng * mk::kLockThreads, rest = n - done;
+        if (rest)
+            hipLaunchKernelGGL((mk::k_struct_reg<3, 6>), dim3(ceil_div(rest, mk::kStructThreads)),
+                               dim3(mk::kStructThreads), 0, st, (const uint8_t*)d_rec + done * sp.rec_len, rest, sp,
+                               vec16 ? 1u : 0u, (uint4*)d_roots + 2 * done);
         HIPCHK(hipGetLastError());
         return MK_OK;
     }

@@ -342,6 +342,22 @@ __device__ __forceinline__ void keccak_f_lock(State& s) {
 #pragma unroll kRoundUnroll
     for (int r = 0; r < 24; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
 }
+// `mid` runs after round K (K = 0: before the permutation), e.g. the issue of
+// the next window's DMA in k_leaf_lock_sc.
+template <int K = 0, typename F>
+__device__ __forceinline__ void keccak_f_digest_lock(State& s, F&& mid) {
+    static_assert(K >= 0 && K <= 22, "mid point");
+    if constexpr (K == 0) mid();
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < K; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    if constexpr (K > 0) mid();
+#pragma unroll kRoundUnroll
+    for (int r = K; r < 22; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    round_asm<true>(s, kRcLo[22], kRcHi[22]);
+    last_round_digest(s, kRcLo[23], kRcHi[23]);
+    asm volatile("" : "+v"(s.lo[0]), "+v"(s.hi[0]), "+v"(s.lo[1]), "+v"(s.hi[1]), "+v"(s.lo[2]), "+v"(s.hi[2]),
+                 "+v"(s.lo[3]), "+v"(s.hi[3]));
+}
 __device__ __forceinline__ void keccak_f_digest_lock(State& s) {
 #pragma unroll kRoundUnroll
     for (int r = 0; r < 22; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);

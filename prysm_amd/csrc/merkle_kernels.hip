@@ -550,10 +550,14 @@ __device__ __forceinline__ void hash_window_sc(uint4* Bw, uint32_t lane, const u
         s.hi[2 + 2 * k] ^= u.w;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (Rnext) lock_dma_c<9, 0>(Bw, Rnext, lane);
     s.lo[15] ^= 1u;
     s.hi[16] ^= 0x80000000u;
-    keccak_f_digest_lock(s);
+    // the next window's block 1 goes out MK_LOCK_DMA_ROUND rounds into this
+    // permutation: late enough that little of the data streamed in between
+    // evicts the line block 2 shares with it, early enough to land in time
+    keccak_f_digest_lock<MK_LOCK_DMA_ROUND>(s, [&] {
+        if (Rnext) lock_dma_c<9, 0>(Bw, Rnext, lane);
+    });
     digest(s, d0, d1);
 }
 
@@ -1375,6 +1379,60 @@ __global__ __launch_bounds__(256, MK_K64_WAVES) void k_keccak64(const uint4* __r
     out[2 * i + 1] = d1;
 }
 
+// Phase-locked 64-B messages (MK_K64_LOCK; C2 and 64-B node pairs) for n =
+// 1024 * ngroups messages, the rest by k_keccak64.  1024-thread workgroups,
+// one per CU, persistent; lane m of wave w hashes message g * 1024 + 64 w + m
+// (one phase-locked permutation).  The wave's 64 messages (4 KB, contiguous)
+// land in its 5 KB of LDS by coalesced DMA in a stride-5 image: position
+// 5 m + u holds unit u of message m (u = 4 repeats unit 3), so consecutive
+// lanes of an instruction read consecutive 16-B units and lane m reads its
+// 4 units back at an odd stride, conflict-free.  The next group's copy goes
+// out as soon as the message is read (one permutation ahead).
+__global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* __restrict__ in, uint64_t ngroups,
+                                                                   uint4* __restrict__ out) {
+    __shared__ uint4 buf[kLockThreads / 64][5 * 64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint4* Bw = buf[wave];
+    auto dma = [&](uint64_t g) {
+        const uint4* src = in + (g * kLockThreads + 64 * wave) * 4;
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (uint32_t i = 0; i < 5; ++i) {
+            const uint32_t p = 64 * i + ln, m = p / 5, u = p - 5 * m;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + 4 * m + (u < 4 ? u : 3)),
+                                             (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, 0);
+        }
+    };
+    uint64_t g = blockIdx.x;
+    if (g < ngroups) dma(g);
+#pragma unroll 1
+    for (; g < ngroups; g += gridDim.x) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's messages have landed
+        State s;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint4 v = Bw[5 * lane + u];
+            s.lo[2 * u] = v.x;
+            s.hi[2 * u] = v.y;
+            s.lo[2 * u + 1] = v.z;
+            s.hi[2 * u + 1] = v.w;
+        }
+#pragma unroll
+        for (int k = 8; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+        s.lo[8] = 1u;  // byte 64
+        s.hi[16] = 0x80000000u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read: the next group's copy may land
+        if (g + gridDim.x < ngroups) dma(g + gridDim.x);
+        keccak_f_digest_lock(s);
+        uint4 d0, d1;
+        digest(s, d0, d1);
+        const uint64_t i = g * kLockThreads + threadIdx.x;
+        out[2 * i] = d0;
+        out[2 * i + 1] = d1;
+    }
+}
+
 // n messages of fixed msg_len bytes (any length / alignment).
 __global__ __launch_bounds__(256) void k_keccak_fixed(const uint8_t* __restrict__ in, uint64_t n, uint32_t msg_len,
                                                       uint4* __restrict__ out) {
@@ -1688,6 +1746,93 @@ __global__ __launch_bounds__(kStructThreads, MK_STRUCT_REG_WAVES) void k_struct_
     roots[2 * i + 1] = d1;
 }
 template __global__ void k_struct_reg<3, 6>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
+
+// Phase-locked struct roots (MK_STRUCT_LOCK) for the validator layout of
+// SURVEY §8d (ValidatorRecord: Pubkey 48 B @0, WithdrawalCredentialsHash32
+// 32 B @48, RandaoCommitmentHash32 32 B @80, six uint64 @112..152; 160-B
+// records, 16-B aligned; the host checks the StructSpec against
+// kValOff/kValLen) for n = 1024 * ngroups records, the rest by k_struct_reg.
+// 1024-thread workgroups, one per CU, persistent; lane m of wave w hashes
+// record g * 1024 + 64 w + m with 3 + 2 phase-locked permutations
+// (hash.go:141-159 over the field hashes of :100-107).  The wave's 64
+// records (10 KB, contiguous) are copied into its LDS by coalesced DMA (64 x
+// 16 B per instruction, consecutive lanes on consecutive units; 160 KB for
+// the workgroup), each field digest overwrites that field's own bytes once
+// they are absorbed, and the struct message is read back from the record's
+// slot; the next group's copy goes out once it is (before the two
+// struct-message permutations).
+__device__ constexpr uint32_t kValOff[9] = {0, 48, 80, 112, 120, 128, 136, 144, 152};
+__device__ constexpr uint32_t kValLen[9] = {48, 32, 32, 8, 8, 8, 8, 8, 8};
+__global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* __restrict__ rec, uint64_t ngroups,
+                                                                 uint4* __restrict__ roots) {
+    constexpr uint32_t kRecLen = 160, kRw = kRecLen / 4, kNinstr = kRecLen / 16;
+    __shared__ uint32_t buf[kLockThreads / 64][64 * kRw];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t* Bw = buf[wave];
+    auto dma = [&](uint64_t g) {
+        const uint4* src = reinterpret_cast<const uint4*>(rec + (g * kLockThreads + 64 * wave) * kRecLen);
+#pragma unroll
+        for (uint32_t i = 0; i < kNinstr; ++i)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + 64 * i + lane),
+                                             (__attribute__((address_space(3))) void*)(Bw + 256 * i), 16, 0, 0);
+    };
+    uint64_t g = blockIdx.x;
+    if (g < ngroups) dma(g);
+#pragma unroll 1
+    for (; g < ngroups; g += gridDim.x) {
+        uint32_t* R = Bw + lane * kRw;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's records have landed
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {  // Keccak(le32(len) || bytes), one block
+            const uint32_t len = kValLen[f], off = kValOff[f] / 4, nd = len / 4 + 1;
+            State s;
+#pragma unroll
+            for (uint32_t q = 0; q < 18; ++q) {
+                uint32_t v = q == 0 ? len : (q < nd ? R[off + q - 1] : 0u);
+                if (q == nd) v ^= 1u;
+                if (q & 1)
+                    s.hi[q / 2] = v;
+                else
+                    s.lo[q / 2] = v;
+            }
+#pragma unroll
+            for (int k = 9; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+            s.hi[16] = 0x80000000u;
+            keccak_f_digest_lock(s);
+            // the digest replaces the field's own bytes (absorbed above)
+            R[off + 0] = s.lo[0]; R[off + 1] = s.hi[0]; R[off + 2] = s.lo[1]; R[off + 3] = s.hi[1];
+            R[off + 4] = s.lo[2]; R[off + 5] = s.hi[2]; R[off + 6] = s.lo[3]; R[off + 7] = s.hi[3];
+        }
+        // struct message (hash.go:141-159): the digests of fields 0..2, then
+        // the six uint64 raw: 36 dwords = block 1 (34) + 2 dwords of block 2
+        State s;
+#pragma unroll
+        for (int q = 0; q < 34; ++q) {
+            const uint32_t v = q < 24 ? R[kValOff[q / 8] / 4 + q % 8] : R[kValOff[3] / 4 + (q - 24)];
+            if (q & 1)
+                s.hi[q / 2] = v;
+            else
+                s.lo[q / 2] = v;
+        }
+#pragma unroll
+        for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+        const uint32_t t0 = R[kValOff[3] / 4 + 10], t1 = R[kValOff[3] / 4 + 11];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // record read: the next group's copy may land
+        if (g + gridDim.x < ngroups) dma(g + gridDim.x);
+        keccak_f_lock(s);
+        s.lo[0] ^= t0;
+        s.hi[0] ^= t1;
+        s.lo[1] ^= 1u;  // domain pad at message byte 144 = block 2 byte 8
+        s.hi[16] ^= 0x80000000u;
+        keccak_f_digest_lock(s);
+        uint4 d0, d1;
+        digest(s, d0, d1);
+        const uint64_t i = g * kLockThreads + threadIdx.x;
+        roots[2 * i] = d0;
+        roots[2 * i + 1] = d1;
+    }
+}
+
 template __global__ void k_struct_reg<2, 0>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
 
 // The same layouts for SMALL registries (the 16,384-validator C1 shape),
@@ -1900,6 +2045,87 @@ __global__ __launch_bounds__(kRecThreads, MK_REC_WAVES) void k_keccak_rec(const 
     }
 }
 template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
+
+// Phase-locked records (MK_REC_LOCK): the k_leaf_lock_sc scheme for n
+// messages of NW 8-B words, n a multiple of 1024 (the host runs the rest with
+// k_keccak_rec).  1024-thread workgroups, one per CU, persistent; lane m of
+// wave w hashes record g * 1024 + 64 w + m of group g with phase-locked
+// permutations.  Each full rate block (17 words = 34 dwords) of the wave's 64
+// records is staged in the wave's 8.5 KB of LDS by dword DMA
+// (global_load_lds_dword) in the flattened order U = 34 m + k: consecutive
+// lanes of an instruction read consecutive dwords of one record (a 280-B
+// record read as 8-B words per lane touches one line per lane and every
+// line ~16 times), and lane m reads its words back as 8-B pairs at dword
+// 34 m + 2 k: 32 distinct even banks per half-wave, conflict-free.  Block
+// b + 1 is in flight during block b's permutation, the next record's block 0
+// during this record's last two; the tail words (< 17) are loaded per lane.
+template <int NW>
+__device__ __forceinline__ void rec_dma_block(uint32_t* Bw, const uint32_t* __restrict__ region, int b, uint32_t lane) {
+    asm volatile("" : "+v"(lane));  // recompute the offsets here (see lock_dma_c)
+#pragma unroll
+    for (int i = 0; i < 34; ++i) {
+        const uint32_t U = 64u * i + lane;
+        const uint32_t m = U / 34, k = U - m * 34;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(region + m * (2 * NW) + 34 * b + k),
+                                         (__attribute__((address_space(3))) void*)(Bw + 64 * i), 4, 0, 0);
+    }
+}
+
+template <int NW>
+__global__ __launch_bounds__(kLockThreads, 1) void k_keccak_rec_lock(const uint2* __restrict__ in, uint64_t ngroups,
+                                                                     uint4* __restrict__ out) {
+    constexpr int NFULL = NW / 17;  // full rate blocks (DMA-staged)
+    constexpr int NTAIL = NW % 17;  // words of the last block (per-lane loads)
+    static_assert(NFULL >= 1 && NTAIL < 16, "layout");
+    __shared__ uint32_t buf[kLockThreads / 64][34 * 64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint32_t* Bw = buf[wave];
+    const uint2* Bw2 = reinterpret_cast<const uint2*>(Bw);
+    auto region = [&](uint64_t g) {
+        return reinterpret_cast<const uint32_t*>(in + (g * kLockThreads + 64 * wave) * NW);
+    };
+    uint64_t g = blockIdx.x;
+    if (g < ngroups) rec_dma_block<NW>(Bw, region(g), 0, lane);
+#pragma unroll 1
+    for (; g < ngroups; g += gridDim.x) {
+        const uint64_t rec = g * kLockThreads + threadIdx.x;
+        const uint64_t gn = g + gridDim.x;
+        uint2 tail[NTAIL > 0 ? NTAIL : 1];
+#pragma unroll
+        for (int w = 0; w < NTAIL; ++w) tail[w] = in[rec * NW + 17 * NFULL + w];
+        State s;
+        zero(s);
+#pragma unroll
+        for (int b = 0; b < NFULL; ++b) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block b (and the tail words) landed
+#pragma unroll
+            for (int w = 0; w < 17; ++w) {
+                const uint2 v = Bw2[17 * lane + w];
+                s.lo[w] ^= v.x;
+                s.hi[w] ^= v.y;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: the next block may land
+            if (b + 1 < NFULL)
+                rec_dma_block<NW>(Bw, region(g), b + 1, lane);
+            else if (gn < ngroups)
+                rec_dma_block<NW>(Bw, region(gn), 0, lane);
+            keccak_f_lock(s);
+        }
+#pragma unroll
+        for (int w = 0; w < NTAIL; ++w) {
+            s.lo[w] ^= tail[w].x;
+            s.hi[w] ^= tail[w].y;
+        }
+        s.lo[NTAIL] ^= 1u;  // domain pad byte right after the message
+        s.hi[16] ^= 0x80000000u;
+        keccak_f_digest_lock(s);
+        uint4 d0, d1;
+        digest(s, d0, d1);
+        out[2 * rec] = d0;
+        out[2 * rec + 1] = d1;
+    }
+}
+template __global__ void k_keccak_rec_lock<35>(const uint2*, uint64_t, uint4*);
 
 // ----------------------------------------------------------------------------
 // Deposit trie level: node j = K(in[2j] || (2j+1 < cin ? in[2j+1] : 0^32)),

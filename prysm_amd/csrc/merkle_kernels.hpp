@@ -39,6 +39,9 @@ __global__ void k_leaf_lock_sc(ReduceArgs a, uint64_t ngroups);  // coalesced LD
 #ifndef MK_LOCK_STAGE
 #define MK_LOCK_STAGE 2  // 0: k_leaf_lock (direct per-lane loads), 2: k_leaf_lock_sc (coalesced LDS-DMA)
 #endif
+#ifndef MK_LOCK_DMA_ROUND
+#define MK_LOCK_DMA_ROUND 12  // k_leaf_lock_sc: round of a window's second permutation after which the next block 1 is fetched
+#endif
 #ifndef MK_LOCK_GRID
 #define MK_LOCK_GRID 256
 #endif
@@ -51,6 +54,11 @@ __global__ void k_struct_fields(const uint8_t* rec, uint64_t n, StructSpec sp, u
 __global__ void k_struct_fused(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
 template <int NB, int NRAW>
 __global__ void k_struct_reg(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
+// validator layout (kValOff/kValLen in merkle_kernels.hip), n = 1024 * ngroups
+__global__ void k_struct_lock(const uint8_t* rec, uint64_t ngroups, uint4* roots);
+#ifndef MK_STRUCT_LOCK
+#define MK_STRUCT_LOCK 0
+#endif
 template <int NB, int NRAW>
 __global__ void k_struct_split(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
 #ifndef MK_STRUCT_SPLIT_MAX_N
@@ -63,12 +71,24 @@ template <uint32_t NT, bool LEAF>
 __global__ void k_wave3(ReduceArgs a);
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
 __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);
+__global__ void k_keccak64_lock(const uint4* in, uint64_t ngroups, uint4* out);  // n = 1024 * ngroups
+#ifndef MK_K64_LOCK
+#define MK_K64_LOCK 0
+#endif
 __global__ void k_keccak_fixed(const uint8_t* in, uint64_t n, uint32_t msg_len, uint4* out);
 __global__ void k_keccak_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint4* out);
 __global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
 __global__ void k_keccak_words(const uint2* in, uint64_t n, uint32_t nwords, uint4* out);
 template <int NW>
 __global__ void k_keccak_rec(const uint2* in, uint64_t n, uint4* out);
+template <int NW>
+__global__ void k_keccak_rec_lock(const uint2* in, uint64_t ngroups, uint4* out);  // n = 1024 * ngroups records
+#ifndef MK_REC_LOCK
+#define MK_REC_LOCK 0
+#endif
+#ifndef MK_REC_LOCK_MIN
+#define MK_REC_LOCK_MIN (1u << 18)  // records: at least one group per CU
+#endif
 
 #ifndef MK_REC_THREADS
 #define MK_REC_THREADS 256
