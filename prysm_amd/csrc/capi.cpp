@@ -445,7 +445,8 @@ int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, 
                                (const uint4*)d_in + 4 * done, rest, (uint4*)d_out + 2 * done);
     } else if (kRecKernel && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0) {
         // phase-locked records first (whole groups of 1024), the rest grid-stride
-        const uint64_t ng = (MK_REC_LOCK && n >= MK_REC_LOCK_MIN) ? n / mk::kLockThreads : 0;
+        const uint64_t ng =
+            (MK_REC_LOCK && n >= MK_REC_LOCK_MIN && ((uintptr_t)d_in % 16) == 0) ? n / mk::kLockThreads : 0;
         if (ng)
             hipLaunchKernelGGL((mk::k_keccak_rec_lock<35>), dim3(std::min<uint64_t>(ng, MK_LOCK_GRID)),
                                dim3(mk::kLockThreads), 0, st, (const uint2*)d_in, ng, (uint4*)d_out);

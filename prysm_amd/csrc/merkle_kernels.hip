@@ -518,10 +518,16 @@ __device__ __forceinline__ void lock_dma_c(uint4* Bw, const uint4* __restrict__ 
     }
 }
 
+// `after_wait` runs right after phase A's wait: the previous group's output
+// store goes there, so no wait ever covers a store issued just before it
+// (stores count in vmcnt; a store's wait is the write's round trip).
+template <typename F>
 __device__ __forceinline__ void hash_window_sc(uint4* Bw, uint32_t lane, const uint4* __restrict__ Rj,
-                                               const uint4* __restrict__ Rnext, uint4& d0, uint4& d1) {
+                                               const uint4* __restrict__ Rnext, uint4& d0, uint4& d1,
+                                               F&& after_wait) {
     State s;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phase A has landed
+    after_wait();
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         const uint4 v = Bw[9 * lane + k];
@@ -571,23 +577,33 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock_sc(ReduceArgs a, 
     auto region = [&](uint64_t g) { return items + lock_src(g * kLockThreads + 64 * wave) * 64; };
     uint64_t g = blockIdx.x;
     if (g < ngroups) lock_dma_c<9, 0>(Bw, region(g), lane);
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;  // the previous group's node, stored one group late
+    uint64_t qnode = 0;
+    bool pend = false;
+    auto flush = [&] {
+        if (pend) {
+            out[2 * qnode] = q0;
+            out[2 * qnode + 1] = q1;
+        }
+    };
+    auto none = [] {};
 #pragma unroll 1
     for (; g < ngroups; g += gridDim.x) {
         const uint4* R = region(g);
         const uint64_t gn = g + gridDim.x;
         const uint4* Rn = gn < ngroups ? region(gn) : nullptr;
         uint4 l0, l1, r0, r1, p0, p1;
-        hash_window_sc(Bw, lane, R, R + 16, l0, l1);
-        hash_window_sc(Bw, lane, R + 16, R + 32, r0, r1);
+        hash_window_sc(Bw, lane, R, R + 16, l0, l1, flush);
+        hash_window_sc(Bw, lane, R + 16, R + 32, r0, r1, none);
         hash_node_lock(l0, l1, r0, r1, p0, p1);
-        hash_window_sc(Bw, lane, R + 32, R + 48, l0, l1);
-        hash_window_sc(Bw, lane, R + 48, Rn, r0, r1);
+        hash_window_sc(Bw, lane, R + 32, R + 48, l0, l1, none);
+        hash_window_sc(Bw, lane, R + 48, Rn, r0, r1, none);
         hash_node_lock(l0, l1, r0, r1, l0, l1);
-        hash_node_lock(p0, p1, l0, l1, r0, r1);
-        const uint64_t node = g * kLockThreads + threadIdx.x;
-        out[2 * node] = r0;
-        out[2 * node + 1] = r1;
+        hash_node_lock(p0, p1, l0, l1, q0, q1);
+        qnode = g * kLockThreads + threadIdx.x;
+        pend = true;
     }
+    flush();
 }
 
 template __global__ void k_reduce<true, true, 2>(ReduceArgs);
@@ -1406,9 +1422,16 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
     };
     uint64_t g = blockIdx.x;
     if (g < ngroups) dma(g);
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;  // the previous group's digest, stored after the next wait
+    uint64_t qi = 0;
+    bool pend = false;
 #pragma unroll 1
     for (; g < ngroups; g += gridDim.x) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's messages have landed
+        if (pend) {
+            out[2 * qi] = q0;
+            out[2 * qi + 1] = q1;
+        }
         State s;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1425,11 +1448,13 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read: the next group's copy may land
         if (g + gridDim.x < ngroups) dma(g + gridDim.x);
         keccak_f_digest_lock(s);
-        uint4 d0, d1;
-        digest(s, d0, d1);
-        const uint64_t i = g * kLockThreads + threadIdx.x;
-        out[2 * i] = d0;
-        out[2 * i + 1] = d1;
+        digest(s, q0, q1);
+        qi = g * kLockThreads + threadIdx.x;
+        pend = true;
+    }
+    if (pend) {
+        out[2 * qi] = q0;
+        out[2 * qi + 1] = q1;
     }
 }
 
@@ -1778,10 +1803,17 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     };
     uint64_t g = blockIdx.x;
     if (g < ngroups) dma(g);
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;  // the previous group's root, stored after the next wait
+    uint64_t qi = 0;
+    bool pend = false;
 #pragma unroll 1
     for (; g < ngroups; g += gridDim.x) {
         uint32_t* R = Bw + lane * kRw;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's records have landed
+        if (pend) {
+            roots[2 * qi] = q0;
+            roots[2 * qi + 1] = q1;
+        }
 #pragma unroll
         for (int f = 0; f < 3; ++f) {  // Keccak(le32(len) || bytes), one block
             const uint32_t len = kValLen[f], off = kValOff[f] / 4, nd = len / 4 + 1;
@@ -1825,11 +1857,13 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
         s.lo[1] ^= 1u;  // domain pad at message byte 144 = block 2 byte 8
         s.hi[16] ^= 0x80000000u;
         keccak_f_digest_lock(s);
-        uint4 d0, d1;
-        digest(s, d0, d1);
-        const uint64_t i = g * kLockThreads + threadIdx.x;
-        roots[2 * i] = d0;
-        roots[2 * i + 1] = d1;
+        digest(s, q0, q1);
+        qi = g * kLockThreads + threadIdx.x;
+        pend = true;
+    }
+    if (pend) {
+        roots[2 * qi] = q0;
+        roots[2 * qi + 1] = q1;
     }
 }
 
@@ -2047,27 +2081,29 @@ __global__ __launch_bounds__(kRecThreads, MK_REC_WAVES) void k_keccak_rec(const 
 template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 
 // Phase-locked records (MK_REC_LOCK): the k_leaf_lock_sc scheme for n
-// messages of NW 8-B words, n a multiple of 1024 (the host runs the rest with
-// k_keccak_rec).  1024-thread workgroups, one per CU, persistent; lane m of
-// wave w hashes record g * 1024 + 64 w + m of group g with phase-locked
-// permutations.  Each full rate block (17 words = 34 dwords) of the wave's 64
-// records is staged in the wave's 8.5 KB of LDS by dword DMA
-// (global_load_lds_dword) in the flattened order U = 34 m + k: consecutive
-// lanes of an instruction read consecutive dwords of one record (a 280-B
-// record read as 8-B words per lane touches one line per lane and every
-// line ~16 times), and lane m reads its words back as 8-B pairs at dword
-// 34 m + 2 k: 32 distinct even banks per half-wave, conflict-free.  Block
-// b + 1 is in flight during block b's permutation, the next record's block 0
-// during this record's last two; the tail words (< 17) are loaded per lane.
+// messages of NW 8-B words (8-B aligned, NW odd: 280-B deposits), n a
+// multiple of 1024 (the host runs the rest with k_keccak_rec).  1024-thread
+// workgroups, one per CU, persistent; lane m of wave w hashes record
+// g * 1024 + 64 w + m of group g with phase-locked permutations.  Each full
+// rate block b (136 B) of the wave's 64 records is staged in the wave's 9 KB
+// of LDS by 16-B DMA: record m's block starts 8 ((m + b) & 1) bytes into a
+// 16-B unit and ends inside the 9th, so the 9 covering units of every record
+// are flattened U = 9 m + u (9 instructions per block; consecutive lanes on
+// consecutive units of one record, where a record read as 8-B words per lane
+// touches one line per lane and every line ~16 times), and lane m reads its
+// 17 words back at byte 144 m + 8 ((m + b) & 1).  Block b + 1 is in flight
+// during block b's permutation, the next record's block 0 during this
+// record's last two; the tail words (< 17) are loaded per lane one group ahead.
 template <int NW>
-__device__ __forceinline__ void rec_dma_block(uint32_t* Bw, const uint32_t* __restrict__ region, int b, uint32_t lane) {
+__device__ __forceinline__ void rec_dma_block(uint4* Bw, const uint8_t* __restrict__ region, int b, uint32_t lane) {
     asm volatile("" : "+v"(lane));  // recompute the offsets here (see lock_dma_c)
 #pragma unroll
-    for (int i = 0; i < 34; ++i) {
+    for (int i = 0; i < 9; ++i) {
         const uint32_t U = 64u * i + lane;
-        const uint32_t m = U / 34, k = U - m * 34;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(region + m * (2 * NW) + 34 * b + k),
-                                         (__attribute__((address_space(3))) void*)(Bw + 64 * i), 4, 0, 0);
+        const uint32_t m = U / 9, u = U - m * 9;
+        const uint32_t start = m * (8 * NW) + 136 * b;  // block b of record m (8-B aligned)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(region + (start & ~15u) + 16 * u),
+                                         (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, 0);
     }
 }
 
@@ -2077,52 +2113,79 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak_rec_lock(const uint2
     constexpr int NFULL = NW / 17;  // full rate blocks (DMA-staged)
     constexpr int NTAIL = NW % 17;  // words of the last block (per-lane loads)
     static_assert(NFULL >= 1 && NTAIL < 16, "layout");
-    __shared__ uint32_t buf[kLockThreads / 64][34 * 64];
+    static_assert((8 * NW) % 16 == 8, "records alternate 16-B alignment");
+    __shared__ uint4 buf[kLockThreads / 64][9 * 64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    uint32_t* Bw = buf[wave];
+    uint4* Bw = buf[wave];
     const uint2* Bw2 = reinterpret_cast<const uint2*>(Bw);
     auto region = [&](uint64_t g) {
-        return reinterpret_cast<const uint32_t*>(in + (g * kLockThreads + 64 * wave) * NW);
+        return reinterpret_cast<const uint8_t*>(in + (g * kLockThreads + 64 * wave) * NW);
+    };
+    // the tail words of a group are loaded with its block-0 DMA (one group
+    // ahead), and a group's digest is stored after the next group's first
+    // wait, so no wait covers a load or store issued just before it
+    uint2 tail[NTAIL > 0 ? NTAIL : 1];
+    auto load_tail = [&](uint64_t g) {
+        const uint64_t rec = g * kLockThreads + threadIdx.x;
+#pragma unroll
+        for (int w = 0; w < NTAIL; ++w) tail[w] = in[rec * NW + 17 * NFULL + w];
     };
     uint64_t g = blockIdx.x;
-    if (g < ngroups) rec_dma_block<NW>(Bw, region(g), 0, lane);
+    if (g < ngroups) {
+        rec_dma_block<NW>(Bw, region(g), 0, lane);
+        load_tail(g);
+    }
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+    uint64_t qi = 0;
+    bool pend = false;
 #pragma unroll 1
     for (; g < ngroups; g += gridDim.x) {
         const uint64_t rec = g * kLockThreads + threadIdx.x;
         const uint64_t gn = g + gridDim.x;
-        uint2 tail[NTAIL > 0 ? NTAIL : 1];
-#pragma unroll
-        for (int w = 0; w < NTAIL; ++w) tail[w] = in[rec * NW + 17 * NFULL + w];
+        uint2 tl[NTAIL > 0 ? NTAIL : 1];
         State s;
         zero(s);
 #pragma unroll
         for (int b = 0; b < NFULL; ++b) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block b (and the tail words) landed
+            if (b == 0) {
+#pragma unroll
+                for (int w = 0; w < NTAIL; ++w) tl[w] = tail[w];
+                if (pend) {
+                    out[2 * qi] = q0;
+                    out[2 * qi + 1] = q1;
+                }
+            }
 #pragma unroll
             for (int w = 0; w < 17; ++w) {
-                const uint2 v = Bw2[17 * lane + w];
+                const uint2 v = Bw2[18 * lane + ((lane + b) & 1) + w];
                 s.lo[w] ^= v.x;
                 s.hi[w] ^= v.y;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: the next block may land
-            if (b + 1 < NFULL)
+            if (b + 1 < NFULL) {
                 rec_dma_block<NW>(Bw, region(g), b + 1, lane);
-            else if (gn < ngroups)
+            } else if (gn < ngroups) {
                 rec_dma_block<NW>(Bw, region(gn), 0, lane);
+                load_tail(gn);
+            }
             keccak_f_lock(s);
         }
 #pragma unroll
         for (int w = 0; w < NTAIL; ++w) {
-            s.lo[w] ^= tail[w].x;
-            s.hi[w] ^= tail[w].y;
+            s.lo[w] ^= tl[w].x;
+            s.hi[w] ^= tl[w].y;
         }
         s.lo[NTAIL] ^= 1u;  // domain pad byte right after the message
         s.hi[16] ^= 0x80000000u;
         keccak_f_digest_lock(s);
-        uint4 d0, d1;
-        digest(s, d0, d1);
-        out[2 * rec] = d0;
-        out[2 * rec + 1] = d1;
+        digest(s, q0, q1);
+        qi = rec;
+        pend = true;
+    }
+    if (pend) {
+        out[2 * qi] = q0;
+        out[2 * qi + 1] = q1;
     }
 }
 template __global__ void k_keccak_rec_lock<35>(const uint2*, uint64_t, uint4*);

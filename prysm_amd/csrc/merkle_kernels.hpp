@@ -57,7 +57,7 @@ __global__ void k_struct_reg(const uint8_t* rec, uint64_t n, StructSpec sp, uint
 // validator layout (kValOff/kValLen in merkle_kernels.hip), n = 1024 * ngroups
 __global__ void k_struct_lock(const uint8_t* rec, uint64_t ngroups, uint4* roots);
 #ifndef MK_STRUCT_LOCK
-#define MK_STRUCT_LOCK 0
+#define MK_STRUCT_LOCK 1
 #endif
 template <int NB, int NRAW>
 __global__ void k_struct_split(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
@@ -73,7 +73,7 @@ __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, 
 __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);
 __global__ void k_keccak64_lock(const uint4* in, uint64_t ngroups, uint4* out);  // n = 1024 * ngroups
 #ifndef MK_K64_LOCK
-#define MK_K64_LOCK 0
+#define MK_K64_LOCK 1
 #endif
 __global__ void k_keccak_fixed(const uint8_t* in, uint64_t n, uint32_t msg_len, uint4* out);
 __global__ void k_keccak_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint4* out);
@@ -84,7 +84,7 @@ __global__ void k_keccak_rec(const uint2* in, uint64_t n, uint4* out);
 template <int NW>
 __global__ void k_keccak_rec_lock(const uint2* in, uint64_t ngroups, uint4* out);  // n = 1024 * ngroups records
 #ifndef MK_REC_LOCK
-#define MK_REC_LOCK 0
+#define MK_REC_LOCK 1
 #endif
 #ifndef MK_REC_LOCK_MIN
 #define MK_REC_LOCK_MIN (1u << 18)  // records: at least one group per CU

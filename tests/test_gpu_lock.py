@@ -1,0 +1,133 @@
+"""GPU parity of the phase-locked kernels (1024-thread workgroups whose Keccak
+rounds hold s_barriers; DESIGN.md §4 "Phase-locked rounds") at the shapes
+where they hand over to the free-running kernels: whole groups of 1024
+threads run locked, the persistent grid's workgroups take unequal numbers of
+groups, and the rest (the spans after the last whole group, the ragged tail)
+runs in k_reduce / k_keccak64 / k_keccak_rec / k_struct_reg.  Every result
+against the CPU oracle, bit-exact.  The library build decides which kernels
+are locked (mk_version); the tests hold for either build."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED000000000000
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import torch
+
+    from prysm_amd import _lib
+
+    assert torch.cuda.is_available()
+    _lib.init(0)
+    return torch.device("cuda:0")
+
+
+# merkleHash leaf passes: 2^20 windows (= 2^23 32-B items) is the smallest
+# locked leaf pass; 4096 windows per locked workgroup, 1024 per k_reduce span
+@pytest.mark.parametrize("n", [
+    1 << 23,                          # 256 locked groups exactly, one per CU
+    (1 << 23) + 8 * 1024 * 3 + 77,    # 3 k_reduce FAST spans after the groups + a ragged window
+    5 * (1 << 21) + 12_345,           # 320 groups over 256 workgroups (uneven) + the rest
+    (1 << 24) - 1,                    # odd item count: the last window is padded
+])
+def test_leaf_lock_merkle_vs_oracle(gpu, n):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    items = torch.empty(n * 32, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 41)
+    root = D.merkle_hash(items, n, 32)
+    torch.cuda.synchronize()
+    assert bytes(root.cpu().numpy()) == O.merkle_hash_gen(n, 32, SEED + 41, nthreads=16)
+
+
+def test_leaf_lock_small_items(gpu):
+    """8-B items: 16 per chunk, the same 256-B windows."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    n = (1 << 25) + 1000
+    items = torch.empty(n * 8, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 42)
+    root = D.merkle_hash(items, n, 8)
+    torch.cuda.synchronize()
+    assert bytes(root.cpu().numpy()) == O.merkle_hash_gen(n, 8, SEED + 42, nthreads=16)
+
+
+@pytest.mark.parametrize("n,world", [(1 << 24, 2), ((1 << 25) + 99, 4)])
+def test_leaf_lock_subtree_shards(gpu, n, world):
+    """Subtree shards (the multi-GPU split) whose leaf passes are
+    locked: every shard root against the oracle's subtree and the finished
+    root against the full merkleHash."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    h, ne, begin = D.shard_plan(n, 32, world)
+    items = torch.empty(n * 32, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 43)
+    roots = torch.zeros(world * 32, dtype=torch.uint8, device=gpu)
+    for s in range(ne):
+        D.merkle_subtree(items[begin[s] * 32:begin[s + 1] * 32], begin[s + 1] - begin[s], 32, h, True,
+                         out=roots[32 * s:32 * s + 32])
+    got = D.merkle_finish(roots, ne, n)
+    torch.cuda.synchronize()
+    for s in range(ne):
+        assert bytes(roots[32 * s:32 * s + 32].cpu().numpy()) == O.merkle_subtree_gen(
+            n, 32, SEED + 43, s, h, nthreads=16), s
+    assert bytes(got.cpu().numpy()) == O.merkle_hash_gen(n, 32, SEED + 43, nthreads=16)
+
+
+# batched Keccak: locked for whole groups of 1024 messages once n >= 2^18
+@pytest.mark.parametrize("msg_len,n", [(64, 1 << 18), (64, (1 << 18) + 1024 * 70 + 5),
+                                       (280, 1 << 18), (280, (1 << 18) + 1024 * 70 + 5)])
+def test_hash_batch_lock_vs_oracle(gpu, msg_len, n):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    msgs = torch.empty(n * msg_len, dtype=torch.uint8, device=gpu)
+    D.synth_fill(msgs, SEED + 44 + msg_len)
+    got = D.hash_batch(msgs, n, msg_len)
+    torch.cuda.synchronize()
+    want = O.keccak256_batch(msgs.cpu().numpy(), msg_len, nthreads=16)
+    assert np.array_equal(got.cpu().numpy().reshape(n, 32), want)
+
+
+# typed registry (ValidatorRecord, 160-B records): locked from 2^18 records
+@pytest.mark.parametrize("n", [1 << 18, (1 << 18) + 1024 * 33 + 17])
+def test_struct_lock_vs_oracle(gpu, n):
+    from oracle import oracle as O
+    from prysm_amd import registry as R
+
+    reg = R.synthetic_registry(n, SEED + 45)
+    raw = reg.records.view(np.uint8).reshape(-1)
+    spec = [(k, o, l) for k, o, l in R.VALIDATOR_FIELDS]
+    want = O.struct_roots(raw, n, 160, spec, nthreads=16)
+    assert np.array_equal(R.struct_roots(reg.records), want)
+
+
+def test_deposit_trie_lock_vs_oracle(gpu):
+    """A 2^18 + 3-deposit batch build through the trie handle: the leaves are
+    locked groups + the rest; root and one branch against the oracle."""
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    n, ln = (1 << 18) + 3, 280
+    host = O.splitmix_bytes(n * ln, SEED + 46)
+    deps = [bytes(host[i * ln:(i + 1) * ln]) for i in range(n)]
+    trie = T.DepositTrie.build(deps)
+    root, levels = O.deposit_trie_levels(deps)
+    assert trie.Root() == root
+    k = n - 2
+    branch = trie.GenerateMerkleBranch(k)
+    assert branch[0] == levels[0][k ^ 1]
