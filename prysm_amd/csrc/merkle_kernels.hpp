@@ -83,8 +83,12 @@ template <int NW>
 __global__ void k_keccak_rec(const uint2* in, uint64_t n, uint4* out);
 template <int NW>
 __global__ void k_keccak_rec_lock(const uint2* in, uint64_t ngroups, uint4* out);  // n = 1024 * ngroups records
+// Off by default: one 2^20 trie builds 3 % faster with it, but the C5 bench's
+// stream of tries overlaps each trie's latency-bound top with the next
+// trie's leaves, and a CU-filling locked workgroup leaves no room for that
+// overlap (0.514 -> 0.612 ms/step, profiles/r03m/bench_c5.json).
 #ifndef MK_REC_LOCK
-#define MK_REC_LOCK 1
+#define MK_REC_LOCK 0
 #endif
 #ifndef MK_REC_LOCK_MIN
 #define MK_REC_LOCK_MIN (1u << 18)  // records: at least one group per CU
