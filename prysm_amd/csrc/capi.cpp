@@ -434,15 +434,12 @@ int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, 
     if (!d_out || (!d_in && msg_len)) return fail(MK_EINVAL, "null pointer");
     const uint64_t grid = ceil_div(n, 256);
     if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0) {
-        // phase-locked whole groups of 1024 messages first, the rest one per thread
-        const uint64_t ng = (MK_K64_LOCK && n >= (1u << 18)) ? n / mk::kLockThreads : 0;
-        if (ng)
-            hipLaunchKernelGGL(mk::k_keccak64_lock, dim3(std::min<uint64_t>(ng, MK_LOCK_GRID)), dim3(mk::kLockThreads),
-                               0, st, (const uint4*)d_in, ng, (uint4*)d_out);
-        const uint64_t done = ng * mk::kLockThreads, rest = n - done;
-        if (rest)
-            hipLaunchKernelGGL(mk::k_keccak64, dim3(ceil_div(rest, 256)), dim3(256), 0, st,
-                               (const uint4*)d_in + 4 * done, rest, (uint4*)d_out + 2 * done);
+        if (MK_K64_LOCK && n >= (1u << 18))  // phase-locked (a partial last group included)
+            hipLaunchKernelGGL(mk::k_keccak64_lock,
+                               dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), MK_LOCK_GRID)),
+                               dim3(mk::kLockThreads), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
+        else
+            hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
     } else if (kRecKernel && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0) {
         // phase-locked records first (whole groups of 1024), the rest grid-stride
         const uint64_t ng =
@@ -829,19 +826,13 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
         return MK_OK;
     }
     if (kStructReg && layout && nb == 3 && nraw == 6) {
-        // phase-locked whole groups of 1024 records first (16-B aligned records of <= 160 B)
-        const uint64_t ng = (MK_STRUCT_LOCK && vec16 && validator_layout(sp) && n >= (1u << 18)) ? n / mk::kLockThreads
-                                                                                                  : 0;
-        if (ng) {
-            hipLaunchKernelGGL(mk::k_struct_lock, dim3(std::min<uint64_t>(ng, MK_LOCK_GRID)), dim3(mk::kLockThreads),
-                               0, st, (const uint8_t*)d_rec, ng, (uint4*)d_roots);
-            HIPCHK(hipGetLastError());
-        }
-        const uint64_t done = ng * mk::kLockThreads, rest = n - done;
-        if (rest)
-            hipLaunchKernelGGL((mk::k_struct_reg<3, 6>), dim3(ceil_div(rest, mk::kStructThreads)),
-                               dim3(mk::kStructThreads), 0, st, (const uint8_t*)d_rec + done * sp.rec_len, rest, sp,
-                               vec16 ? 1u : 0u, (uint4*)d_roots + 2 * done);
+        if (MK_STRUCT_LOCK && vec16 && validator_layout(sp) && n >= (1u << 18))  // phase-locked, partial last group
+            hipLaunchKernelGGL(mk::k_struct_lock, dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), MK_LOCK_GRID)),
+                               dim3(mk::kLockThreads), 0, st, (const uint8_t*)d_rec, n, (uint4*)d_roots);
+        else
+            hipLaunchKernelGGL((mk::k_struct_reg<3, 6>), dim3(ceil_div(n, mk::kStructThreads)),
+                               dim3(mk::kStructThreads), 0, st, (const uint8_t*)d_rec, n, sp, vec16 ? 1u : 0u,
+                               (uint4*)d_roots);
         HIPCHK(hipGetLastError());
         return MK_OK;
     }

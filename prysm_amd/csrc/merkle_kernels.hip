@@ -1404,19 +1404,22 @@ __global__ __launch_bounds__(256, MK_K64_WAVES) void k_keccak64(const uint4* __r
 // lanes of an instruction read consecutive 16-B units and lane m reads its
 // 4 units back at an odd stride, conflict-free.  The next group's copy goes
 // out as soon as the message is read (one permutation ahead).
-__global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* __restrict__ in, uint64_t ngroups,
+__global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* __restrict__ in, uint64_t n,
                                                                    uint4* __restrict__ out) {
     __shared__ uint4 buf[kLockThreads / 64][5 * 64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint4* Bw = buf[wave];
+    // a partial last group: lanes past n hash a copy of message n - 1 and store nothing
+    const uint64_t ngroups = (n + kLockThreads - 1) / kLockThreads;
     auto dma = [&](uint64_t g) {
-        const uint4* src = in + (g * kLockThreads + 64 * wave) * 4;
+        const uint64_t m0 = g * kLockThreads + 64 * wave;
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));
 #pragma unroll
         for (uint32_t i = 0; i < 5; ++i) {
             const uint32_t p = 64 * i + ln, m = p / 5, u = p - 5 * m;
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + 4 * m + (u < 4 ? u : 3)),
+            const uint64_t msg = m0 + m < n ? m0 + m : n - 1;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(in + 4 * msg + (u < 4 ? u : 3)),
                                              (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, 0);
         }
     };
@@ -1428,7 +1431,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
 #pragma unroll 1
     for (; g < ngroups; g += gridDim.x) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's messages have landed
-        if (pend) {
+        if (pend && qi < n) {
             out[2 * qi] = q0;
             out[2 * qi + 1] = q1;
         }
@@ -1452,7 +1455,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
         qi = g * kLockThreads + threadIdx.x;
         pend = true;
     }
-    if (pend) {
+    if (pend && qi < n) {
         out[2 * qi] = q0;
         out[2 * qi + 1] = q1;
     }
@@ -1788,18 +1791,25 @@ template __global__ void k_struct_reg<3, 6>(const uint8_t*, uint64_t, StructSpec
 // struct-message permutations).
 __device__ constexpr uint32_t kValOff[9] = {0, 48, 80, 112, 120, 128, 136, 144, 152};
 __device__ constexpr uint32_t kValLen[9] = {48, 32, 32, 8, 8, 8, 8, 8, 8};
-__global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* __restrict__ rec, uint64_t ngroups,
+__global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* __restrict__ rec, uint64_t n,
                                                                  uint4* __restrict__ roots) {
     constexpr uint32_t kRecLen = 160, kRw = kRecLen / 4, kNinstr = kRecLen / 16;
     __shared__ uint32_t buf[kLockThreads / 64][64 * kRw];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t* Bw = buf[wave];
+    // the last group may be partial: its lanes past n copy the last record
+    // (every wave still runs the same permutations and barriers) and store nothing
+    const uint64_t ngroups = (n + kLockThreads - 1) / kLockThreads;
+    const uint64_t last_unit = n * (kRecLen / 16) - 1;
     auto dma = [&](uint64_t g) {
-        const uint4* src = reinterpret_cast<const uint4*>(rec + (g * kLockThreads + 64 * wave) * kRecLen);
+        const uint64_t u0 = (g * kLockThreads + 64 * wave) * (kRecLen / 16);
+        const uint4* src = reinterpret_cast<const uint4*>(rec);
 #pragma unroll
-        for (uint32_t i = 0; i < kNinstr; ++i)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + 64 * i + lane),
+        for (uint32_t i = 0; i < kNinstr; ++i) {
+            const uint64_t u = u0 + 64 * i + lane;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (u < last_unit ? u : last_unit)),
                                              (__attribute__((address_space(3))) void*)(Bw + 256 * i), 16, 0, 0);
+        }
     };
     uint64_t g = blockIdx.x;
     if (g < ngroups) dma(g);
@@ -1810,7 +1820,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     for (; g < ngroups; g += gridDim.x) {
         uint32_t* R = Bw + lane * kRw;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's records have landed
-        if (pend) {
+        if (pend && qi < n) {
             roots[2 * qi] = q0;
             roots[2 * qi + 1] = q1;
         }
@@ -1861,7 +1871,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
         qi = g * kLockThreads + threadIdx.x;
         pend = true;
     }
-    if (pend) {
+    if (pend && qi < n) {
         roots[2 * qi] = q0;
         roots[2 * qi + 1] = q1;
     }

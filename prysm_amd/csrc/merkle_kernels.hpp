@@ -54,8 +54,8 @@ __global__ void k_struct_fields(const uint8_t* rec, uint64_t n, StructSpec sp, u
 __global__ void k_struct_fused(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
 template <int NB, int NRAW>
 __global__ void k_struct_reg(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
-// validator layout (kValOff/kValLen in merkle_kernels.hip), n = 1024 * ngroups
-__global__ void k_struct_lock(const uint8_t* rec, uint64_t ngroups, uint4* roots);
+// validator layout (kValOff/kValLen in merkle_kernels.hip), any n (a partial last group)
+__global__ void k_struct_lock(const uint8_t* rec, uint64_t n, uint4* roots);
 #ifndef MK_STRUCT_LOCK
 #define MK_STRUCT_LOCK 1
 #endif
@@ -71,7 +71,7 @@ template <uint32_t NT, bool LEAF>
 __global__ void k_wave3(ReduceArgs a);
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
 __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);
-__global__ void k_keccak64_lock(const uint4* in, uint64_t ngroups, uint4* out);  // n = 1024 * ngroups
+__global__ void k_keccak64_lock(const uint4* in, uint64_t n, uint4* out);  // any n (a partial last group)
 #ifndef MK_K64_LOCK
 #define MK_K64_LOCK 1
 #endif
