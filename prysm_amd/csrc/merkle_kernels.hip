@@ -504,7 +504,18 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock(ReduceArgs a, uin
 // instruction, each line once), and the LDS image is that flat order: lane m
 // reads its unit u at row 9 m + u (or 7 m + u - 9) -- an odd stride, so the
 // 16-B reads of any 16 consecutive lanes hit distinct bank quads.
-template <int NU, int U0>
+// MK_LOCK_NT=1 (default): the window's line 0 (units 0..7) and block 2
+// (units 9..15, their last use) are fetched non-temporally, so they do not
+// push line 1 out of L2 between block 1's unit 8 and block 2.  Phase A is
+// then 9 instructions of line-0 units in a stride-9 image (the 9th position
+// repeats unit 7) plus one of unit 8 into rows 576..639 (160 KB of LDS).
+// One process, 2^28 (profiles/r03q): fetch 12.14 -> 8.89 GB per leaf pass
+// (1.41x -> 1.03x the algorithmic 8.59 GB), leaf pass 8.138 -> 8.071 ms.
+#ifndef MK_LOCK_NT
+#define MK_LOCK_NT 1
+#endif
+constexpr int kLockAux = MK_LOCK_NT ? 2 : 0;  // global_load_lds aux: nt
+template <int NU, int U0, int AUX = 0>
 __device__ __forceinline__ void lock_dma_c(uint4* Bw, const uint4* __restrict__ Rj, uint32_t lane) {
     // launder the lane index so the per-lane offsets are recomputed here (a
     // few VALU per DMA) instead of being hoisted and held in 16+ VGPRs
@@ -514,7 +525,24 @@ __device__ __forceinline__ void lock_dma_c(uint4* Bw, const uint4* __restrict__ 
         const uint32_t U = 64u * i + lane;
         const uint32_t m = U / NU, u = U - m * NU;
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Rj + m * 64 + U0 + u),
-                                         (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, AUX);
+    }
+}
+// phase A of a window step (block 1 = units 0..8)
+__device__ __forceinline__ void lock_dma_a(uint4* Bw, const uint4* __restrict__ Rj, uint32_t lane) {
+    if constexpr (!MK_LOCK_NT) {
+        lock_dma_c<9, 0>(Bw, Rj, lane);
+    } else {
+        asm volatile("" : "+v"(lane));
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            const uint32_t U = 64u * i + lane;
+            const uint32_t m = U / 9, u = U - m * 9;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Rj + m * 64 + (u < 8 ? u : 7)),
+                                             (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, kLockAux);
+        }
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Rj + lane * 64 + 8),
+                                         (__attribute__((address_space(3))) void*)(Bw + 576), 16, 0, 0);
     }
 }
 
@@ -536,13 +564,13 @@ __device__ __forceinline__ void hash_window_sc(uint4* Bw, uint32_t lane, const u
         s.lo[2 * k + 1] = v.z;
         s.hi[2 * k + 1] = v.w;
     }
-    const uint4 v8 = Bw[9 * lane + 8];
+    const uint4 v8 = Bw[MK_LOCK_NT ? 576 + lane : 9 * lane + 8];
     s.lo[16] = v8.x;
     s.hi[16] = v8.y;
 #pragma unroll
     for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: phase B may overwrite them
-    lock_dma_c<7, 9>(Bw, Rj, lane);
+    lock_dma_c<7, 9, kLockAux>(Bw, Rj, lane);
     keccak_f_lock(s);
     s.lo[0] ^= v8.z;
     s.hi[0] ^= v8.w;
@@ -562,13 +590,13 @@ __device__ __forceinline__ void hash_window_sc(uint4* Bw, uint32_t lane, const u
     // permutation: late enough that little of the data streamed in between
     // evicts the line block 2 shares with it, early enough to land in time
     keccak_f_digest_lock<MK_LOCK_DMA_ROUND>(s, [&] {
-        if (Rnext) lock_dma_c<9, 0>(Bw, Rnext, lane);
+        if (Rnext) lock_dma_a(Bw, Rnext, lane);
     });
     digest(s, d0, d1);
 }
 
 __global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock_sc(ReduceArgs a, uint64_t ngroups) {
-    __shared__ uint4 buf[kLockThreads / 64][9 * 64];
+    __shared__ uint4 buf[kLockThreads / 64][(MK_LOCK_NT ? 10 : 9) * 64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint4* Bw = buf[wave];
     const uint4* items = reinterpret_cast<const uint4*>(a.items);
@@ -576,7 +604,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock_sc(ReduceArgs a, 
     // the wave's 64 nodes = 256 consecutive windows (64 KB); lane m's windows at m * 64 uint4
     auto region = [&](uint64_t g) { return items + lock_src(g * kLockThreads + 64 * wave) * 64; };
     uint64_t g = blockIdx.x;
-    if (g < ngroups) lock_dma_c<9, 0>(Bw, region(g), lane);
+    if (g < ngroups) lock_dma_a(Bw, region(g), lane);
     uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;  // the previous group's node, stored one group late
     uint64_t qnode = 0;
     bool pend = false;
