@@ -445,7 +445,7 @@ int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, 
         const uint64_t ng =
             (MK_REC_LOCK && n >= MK_REC_LOCK_MIN && ((uintptr_t)d_in % 16) == 0) ? n / mk::kLockThreads : 0;
         if (ng)
-            hipLaunchKernelGGL((mk::k_keccak_rec_lock<35>), dim3(std::min<uint64_t>(ng, MK_LOCK_GRID)),
+            hipLaunchKernelGGL((mk::k_keccak_rec_lock<35>), dim3(std::min<uint64_t>(ng, MK_REC_LOCK_GRID)),
                                dim3(mk::kLockThreads), 0, st, (const uint2*)d_in, ng, (uint4*)d_out);
         const uint64_t done = ng * mk::kLockThreads, rest = n - done;
         if (rest)

@@ -248,6 +248,19 @@ __device__ __forceinline__ void hash_node_lock(uint4 l0, uint4 l1, uint4 r0, uin
     digest(s, d0, d1);
 }
 
+// Node-pass inputs (read once; MK_NODE_NT=1: non-temporal)
+#ifndef MK_NODE_NT
+#define MK_NODE_NT 0
+#endif
+__device__ __forceinline__ uint4 ld_node(const uint4* p) {
+    if constexpr (MK_NODE_NT) {
+        const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return ld_stream(p);
+    }
+}
+
 // ----------------------------------------------------------------------------
 // First-level node j of a reduce pass.
 //   LEAF: window j of the item buffer.
@@ -408,8 +421,8 @@ k_reduce(ReduceArgs a) {
                 hash_window256(w + 16, r0, r1);
             } else {
                 const uint4* in = reinterpret_cast<const uint4*>(a.items) + j0 * 4;
-                hash_pair(ld_stream(in), ld_stream(in + 1), ld_stream(in + 2), ld_stream(in + 3), false, l0, l1);
-                hash_pair(ld_stream(in + 4), ld_stream(in + 5), ld_stream(in + 6), ld_stream(in + 7), false, r0, r1);
+                hash_pair(ld_node(in), ld_node(in + 1), ld_node(in + 2), ld_node(in + 3), false, l0, l1);
+                hash_pair(ld_node(in + 4), ld_node(in + 5), ld_node(in + 6), ld_node(in + 7), false, r0, r1);
             }
             hash_pair(l0, l1, r0, r1, false, d0, d1);
             lds[2 * q] = d0;
@@ -515,6 +528,11 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock(ReduceArgs a, uin
 #define MK_LOCK_NT 1
 #endif
 constexpr int kLockAux = MK_LOCK_NT ? 2 : 0;  // global_load_lds aux: nt
+// the side configs' locked kernels (C2 messages, C3 records): inputs read once
+#ifndef MK_SIDE_NT
+#define MK_SIDE_NT 0
+#endif
+constexpr int kSideAux = MK_SIDE_NT ? 2 : 0;
 template <int NU, int U0, int AUX = 0>
 __device__ __forceinline__ void lock_dma_c(uint4* Bw, const uint4* __restrict__ Rj, uint32_t lane) {
     // launder the lane index so the per-lane offsets are recomputed here (a
@@ -1423,6 +1441,15 @@ __global__ __launch_bounds__(256, MK_K64_WAVES) void k_keccak64(const uint4* __r
     out[2 * i + 1] = d1;
 }
 
+// digest outputs nobody in this kernel reads again: non-temporal with MK_SIDE_NT
+__device__ __forceinline__ void st_out(uint4* p, uint4 v) {
+    if constexpr (MK_SIDE_NT) {
+        __builtin_nontemporal_store(*reinterpret_cast<const u32x4_t*>(&v), reinterpret_cast<u32x4_t*>(p));
+    } else {
+        *p = v;
+    }
+}
+
 // Phase-locked 64-B messages (MK_K64_LOCK; C2 and 64-B node pairs) for n =
 // 1024 * ngroups messages, the rest by k_keccak64.  1024-thread workgroups,
 // one per CU, persistent; lane m of wave w hashes message g * 1024 + 64 w + m
@@ -1448,7 +1475,8 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
             const uint32_t p = 64 * i + ln, m = p / 5, u = p - 5 * m;
             const uint64_t msg = m0 + m < n ? m0 + m : n - 1;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(in + 4 * msg + (u < 4 ? u : 3)),
-                                             (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, 0);
+                                             (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0,
+                                             kSideAux);
         }
     };
     uint64_t g = blockIdx.x;
@@ -1460,8 +1488,8 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
     for (; g < ngroups; g += gridDim.x) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's messages have landed
         if (pend && qi < n) {
-            out[2 * qi] = q0;
-            out[2 * qi + 1] = q1;
+            st_out(out + 2 * qi, q0);
+            st_out(out + 2 * qi + 1, q1);
         }
         State s;
 #pragma unroll
@@ -1484,8 +1512,8 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
         pend = true;
     }
     if (pend && qi < n) {
-        out[2 * qi] = q0;
-        out[2 * qi + 1] = q1;
+        st_out(out + 2 * qi, q0);
+        st_out(out + 2 * qi + 1, q1);
     }
 }
 
@@ -1836,7 +1864,8 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
         for (uint32_t i = 0; i < kNinstr; ++i) {
             const uint64_t u = u0 + 64 * i + lane;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (u < last_unit ? u : last_unit)),
-                                             (__attribute__((address_space(3))) void*)(Bw + 256 * i), 16, 0, 0);
+                                             (__attribute__((address_space(3))) void*)(Bw + 256 * i), 16, 0,
+                                             kSideAux);
         }
     };
     uint64_t g = blockIdx.x;

@@ -90,6 +90,9 @@ __global__ void k_keccak_rec_lock(const uint2* in, uint64_t ngroups, uint4* out)
 #ifndef MK_REC_LOCK
 #define MK_REC_LOCK 0
 #endif
+#ifndef MK_REC_LOCK_GRID
+#define MK_REC_LOCK_GRID 256  // < 256 leaves CUs free for work overlapping the leaves (a stream of tries)
+#endif
 #ifndef MK_REC_LOCK_MIN
 #define MK_REC_LOCK_MIN (1u << 18)  // records: at least one group per CU
 #endif
