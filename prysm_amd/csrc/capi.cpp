@@ -381,10 +381,11 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
             uint64_t fast_base = 0;
             if (ps.nlock && !a.elem_len) {  // phase-locked leaf workgroups first: 4 spans each, levels == 3
                 a.wg_base = 0;
-                // persistent grid (one 1024-thread workgroup per CU); k_leaf_lock (MK_LOCK_STAGE=0)
-                // takes one group per workgroup
+                // persistent grid (one 1024-thread workgroup per CU) for whole trees, one group per
+                // workgroup for subtree shards (planner.cpp); k_leaf_lock (MK_LOCK_STAGE=0) always the latter
                 if (MK_LOCK_STAGE == 2)
-                    hipLaunchKernelGGL(mk::k_leaf_lock_sc, dim3(std::min<uint64_t>(ps.nlock, MK_LOCK_GRID)),
+                    hipLaunchKernelGGL(mk::k_leaf_lock_sc,
+                                       dim3(ps.lock_persist ? std::min<uint64_t>(ps.nlock, MK_LOCK_GRID) : ps.nlock),
                                        dim3(mk::kLockThreads), 0, st, a, ps.nlock);
                 else
                     hipLaunchKernelGGL(mk::k_leaf_lock, dim3(ps.nlock), dim3(mk::kLockThreads), 0, st, a, ps.nlock);
