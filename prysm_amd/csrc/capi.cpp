@@ -303,6 +303,21 @@ bool inject_ehip() {
     return on;
 }
 
+// Workgroups of a persistent phase-locked launch on `st`: one per CU the
+// stream may use (its CU mask, hipExtStreamCreateWithCUMask), at most
+// MK_LOCK_GRID.  A persistent 1024-thread workgroup needs a whole CU, so a
+// grid larger than the stream's CUs would run a second, straggling round.
+uint64_t lock_grid_cap(hipStream_t st) {
+    uint32_t m[16] = {0};  // up to 512 CUs
+    if (hipExtStreamGetCUMask(st, 16, m) != hipSuccess) {
+        (void)hipGetLastError();
+        return MK_LOCK_GRID;
+    }
+    uint64_t c = 0;
+    for (uint32_t w : m) c += (uint64_t)__builtin_popcount(w);
+    return c ? std::min<uint64_t>(c, MK_LOCK_GRID) : MK_LOCK_GRID;
+}
+
 int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t* d_ws, uint64_t ws_bytes,
                 hipStream_t st) {
     if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
@@ -385,7 +400,7 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                 // workgroup for subtree shards (planner.cpp); k_leaf_lock (MK_LOCK_STAGE=0) always the latter
                 if (MK_LOCK_STAGE == 2)
                     hipLaunchKernelGGL(mk::k_leaf_lock_sc,
-                                       dim3(ps.lock_persist ? std::min<uint64_t>(ps.nlock, MK_LOCK_GRID) : ps.nlock),
+                                       dim3(ps.lock_persist ? std::min<uint64_t>(ps.nlock, lock_grid_cap(st)) : ps.nlock),
                                        dim3(mk::kLockThreads), 0, st, a, ps.nlock);
                 else
                     hipLaunchKernelGGL(mk::k_leaf_lock, dim3(ps.nlock), dim3(mk::kLockThreads), 0, st, a, ps.nlock);
@@ -437,7 +452,7 @@ int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, 
     if (msg_len == 64 && ((uintptr_t)d_in % 16) == 0 && ((uintptr_t)d_out % 16) == 0) {
         if (MK_K64_LOCK && n >= (1u << 18))  // phase-locked (a partial last group included)
             hipLaunchKernelGGL(mk::k_keccak64_lock,
-                               dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), MK_LOCK_GRID)),
+                               dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), lock_grid_cap(st))),
                                dim3(mk::kLockThreads), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
         else
             hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
@@ -446,7 +461,8 @@ int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, 
         const uint64_t ng =
             (MK_REC_LOCK && n >= MK_REC_LOCK_MIN && ((uintptr_t)d_in % 16) == 0) ? n / mk::kLockThreads : 0;
         if (ng)
-            hipLaunchKernelGGL((mk::k_keccak_rec_lock<35>), dim3(std::min<uint64_t>(ng, MK_REC_LOCK_GRID)),
+            hipLaunchKernelGGL((mk::k_keccak_rec_lock<35>),
+                               dim3(std::min<uint64_t>({ng, (uint64_t)MK_REC_LOCK_GRID, lock_grid_cap(st)})),
                                dim3(mk::kLockThreads), 0, st, (const uint2*)d_in, ng, (uint4*)d_out);
         const uint64_t done = ng * mk::kLockThreads, rest = n - done;
         if (rest)
@@ -828,7 +844,7 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
     }
     if (kStructReg && layout && nb == 3 && nraw == 6) {
         if (MK_STRUCT_LOCK && vec16 && validator_layout(sp) && n >= (1u << 18))  // phase-locked, partial last group
-            hipLaunchKernelGGL(mk::k_struct_lock, dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), MK_LOCK_GRID)),
+            hipLaunchKernelGGL(mk::k_struct_lock, dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), lock_grid_cap(st))),
                                dim3(mk::kLockThreads), 0, st, (const uint8_t*)d_rec, n, (uint4*)d_roots);
         else
             hipLaunchKernelGGL((mk::k_struct_reg<3, 6>), dim3(ceil_div(n, mk::kStructThreads)),
