@@ -508,12 +508,11 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock(ReduceArgs a, uin
 // and a locked workgroup has no other workgroup on its CU to cover the wait;
 // its per-lane 16-B loads of lanes 1 KB apart also touch 64 lines per
 // instruction and every line 8 times.  Here phase A of window j (units
-// 0..8 = block 1) lands in the wave's 9 KB of LDS during the previous
-// window's second permutation and phase B (units 9..15) during this window's
-// first, and the 576 (phase A: units
-// 0..8) or 448 (phase B: units 9..15) 16-B units of the step are flattened
-// window-major (U = 9 m + u or 7 m + u - 9), so consecutive lanes of a DMA
-// instruction read consecutive units of one window (~15 lines per
+// 0..8 = block 1) lands in the wave's LDS (10 KB per wave) during the
+// previous window's second permutation and phase B (units 9..15) during this
+// window's first.  The 16-B units of a step are flattened window-major
+// (phase A: U = 9 m + u; phase B: U = 7 m + u - 9), so consecutive lanes of a
+// DMA instruction read consecutive units of one window (~15 lines per
 // instruction, each line once), and the LDS image is that flat order: lane m
 // reads its unit u at row 9 m + u (or 7 m + u - 9) -- an odd stride, so the
 // 16-B reads of any 16 consecutive lanes hit distinct bank quads.
