@@ -308,6 +308,12 @@ bool inject_ehip() {
 // MK_LOCK_GRID.  A persistent 1024-thread workgroup needs a whole CU, so a
 // grid larger than the stream's CUs would run a second, straggling round.
 uint64_t lock_grid_cap(hipStream_t st) {
+    // no stream query inside a graph capture (the default grid is recorded)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
+        (void)hipGetLastError();
+        return MK_LOCK_GRID;
+    }
     uint32_t m[16] = {0};  // up to 512 CUs
     if (hipExtStreamGetCUMask(st, 16, m) != hipSuccess) {
         (void)hipGetLastError();

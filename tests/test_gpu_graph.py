@@ -32,7 +32,9 @@ def _capture(fn):
     return g
 
 
-@pytest.mark.parametrize("n,item_len", [(1 << 20, 32), ((1 << 16) + 3, 32), (100_003, 8), (5, 32)])
+# (1 << 23) + 77: the phase-locked leaf pass (k_leaf_lock_sc) inside the graph
+@pytest.mark.parametrize("n,item_len", [(1 << 20, 32), ((1 << 16) + 3, 32), (100_003, 8), (5, 32),
+                                        ((1 << 23) + 77, 32)])
 def test_graph_merkle_hash(gpu, n, item_len):
     import torch
 
@@ -146,3 +148,26 @@ def test_graph_capture_refused_by_merkle_many(gpu):
     for i in range(3):
         want = O.merkle_hash_flat(host[offs[i]:offs[i] + ns[i] * ils[i]], ns[i], ils[i])
         assert bytes(roots[32 * i:32 * i + 32].cpu().numpy()) == want
+
+
+def test_graph_hash_batch_locked(gpu):
+    """2^18 + 5 64-B messages: k_keccak64_lock (a partial last group) captured
+    and replayed over new contents."""
+    import numpy as np
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    n = (1 << 18) + 5
+    msgs = torch.empty(n * 64, dtype=torch.uint8, device=gpu)
+    D.synth_fill(msgs, SEED + 77)
+    out = torch.zeros(n * 32, dtype=torch.uint8, device=gpu)
+    g = _capture(lambda: D.hash_batch(msgs, n, 64, out=out))
+    for seed in (SEED + 77, SEED + 78):
+        D.synth_fill(msgs, seed)
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        want = O.keccak256_batch(msgs.cpu().numpy(), 64, nthreads=16)
+        assert np.array_equal(out.cpu().numpy().reshape(n, 32), want)
