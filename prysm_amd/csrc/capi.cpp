@@ -568,12 +568,31 @@ struct ElemPlan {
     bool fused = false;
     uint64_t dig_bytes = 0;  // two-phase: digest array at the start of the workspace
     uint64_t ws_bytes = 0;
+    bool locked = false;  // k_elem_lock writes the window digests, `p` reduces them (node input, mix-in n)
+    uint64_t nwin = 0;
 };
+
+#ifndef MK_ELEM_LOCK
+#define MK_ELEM_LOCK 1
+#endif
+#ifndef MK_ELEM_LOCK_MIN_LOG2
+#define MK_ELEM_LOCK_MIN_LOG2 23  // elements (2^20 windows: 1024 groups)
+#endif
 
 int make_elem_plan(uint64_t n, uint32_t elem_len, bool aligned16, ElemPlan& e) {
     e = ElemPlan();
     if (n > (UINT64_MAX / 4) / 32) return fail(MK_EINVAL, "n too large");
     const bool fast32 = elem_len == 32 && aligned16;
+    if (MK_ELEM_LOCK && fast32 && n % 8 == 0 && n >= (1ull << MK_ELEM_LOCK_MIN_LOG2)) {
+        // phase-locked element windows (every window full: 8 elements = 2
+        // chunks), then the tree above them from its level-1 nodes
+        e.locked = true;
+        e.nwin = n / 8;
+        TRY(mk::make_plan(e.nwin, 32, false, 0, false, true, e.p, /*node_input=*/true, 0, /*mixin_n=*/n));
+        e.dig_bytes = (32 * e.nwin + 255) & ~255ull;
+        e.ws_bytes = e.dig_bytes + mk::plan_ws_bytes(e.p);
+        return MK_OK;
+    }
     TRY(mk::make_plan(n, 32, false, 0, false, fast32, e.p, false, 0, 0, /*leaf_ni1=*/fast32));
     e.fused = fast32 && !e.p.small && !e.p.passes.empty() && !e.p.passes[0].wave && !e.p.passes[0].sp;
     if (!e.fused && fast32) TRY(mk::make_plan(n, 32, false, 0, false, true, e.p));  // the ordinary plan over digests
@@ -613,6 +632,26 @@ int dev_tree_hash_elems(const void* d_elems, uint64_t n, uint32_t elem_len, void
     if (n && !d_ws) return fail(MK_EINVAL, "null workspace");
     if (e.fused) return launch_plan(e.p, (const uint8_t*)d_elems, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st);
     uint8_t* dig = (uint8_t*)d_ws;
+    if (e.locked) {
+        ProfRec rec{};
+        const bool prof = prof_on();
+        if (prof) {
+            HIPCHK(hipEventCreate(&rec.a));
+            HIPCHK(hipEventCreate(&rec.b));
+            HIPCHK(hipEventRecord(rec.a, st));
+        }
+        hipLaunchKernelGGL(mk::k_elem_lock, dim3(std::min<uint64_t>(ceil_div(e.nwin, mk::kLockThreads), lock_grid_cap(st))),
+                           dim3(mk::kLockThreads), 0, st, (const uint4*)d_elems, e.nwin, (uint4*)dig);
+        HIPCHK(hipGetLastError());
+        if (prof) {
+            HIPCHK(hipEventRecord(rec.b, st));
+            rec.perms = 10.0 * (double)e.nwin;  // 8 element digests + the 2-block window
+            rec.hashes = 9.0 * (double)e.nwin;
+            std::lock_guard<std::mutex> lk(g_prof_mu);
+            g_prof.push_back(rec);
+        }
+        return launch_plan(e.p, dig, (uint8_t*)d_out32, dig + e.dig_bytes, ws_bytes - e.dig_bytes, st);
+    }
     if (n) {
         ProfRec rec{};
         const bool prof = prof_on();

@@ -877,6 +877,136 @@ __global__ __launch_bounds__(kReduceThreads, FAST ? MK_ELEM_WAVES : 1) void k_re
 }
 
 template __global__ void k_reduce_elem<true>(ReduceArgs);
+
+// Phase-locked element windows (MK_ELEM_LOCK; C4 secondary, TreeHash of
+// [][32]byte): lane m of wave w hashes window g * 1024 + 64 w + m of group g
+// -- its 8 element digests K(le32(32) || e) (1 permutation each) and the
+// window K(d0 || .. || d7) (2) -- with phase-locked permutations and writes
+// the window digest (a level-1 node of the tree; the host finishes the tree
+// from those nodes).  n windows in all; a partial last group's lanes past n
+// hash copies of window n - 1 and store nothing.  The window's two halves
+// (elements 0..3, 4..7: 128 B = 8 units each) are staged in the wave's 9 KB
+// of LDS by coalesced non-temporal DMA in a stride-9 image (the 9th
+// position repeats unit 7); digests 0..3 wait in VGPRs, digests 4..7 replace
+// their elements in LDS, and the next window's first half goes out once
+// block 2 of this window's message has been read.
+__device__ __forceinline__ void elem_dma_half(uint4* Bw, const uint4* __restrict__ W0, uint64_t m0, uint64_t nwin,
+                                              int half, uint32_t lane) {
+    asm volatile("" : "+v"(lane));
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        const uint32_t U = 64u * i + lane;
+        const uint32_t m = U / 9, u = U - m * 9;
+        const uint64_t win = m0 + m < nwin ? m0 + m : nwin - 1;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(W0 + win * 16 + 8 * half + (u < 8 ? u : 7)),
+                                         (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, kLockAux);
+    }
+}
+__device__ __forceinline__ void elem_digest_lock(uint4 a, uint4 b, uint32_t (&d)[8]) {
+    State s;
+    s.lo[0] = 32u;  // le32(len)
+    s.hi[0] = a.x;
+    s.lo[1] = a.y;
+    s.hi[1] = a.z;
+    s.lo[2] = a.w;
+    s.hi[2] = b.x;
+    s.lo[3] = b.y;
+    s.hi[3] = b.z;
+    s.lo[4] = b.w;
+    s.hi[4] = 1u;  // domain pad at byte 36
+#pragma unroll
+    for (int k = 5; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+    s.hi[16] = 0x80000000u;
+    keccak_f_digest_lock(s);
+    d[0] = s.lo[0]; d[1] = s.hi[0]; d[2] = s.lo[1]; d[3] = s.hi[1];
+    d[4] = s.lo[2]; d[5] = s.hi[2]; d[6] = s.lo[3]; d[7] = s.hi[3];
+}
+__global__ __launch_bounds__(kLockThreads, 1) void k_elem_lock(const uint4* __restrict__ elems, uint64_t nwin,
+                                                               uint4* __restrict__ out) {
+    __shared__ uint4 buf[kLockThreads / 64][9 * 64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint4* Bw = buf[wave];
+    const uint4* Rl = Bw + 9 * lane;  // this lane's 8 staged units (+1 repeat)
+    const uint64_t ngroups = (nwin + kLockThreads - 1) / kLockThreads;
+    uint64_t g = blockIdx.x;
+    if (g < ngroups) elem_dma_half(Bw, elems, g * kLockThreads + 64 * wave, nwin, 0, lane);
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+    uint64_t qi = 0;
+    bool pend = false;
+#pragma unroll 1
+    for (; g < ngroups; g += gridDim.x) {
+        const uint64_t m0 = g * kLockThreads + 64 * wave;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // first half landed
+        if (pend && qi < nwin) {
+            out[2 * qi] = q0;
+            out[2 * qi + 1] = q1;
+        }
+        uint32_t dlo[4][8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 a = Rl[2 * k], b = Rl[2 * k + 1];
+            if (k == 3) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // first half read: the second may land
+                elem_dma_half(Bw, elems, m0, nwin, 1, lane);
+            }
+            elem_digest_lock(a, b, dlo[k]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // second half landed
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 a = Rl[2 * k], b = Rl[2 * k + 1];
+            uint32_t d[8];
+            elem_digest_lock(a, b, d);
+            // digest 4 + k replaces element 4 + k (same 32 B, already absorbed)
+            uint4* R = Bw + 9 * lane;
+            R[2 * k] = make_uint4(d[0], d[1], d[2], d[3]);
+            R[2 * k + 1] = make_uint4(d[4], d[5], d[6], d[7]);
+        }
+        // the window message d0..d7 (256 B): block 1 = d0..d3 + the first 8 B of d4
+        State s;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                s.lo[4 * k + w] = dlo[k][2 * w];
+                s.hi[4 * k + w] = dlo[k][2 * w + 1];
+            }
+        const uint4 t4a = Rl[0];
+        s.lo[16] = t4a.x;
+        s.hi[16] = t4a.y;
+#pragma unroll
+        for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
+        keccak_f_lock(s);
+        // block 2 = d4[8..32) + d5 + d6 + d7 + padding at byte 256 = byte 120
+        s.lo[0] ^= t4a.z;
+        s.hi[0] ^= t4a.w;
+        {
+            const uint4 t = Rl[1];
+            s.lo[1] ^= t.x; s.hi[1] ^= t.y; s.lo[2] ^= t.z; s.hi[2] ^= t.w;
+        }
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            const uint4 a = Rl[2 * k], b = Rl[2 * k + 1];
+            s.lo[4 * k - 1] ^= a.x; s.hi[4 * k - 1] ^= a.y; s.lo[4 * k] ^= a.z; s.hi[4 * k] ^= a.w;
+            s.lo[4 * k + 1] ^= b.x; s.hi[4 * k + 1] ^= b.y; s.lo[4 * k + 2] ^= b.z; s.hi[4 * k + 2] ^= b.w;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // digests read: the next window's first half may land
+        if (g + gridDim.x < ngroups)
+            elem_dma_half(Bw, elems, (g + gridDim.x) * kLockThreads + 64 * wave, nwin, 0, lane);
+        s.lo[15] ^= 1u;  // byte 256 = byte 120 of block 2
+        s.hi[16] ^= 0x80000000u;
+        keccak_f_digest_lock(s);
+        digest(s, q0, q1);
+        qi = g * kLockThreads + threadIdx.x;
+        pend = true;
+    }
+    if (pend && qi < nwin) {
+        out[2 * qi] = q0;
+        out[2 * qi + 1] = q1;
+    }
+}
+
+
 template __global__ void k_reduce_elem<false>(ReduceArgs);
 
 // Element digests K(le32(elem_len) || element i) -> out[i] (32 B): the first

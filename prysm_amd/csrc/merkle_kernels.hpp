@@ -47,6 +47,8 @@ __global__ void k_leaf_lock_sc(ReduceArgs a, uint64_t ngroups);  // coalesced LD
 #endif
 template <bool FAST>
 __global__ void k_reduce_elem(ReduceArgs a);
+// phase-locked element windows: nwin window digests (level-1 nodes) of 8 x 32-B elements each
+__global__ void k_elem_lock(const uint4* elems, uint64_t nwin, uint4* out);
 template <bool FAST32>
 __global__ void k_elem_digests(const uint8_t* elems, uint64_t n, uint32_t elem_len, uint4* out);
 template <bool FAST>

@@ -123,6 +123,23 @@ def test_tree_hash_reflective_routes(gpu):
             assert ssz.tree_hash(vals, ssz.Slice(ssz.ByteArray(L))) == want, (n, L)
 
 
+# k_elem_lock (phase-locked element windows, n % 8 == 0 and n >= 2^23):
+# 1024 groups; a partial last group + an odd window count; n not a multiple
+# of 8 falls back to the fused form at the same size
+@pytest.mark.parametrize("n", [1 << 23, (1 << 23) + 8 * (1024 * 37 + 5), (1 << 23) + 4])
+def test_tree_hash_32b_locked_windows(gpu, n):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    items = torch.empty(n * 32, dtype=torch.uint8, device=gpu)
+    D.synth_fill(items, SEED + 23)
+    out = D.tree_hash_bytes_list(items, n, 32)
+    torch.cuda.synchronize()
+    assert bytes(out.cpu().numpy()) == O.tree_hash_bytes_list(items.cpu().numpy(), n, 32, nthreads=16)
+
+
 def test_tree_hash_2p28_golden(gpu):
     """The secondary C4 line's workload: TreeHash([][32]byte) of 2^28
     SplitMix64 elements (8 GiB generated on the device) vs the committed
