@@ -1496,7 +1496,7 @@ extern "C" {
 #define MK_STR(x) MK_STR2(x)
 const char* mk_version(void) {
     return "prysm_merkle 0.3 (gfx950; leaf_lock=" MK_STR(MK_LEAF_LOCK) " lock_stage=" MK_STR(MK_LOCK_STAGE)
-           " lock_bars=" MK_STR(MK_LOCK_BARS) ")";
+           " lock_bars=" MK_STR(MK_LOCK_BARS) " elem_lock=" MK_STR(MK_ELEM_LOCK) ")";
 }
 
 const char* mk_strerror(int code) {

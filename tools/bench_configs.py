@@ -241,6 +241,19 @@ def run_config(args):
         nl = max(launches, 1)
         leaf_s = leaf_ms / 1e3 / nl
         leaf_ops = (lperms / nl) * OPS_PER_PERM - (lhashes / nl) * OPS_SAVED_PER_HASH
+        # the element pass this build runs (mk_version carries MK_ELEM_LOCK;
+        # the locked form needs n % 8 == 0 and n >= 2^23, true at 2^28)
+        if "elem_lock=1" in _lib.load().mk_version().decode():
+            kname = "k_elem_lock"
+            kdesc = ("k_elem_lock (phase-locked element windows: 1024-thread workgroups, s_barrier in every Keccak "
+                     "round; 8 element digests + the window hash per thread, 10 permutations; coalesced LDS-DMA "
+                     "staging)")
+        else:
+            kname = "k_reduce_elem"
+            kdesc = "k_reduce_elem<FAST> (8 element digests + window + pair level + 3 LDS levels)"
+        from bench import load_pmc
+
+        traffic, clk, pmc_src = load_pmc(kname)
         cpu = None
         if not args.no_cpu_baseline:
             from oracle import oracle as O
@@ -258,7 +271,7 @@ def run_config(args):
               {"workload": "C4 secondary: ssz.TreeHash of 2^28 x [32]byte elements (8 GiB), one device call, "
                            "element digests fused into the leaf pass", "n": n, "elem_len": el, "root": root,
                "root_matches_golden": True},
-              cpu, {"kernel": "k_reduce_elem<FAST> (8 element digests + window + pair level + 3 LDS levels)",
+              cpu, {"kernel": kdesc, "traffic": traffic, "traffic_source": pmc_src, "effective_clock_GHz": clk,
                     "leaf_kernel_ms": leaf_s * 1e3, "leaf_kernel_achieved": leaf_ops / leaf_s / 1e12,
                     "leaf_kernel_frac": leaf_ops / leaf_s / PEAK_INT_OPS,
                     "leaf_perms_per_launch": lperms / nl, "leaf_hashes_per_launch": lhashes / nl,
