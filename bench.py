@@ -86,7 +86,7 @@ def leaf_kernel():
 
     v = _lib.load().mk_version().decode()
     if "leaf_lock=1" in v:
-        return ("k_leaf_lock_sc" if "lock_stage=2" in v else "k_leaf_lock",
+        return ("k_leaf_lock_sc",
                 "k_leaf_lock_sc (phase-locked leaf pass: 1024-thread workgroups, s_barrier in every Keccak round; "
                 "4 windows -> 1 node per thread, 3 levels; coalesced LDS-DMA staging)")
     return "k_reduce<true, true, 2>", "k_reduce<LEAF, FAST, 2> (leaf pass: 256-B windows + 4 fused levels)"
@@ -354,7 +354,11 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
     log(f"rank {rank}/{world}: {local_n} items ({nbytes / 2**30:.2f} GiB), shard height {sp.height}, "
         f"nonempty {sp.nonempty}, frontier {k}")
 
-    def step_one_stream():
+    # N > 1: hipEvent marks of the rank step's phases (leaf pass, node passes
+    # to the frontier, all-gather, finisher), recorded during the timed steps
+    timer = P.PhaseTimer(cuda=True) if world > 1 else None
+
+    def step_one_stream(t=None):
         return P.sharded_merkle_hash(
             items, n, item_len, sp, rank, world,
             subtree_fn=lambda it, sn, il, h, pad: D.merkle_subtree(it, sn, il, h, pad, out=root_buf, ws=ws),
@@ -363,7 +367,8 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
             gather_buf=gather_buf, finish_stream=finish_stream, frontier_log2=k,
             frontier_fn=lambda it, sn, il, h, kk, pad: D.merkle_subtree_frontier(it, sn, il, h, kk, pad,
                                                                                  out=frontier_buf, ws=ws),
-            finish_nodes_fn=lambda g, c, nt: D.merkle_finish_nodes(g, c, nt, out=finish_out, ws=finish_ws))
+            finish_nodes_fn=lambda g, c, nt: D.merkle_finish_nodes(g, c, nt, out=finish_out, ws=finish_ws),
+            timer=t)
 
     # --pipeline: everything above the leaf pass of step i runs on a side
     # stream that overlaps step i+1's leaf pass (N = 1: pipeline.py; N > 1:
@@ -376,7 +381,8 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
             pipe = MerklePipeline(n, item_len, dev)
             k = pipe.k
         else:
-            pipe = P.ShardedMerklePipeline(n, item_len, sp, rank, world, dev, gather_log2=k, workspace=ws)
+            pipe = P.ShardedMerklePipeline(n, item_len, sp, rank, world, dev, gather_log2=k, workspace=ws,
+                                           timer=timer)
             pipe = pipe if pipe.ok else None
     if pipe is not None:
         # the pipelined root must equal the one-stream root of the same items
@@ -398,7 +404,7 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
         log(f"rank {rank}: pipelined (frontier {k}), the levels above the leaf pass on a side stream")
 
     def step():
-        return pipe.submit(items) if pipe is not None else step_one_stream()
+        return pipe.submit(items) if pipe is not None else step_one_stream(timer)
 
     for i in range(args.warmup):
         step()
@@ -415,9 +421,13 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
     torch.cuda.synchronize()
     sampler = ClockSampler(local)
     sampler.start()
+    if timer is not None:
+        timer.steps.clear()  # warmup steps were not marked (start_step not called)
     t0 = time.perf_counter()
     last_log = t0
     for i in range(args.steps):
+        if timer is not None:
+            timer.start_step()
         r = step()
         if time.perf_counter() - last_log > 30:
             log(f"step {i + 1}/{args.steps}")
@@ -435,6 +445,23 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
         if want is not None and root_hex != want:
             log(f"ERROR: root {root_hex} != golden {want}")
             status = 1
+
+    if timer is not None:
+        timer.stop()  # no marks after the timed region
+    phases = timer.record(world, dev if args.backend == "nccl" else None) if timer is not None else None
+    # N = 1: the latency of one complete Merkleization (one stream, not
+    # pipelined), hipEvents over >= 20 runs, after the timed region
+    single_tree_ms = None
+    if world == 1:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        runs = max(20, args.steps)
+        step_one_stream()
+        e0.record()
+        for _ in range(runs):
+            step_one_stream()
+        e1.record()
+        torch.cuda.synchronize()
+        single_tree_ms = e0.elapsed_time(e1) / runs
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     per_rank = None
@@ -477,7 +504,14 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
                        "root": root_hex, "root_matches_golden": None if golden_root(args.log2n, item_len) is None
                        else root_hex == golden_root(args.log2n, item_len),
                        "backend": backend_pg, "world_size": world_pg, "share_device": bool(args.share_device),
-                       "per_rank_ms_per_step_and_leaf_ms": per_rank},
+                       "per_rank_ms_per_step_and_leaf_ms": per_rank,
+                       # one complete Merkleization alone (N = 1: one stream, not pipelined)
+                       "single_tree_ms": single_tree_ms,
+                       # N > 1: rank 0's phases of the step and every rank's [leaf, nodes, gather,
+                       # finish] (parallel.PhaseTimer; pipelined: nodes/gather/finish overlap the
+                       # next leaf pass, so their sum exceeds ms_per_step)
+                       "phases_ms": phases["phases_ms"] if phases else None,
+                       "per_rank_phases_ms": phases["per_rank_phases_ms"] if phases else None},
             "roofline": {
                 "bound": "valu-int",
                 "kernel": kdesc,

@@ -31,22 +31,6 @@ namespace {
 #define MK_SIDE_PRIO 1
 #endif
 constexpr bool kSidePrio = MK_SIDE_PRIO != 0;  // library side/copy streams at high priority
-// Half-span tail (0 = off): of a leaf pass of 4 x MK_HALF_TAIL ..
-// MK_HALF_TAIL_MAX full 1024-window workgroups (a few rounds of the 1,280
-// resident slots: the per-rank shards of a multi-GPU tree), the last
-// MK_HALF_TAIL spans run as twice as many 512-window workgroups at the end
-// of the same grid (k_reduce a.half_from), so the straggling last round is
-// made of half-length workgroups.  One process, same box (profiles/r03f):
-// 2^25 leaf pass 1.2986 -> 1.2902 ms, the 8-GPU rank step 1.3526 -> 1.3330
-// ms; 2^26 and 2^28 unchanged (hence the upper bound).  Round 3 first tried
-// them as a second kernel on another stream (MK_TAIL_SPLIT): the two grids'
-// workgroups interleave and the 2^25 leaf pass got 5 % slower (profiles/r03e).
-#ifndef MK_HALF_TAIL
-#define MK_HALF_TAIL 256
-#endif
-#ifndef MK_HALF_TAIL_MAX
-#define MK_HALF_TAIL_MAX 8192
-#endif
 #ifndef MK_REC_KERNEL
 #define MK_REC_KERNEL 1
 #endif
@@ -355,17 +339,10 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
             HIPCHK(hipGetLastError());
         } else if (ps.wave) {
             a.wg_base = 0;
-            if (ps.w3) {
-                if (ps.leaf)
-                    launch_wave3<true>(ps.nt, ps.nwg, a, st);
-                else
-                    launch_wave3<false>(ps.nt, ps.nwg, a, st);
-            } else {
-                if (ps.leaf)
-                    hipLaunchKernelGGL((mk::k_wave2<true>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
-                else
-                    hipLaunchKernelGGL((mk::k_wave2<false>), dim3(ps.nwg), dim3(mk::kWaveThreads), 0, st, a);
-            }
+            if (ps.leaf)
+                launch_wave3<true>(ps.nt, ps.nwg, a, st);
+            else
+                launch_wave3<false>(ps.nt, ps.nwg, a, st);
             HIPCHK(hipGetLastError());
         } else {
             // The ragged workgroup(s) of a pass are latency-bound; when the pass
@@ -403,30 +380,17 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
             if (ps.nlock && !a.elem_len) {  // phase-locked leaf workgroups first: 4 spans each, levels == 3
                 a.wg_base = 0;
                 // persistent grid (one 1024-thread workgroup per CU) for whole trees, one group per
-                // workgroup for subtree shards (planner.cpp); k_leaf_lock (MK_LOCK_STAGE=0) always the latter
-                if (MK_LOCK_STAGE == 2)
-                    hipLaunchKernelGGL(mk::k_leaf_lock_sc,
-                                       dim3(ps.lock_persist ? std::min<uint64_t>(ps.nlock, lock_grid_cap(st)) : ps.nlock),
-                                       dim3(mk::kLockThreads), 0, st, a, ps.nlock);
-                else
-                    hipLaunchKernelGGL(mk::k_leaf_lock, dim3(ps.nlock), dim3(mk::kLockThreads), 0, st, a, ps.nlock);
+                // workgroup for subtree shards (planner.cpp)
+                hipLaunchKernelGGL(mk::k_leaf_lock_sc,
+                                   dim3(ps.lock_persist ? std::min<uint64_t>(ps.nlock, lock_grid_cap(st)) : ps.nlock),
+                                   dim3(mk::kLockThreads), 0, st, a, ps.nlock);
                 HIPCHK(hipGetLastError());
                 fast_base = ps.nlock * 4;
             }
             if (ps.nfast > fast_base) {
                 a.wg_base = fast_base;
                 const uint64_t nfast = ps.nfast - fast_base;
-                // half-span tail (MK_HALF_TAIL): the last T full spans as 2T
-                // half-length workgroups at the end of the same grid
-                const uint64_t T = (MK_HALF_TAIL > 0 && mk::kLeafSplit && ps.leaf && !a.elem_len && ps.ni == 2 &&
-                                    !ps.nlock && nfast >= 4ull * MK_HALF_TAIL && nfast <= MK_HALF_TAIL_MAX)
-                                       ? (uint64_t)MK_HALF_TAIL
-                                       : 0;
-                if (T) {
-                    a.half_from = nfast - T;
-                    hipLaunchKernelGGL((mk::k_reduce<true, true, 2>), dim3(nfast + T), dim3(kReduceThreads), 0, st,
-                                       a);
-                } else if (ps.leaf && a.elem_len)
+                if (ps.leaf && a.elem_len)
                     hipLaunchKernelGGL((mk::k_reduce_elem<true>), dim3(nfast), dim3(kReduceThreads), 0, st, a);
                 else if (ps.leaf && ps.ni == 1)
                     hipLaunchKernelGGL((mk::k_reduce<true, true, 1>), dim3(nfast), dim3(kReduceThreads), 0, st, a);
@@ -463,19 +427,8 @@ int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, 
         else
             hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
     } else if (kRecKernel && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0) {
-        // phase-locked records first (whole groups of 1024), the rest grid-stride
-        const uint64_t ng =
-            (MK_REC_LOCK && n >= MK_REC_LOCK_MIN && ((uintptr_t)d_in % 16) == 0) ? n / mk::kLockThreads : 0;
-        if (ng)
-            hipLaunchKernelGGL((mk::k_keccak_rec_lock<35>),
-                               dim3(std::min<uint64_t>({ng, (uint64_t)MK_REC_LOCK_GRID, lock_grid_cap(st)})),
-                               dim3(mk::kLockThreads), 0, st, (const uint2*)d_in, ng, (uint4*)d_out);
-        const uint64_t done = ng * mk::kLockThreads, rest = n - done;
-        if (rest)
-            hipLaunchKernelGGL((mk::k_keccak_rec<35>),
-                               dim3(std::min<uint64_t>(ceil_div(rest, mk::kRecThreads), mk::kRecGridMax)),
-                               dim3(mk::kRecThreads), 0, st, (const uint2*)d_in + done * 35, rest,
-                               (uint4*)d_out + 2 * done);
+        hipLaunchKernelGGL((mk::k_keccak_rec<35>), dim3(std::min<uint64_t>(ceil_div(n, mk::kRecThreads), mk::kRecGridMax)),
+                           dim3(mk::kRecThreads), 0, st, (const uint2*)d_in, n, (uint4*)d_out);
     } else if (msg_len % 8 == 0 && msg_len > 0 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0) {
         hipLaunchKernelGGL(mk::k_keccak_words, dim3(grid), dim3(256), 0, st, (const uint2*)d_in, n, msg_len / 8,
                            (uint4*)d_out);
@@ -1110,13 +1063,58 @@ int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from,
     return MK_OK;
 }
 
+// Levels 1..nlv of the batch build for the leaves [done, n) (level 0 holds
+// them; the levels of [0, done) are already built): the suffix of each level,
+// one k_trie_level launch per level.
+int trie_suffix_levels(void* d_levels, uint64_t cap, uint64_t n, uint64_t done, uint32_t nlv, hipStream_t st) {
+    for (uint32_t d = 0; d < nlv; ++d) {
+        const uint64_t c = mk::trie_count(n, d), plo = done >> (d + 1);
+        if (c <= 2 * plo) continue;  // nothing left at this level
+        hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(((c + 1) >> 1) - plo, 256)), dim3(256), 0, st,
+                           (const uint4*)(trie_level(d_levels, cap, d) + 2 * (2 * plo)), c - 2 * plo,
+                           trie_level(d_levels, cap, d + 1) + 2 * plo);
+        HIPCHK(hipGetLastError());
+    }
+    return MK_OK;
+}
+
 // Batch build front over an empty trie: leaf hashes into level 0, then
-// levels 1 .. d_to.  (Fusing levels 1-2 into the 280-B leaf kernel measured
-// no faster: profiles/r02d/rejected/ab_trie_leaves4.log.)
+// levels 1 .. d_to.  A whole trie in one call (d_to == depth) of 280-B
+// deposits at a 16-B aligned address: whole groups of the phase-locked
+// k_trie_rec_lock (leaves + levels 1..log2(DPT) in one launch), the rest (a
+// partial group) k_keccak_rec + k_trie_level.  A front whose top the caller
+// runs elsewhere (d_to < depth: pipeline.TriePipeline overlaps trie i's top
+// with trie i+1's front) keeps the free-running kernels: a locked workgroup
+// fills its CU, so the top could not co-run (one process, same box,
+// profiles/r04c-r04d: one trie 0.596 -> 0.582 ms locked, the stream of
+// tries 0.514 -> 0.604 ms/step).
 int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t* d_offs, uint64_t n,
                uint32_t fixed_len, uint32_t d_to, uint32_t depth, void* d_root32, hipStream_t st) {
-    TRY(dev_leaf_hashes(d_data, d_offs, n, fixed_len, trie_level(d_levels, cap, 0), st));
-    return trie_levels_range(d_levels, cap, n, 0, d_to, depth, d_root32, st);
+    constexpr uint32_t NT = MK_TRIE_LOCK_NT, DPT = MK_TRIE_LOCK_DPT;
+    constexpr uint32_t nlv = DPT == 8 ? 3 : DPT == 4 ? 2 : 1;
+    const uint64_t ng = (MK_TRIE_LOCK && !d_offs && fixed_len == 280 && ((uintptr_t)d_data % 16) == 0 &&
+                         n >= MK_TRIE_LOCK_MIN && d_to == depth && depth >= nlv)
+                            ? n / (NT * DPT)
+                            : 0;
+    if (!ng) {
+        TRY(dev_leaf_hashes(d_data, d_offs, n, fixed_len, trie_level(d_levels, cap, 0), st));
+        return trie_levels_range(d_levels, cap, n, 0, d_to, depth, d_root32, st);
+    }
+    if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
+    uint4* L[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (uint32_t d = 0; d <= nlv; ++d) L[d] = trie_level(d_levels, cap, d);
+    // persistent: every workgroup runs the same number of groups where possible
+    const uint64_t cap_wg = std::min<uint64_t>(MK_TRIE_LOCK_GRID, lock_grid_cap(st));
+    const uint64_t grid = ceil_div(ng, ceil_div(ng, cap_wg));
+    hipLaunchKernelGGL((mk::k_trie_rec_lock<NT, DPT>), dim3(grid), dim3(NT), 0, st, (const uint2*)d_data, ng, L[0],
+                       L[1], L[2], L[3]);
+    HIPCHK(hipGetLastError());
+    const uint64_t done = ng * NT * DPT;
+    if (done < n) {
+        TRY(dev_hash_batch((const uint8_t*)d_data + done * 280, n - done, 280, L[0] + 2 * done, st));
+        TRY(trie_suffix_levels(d_levels, cap, n, done, nlv, st));
+    }
+    return trie_levels_range(d_levels, cap, n, nlv, d_to, depth, d_root32, st);
 }
 
 int dev_trie_append(void* d_levels, uint64_t cap, uint64_t count, const void* d_data, const uint64_t* d_offs,
@@ -1494,9 +1492,14 @@ extern "C" {
 
 #define MK_STR2(x) #x
 #define MK_STR(x) MK_STR2(x)
+// MK_BUILD_FLAGS: the -D knobs of a variant build (Makefile `variant`), "default"
+// for the shipped library; __graft_entry__.build() refuses any other value
+#ifndef MK_BUILD_FLAGS
+#define MK_BUILD_FLAGS "default"
+#endif
 const char* mk_version(void) {
-    return "prysm_merkle 0.3 (gfx950; leaf_lock=" MK_STR(MK_LEAF_LOCK) " lock_stage=" MK_STR(MK_LOCK_STAGE)
-           " lock_bars=" MK_STR(MK_LOCK_BARS) " elem_lock=" MK_STR(MK_ELEM_LOCK) ")";
+    return "prysm_merkle 0.4 (gfx950; leaf_lock=" MK_STR(MK_LEAF_LOCK) " lock_bars=" MK_STR(MK_LOCK_BARS)
+           " elem_lock=" MK_STR(MK_ELEM_LOCK) " trie_lock=" MK_STR(MK_TRIE_LOCK) " flags=" MK_BUILD_FLAGS ")";
 }
 
 const char* mk_strerror(int code) {

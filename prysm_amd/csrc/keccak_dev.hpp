@@ -168,7 +168,7 @@ __device__ __forceinline__ void arho_all(const State& a, uint32_t (&blo)[25], ui
     (arho<Is>(a, blo, bhi), ...);
 }
 
-// BAR (phase-locked rounds, k_leaf_lock): an s_barrier between rho and chi.
+// BAR (phase-locked rounds, the locked kernels): an s_barrier between rho and chi.
 // In a 1024-thread workgroup (4 waves per SIMD, all of one workgroup) it
 // starts every round's chi with the 4 waves of each SIMD on the same
 // instruction.  The round's two long full-rate runs (chi + the next

@@ -175,7 +175,6 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
 #ifndef MK_LEAF_SPLIT_WAVES
 #define MK_LEAF_SPLIT_WAVES 5
 #endif
-template <bool BAR = false>
 __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w, uint4& d0, uint4& d1) {
     State s;
     uint4 v[9];
@@ -193,10 +192,7 @@ __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w
     const uint32_t t0 = v[8].z, t1 = v[8].w;
 #pragma unroll
     for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
-    if constexpr (BAR)
-        keccak_f_lock(s);
-    else
-        keccak_f(s);
+    keccak_f(s);
     asm volatile("" ::: "memory");  // block 2 loads stay after the permutation
     s.lo[0] ^= t0;
     s.hi[0] ^= t1;
@@ -226,14 +222,11 @@ __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w
     }
     s.lo[15] ^= 1u;  // byte 256 = byte 120 of block 1
     s.hi[16] ^= 0x80000000u;
-    if constexpr (BAR)
-        keccak_f_digest_lock(s);
-    else
-        keccak_f_digest(s);
+    keccak_f_digest(s);
     digest(s, d0, d1);
 }
 
-// K(L || R) of two 32-B nodes with phase-locked rounds (k_leaf_lock).
+// K(L || R) of two 32-B nodes with phase-locked rounds (the locked kernels).
 __device__ __forceinline__ void hash_node_lock(uint4 l0, uint4 l1, uint4 r0, uint4 r1, uint4& d0, uint4& d1) {
     State s;
     s.lo[0] = l0.x; s.hi[0] = l0.y; s.lo[1] = l0.z; s.hi[1] = l0.w;
@@ -374,14 +367,8 @@ k_reduce(ReduceArgs a) {
     __shared__ uint4 lds[2 * kSpan2];
     const uint32_t tid = threadIdx.x;
     const uint64_t wg = a.wg_base + blockIdx.x;
-    // a.half_from > 0 (FAST split leaf passes, MK_HALF_TAIL): workgroups from
-    // that index on take half a span (one window pair per thread), so the
-    // pass's last, straggling round is made of half-length workgroups; they
-    // are dispatched last because they have the highest indices
-    const bool half = kSplit && NI == 2 && a.half_from && wg >= a.half_from;
-    const uint64_t lo1 = half ? a.half_from * kSpan1 + (wg - a.half_from) * (kSpan1 / 2) : wg * kSpan1;
-    const int ni = half ? 1 : NI;
-    const uint64_t span1 = half ? kSpan1 / 2 : kSpan1;
+    const uint64_t lo1 = wg * kSpan1;
+    const uint64_t span1 = kSpan1;
     const uint64_t c1 = a.c1;
     const uint64_t m1 = (c1 - lo1) < span1 ? (c1 - lo1) : span1;
     const bool pair = a.levels >= 2 && (c1 > 1 || a.pad_at_one);
@@ -393,7 +380,7 @@ k_reduce(ReduceArgs a) {
         // the left window's digest waits in the thread's own level slot (the
         // pair node overwrites it), so no digest is held across a window
 #pragma unroll 1
-        for (int i = 0; i < ni; ++i) {
+        for (int i = 0; i < NI; ++i) {
             const uint32_t q = i * kReduceThreads + tid;
             const uint4* w = reinterpret_cast<const uint4*>(a.items) + (lo1 + 2 * (uint64_t)q) * 16;
             uint4 l0, l1, r0, r1, d0, d1;
@@ -472,40 +459,14 @@ k_reduce(ReduceArgs a) {
 // levels above the chunks (4 x 2 + 2 + 1 = 11 permutations, all locked) and
 // writes it: workgroup g covers windows [4096 g, 4096 g + 4096) of the pass,
 // i.e. the spans of k_reduce workgroups 4g..4g+3 run with a.levels == 3, and
-// writes their output nodes [1024 g, 1024 g + 1024).  No LDS, no divergence:
-// every wave runs the same number of barriers (the host launches only full
-// workgroups of full windows).  This direct-load form (MK_LOCK_STAGE=0) is
-// kept as the A/B reference of the staged default k_leaf_lock_sc below:
-// 2^28 leaf pass 8.54 vs 8.25 ms in one process (profiles/r03i/ab_lock4_28.jsonl).
-#ifndef MK_LOCK_NOLOAD
-#define MK_LOCK_NOLOAD 0  // probe only: windows read from a 16 MB wrap of the input (wrong roots)
-#endif
-__device__ __forceinline__ uint64_t lock_src(uint64_t node) { return MK_LOCK_NOLOAD ? (node & 0x3FFFull) : node; }
-__device__ __forceinline__ void leaf_lock_group(const ReduceArgs& a, uint64_t node) {
-    const uint4* w = reinterpret_cast<const uint4*>(a.items) + lock_src(node) * 64;
-    uint4 l0, l1, r0, r1, p0, p1;
-    hash_window256_split<true>(w, l0, l1);
-    hash_window256_split<true>(w + 16, r0, r1);
-    hash_node_lock(l0, l1, r0, r1, p0, p1);
-    hash_window256_split<true>(w + 32, l0, l1);
-    hash_window256_split<true>(w + 48, r0, r1);
-    hash_node_lock(l0, l1, r0, r1, l0, l1);
-    hash_node_lock(p0, p1, l0, l1, r0, r1);
-    uint4* out = reinterpret_cast<uint4*>(a.out);
-    out[2 * node] = r0;
-    out[2 * node + 1] = r1;
-}
-// grid = ngroups (one group of 1024 nodes per workgroup), or fewer workgroups
-// looping over the groups (persistent)
-__global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock(ReduceArgs a, uint64_t ngroups) {
-#pragma unroll 1
-    for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) leaf_lock_group(a, g * kLockThreads + threadIdx.x);
-}
-
-// The default form (MK_LOCK_STAGE=2): the windows staged in LDS by COALESCED
+// writes their output nodes [1024 g, 1024 g + 1024).  No divergence: every
+// wave runs the same number of barriers (the host launches only full
+// workgroups of full windows).  The windows are staged in LDS by COALESCED
 // DMA (global_load_lds_dwordx4: no VGPRs held while a load is in flight) on a
-// persistent grid.  In k_leaf_lock every wave waits for its window loads,
-// and a locked workgroup has no other workgroup on its CU to cover the wait;
+// persistent grid.  With direct per-lane loads (round 3's k_leaf_lock, 2^28
+// leaf pass 8.54 vs 8.25 ms, profiles/r03i/ab_lock4_28.jsonl; removed in
+// round 4) every wave waits for its window loads, and a locked workgroup has
+// no other workgroup on its CU to cover the wait;
 // its per-lane 16-B loads of lanes 1 KB apart also touch 64 lines per
 // instruction and every line 8 times.  Here phase A of window j (units
 // 0..8 = block 1) lands in the wave's LDS (10 KB per wave) during the
@@ -619,7 +580,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock_sc(ReduceArgs a, 
     const uint4* items = reinterpret_cast<const uint4*>(a.items);
     uint4* out = reinterpret_cast<uint4*>(a.out);
     // the wave's 64 nodes = 256 consecutive windows (64 KB); lane m's windows at m * 64 uint4
-    auto region = [&](uint64_t g) { return items + lock_src(g * kLockThreads + 64 * wave) * 64; };
+    auto region = [&](uint64_t g) { return items + (g * kLockThreads + 64 * wave) * 64; };
     uint64_t g = blockIdx.x;
     if (g < ngroups) lock_dma_a(Bw, region(g), lane);
     uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;  // the previous group's node, stored one group late
@@ -1031,170 +992,6 @@ __global__ __launch_bounds__(256) void k_elem_digests(const uint8_t* __restrict_
 template __global__ void k_elem_digests<true>(const uint8_t*, uint64_t, uint32_t, uint4*);
 template __global__ void k_elem_digests<false>(const uint8_t*, uint64_t, uint32_t, uint4*);
 
-// ----------------------------------------------------------------------------
-// Latency pass with two lanes per state (keccak_dev.hpp, mk::pair): lane pair
-// (2k, 2k+1) owns node k; the even lane carries the low 32-bit halves of the
-// Keccak lanes, the odd lane the high halves.  Nodes live in LDS as 8 dwords;
-// a lane touches dwords 2w + odd (w = 0..3) of every node.
-namespace {
-
-// K(L || R) or K(L || 0^128) on own halves (pair-uniform `padded`).
-__device__ __forceinline__ void hash_pair2(const uint32_t (&l)[4], const uint32_t (&r)[4], bool padded, bool odd,
-                                           uint32_t (&d)[4]) {
-    pair::Half s;
-    pair::zero(s);
-#pragma unroll
-    for (int w = 0; w < 4; ++w) s.v[w] = l[w];
-    if (!padded) {
-#pragma unroll
-        for (int w = 0; w < 4; ++w) s.v[4 + w] = r[w];
-    }
-    const int nperm = padded ? 2 : 1;
-#pragma unroll 1
-    for (int k = 0; k < nperm; ++k) {
-        if (k == nperm - 1) {
-            if (!odd) {
-                if (padded)
-                    s.v[3] ^= 1u;
-                else
-                    s.v[8] ^= 1u;
-            } else {
-                s.v[16] ^= 0x80000000u;
-            }
-        }
-        pair::keccak_f(s, odd);
-    }
-#pragma unroll
-    for (int w = 0; w < 4; ++w) d[w] = s.v[w];
-}
-
-// full 256-B window on own halves (two blocks, one keccak_f copy)
-__device__ __forceinline__ void hash_window2(const uint32_t* __restrict__ w32, bool odd, uint32_t (&d)[4]) {
-    pair::Half s;
-    pair::zero(s);
-    const uint32_t p = odd ? 1u : 0u;
-#pragma unroll 1
-    for (int b = 0; b < 2; ++b) {
-        if (b == 0) {
-#pragma unroll
-            for (int w = 0; w < 17; ++w) s.v[w] ^= w32[2 * w + p];
-        } else {
-#pragma unroll
-            for (int w = 0; w < 15; ++w) s.v[w] ^= w32[2 * (17 + w) + p];
-            if (!odd)
-                s.v[15] ^= 1u;
-            else
-                s.v[16] ^= 0x80000000u;
-        }
-        pair::keccak_f(s, odd);
-    }
-#pragma unroll
-    for (int w = 0; w < 4; ++w) d[w] = s.v[w];
-}
-
-}  // namespace
-
-template <bool LEAF>
-__global__ __launch_bounds__(kWaveThreads) void k_wave2(ReduceArgs a) {
-    __shared__ uint32_t lds[8 * kWave2Span];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t k = tid >> 1;          // node slot of this lane pair
-    const bool odd = (tid & 1u) != 0;
-    const uint32_t p = odd ? 1u : 0u;
-    const uint64_t wg = a.wg_base + blockIdx.x;
-    const uint64_t lo1 = wg * kWave2Span;
-    const uint64_t c1 = a.c1;
-    const uint64_t m1 = (c1 - lo1) < kWave2Span ? (c1 - lo1) : kWave2Span;
-    if (k < m1) {
-        const uint64_t j = lo1 + k;
-        uint32_t d[4];
-        if constexpr (LEAF) {
-            if (j < a.c1_full) {
-                hash_window2(reinterpret_cast<const uint32_t*>(a.items) + j * 64, odd, d);
-            } else {  // ragged window: both lanes run the full-state sponge
-                uint4 d0, d1;
-                first_level_generic<true>(a, j, d0, d1);
-                d[0] = odd ? d0.y : d0.x;
-                d[1] = odd ? d0.w : d0.z;
-                d[2] = odd ? d1.y : d1.x;
-                d[3] = odd ? d1.w : d1.z;
-            }
-        } else {
-            const uint32_t* in = reinterpret_cast<const uint32_t*>(a.items);
-            uint32_t l[4], r[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int w = 0; w < 4; ++w) l[w] = in[16 * j + 2 * w + p];
-            if (a.cin == 1 && !a.pad_at_one) {  // single node: it is the root
-#pragma unroll
-                for (int w = 0; w < 4; ++w) d[w] = l[w];
-            } else {
-                const bool padded = !(2 * j + 1 < a.cin);
-                if (!padded) {
-#pragma unroll
-                    for (int w = 0; w < 4; ++w) r[w] = in[16 * j + 8 + 2 * w + p];
-                }
-                hash_pair2(l, r, padded, odd, d);
-            }
-        }
-#pragma unroll
-        for (int w = 0; w < 4; ++w) lds[8 * k + 2 * w + p] = d[w];
-    }
-    __syncthreads();
-    uint64_t c = c1, m = m1;
-    int left = a.finalize ? 64 : (int)a.levels - 1;
-    int done = 0;
-    while (left > 0 && (c > 1 || a.pad_at_one)) {
-        const uint64_t mn = (m + 1) / 2;
-        const bool act = k < mn;
-        uint32_t l[4], r[4] = {0, 0, 0, 0};
-        bool padded = false;
-        if (act) {
-            padded = !(2 * (uint64_t)k + 1 < m);
-#pragma unroll
-            for (int w = 0; w < 4; ++w) l[w] = lds[16 * k + 2 * w + p];
-            if (!padded) {
-#pragma unroll
-                for (int w = 0; w < 4; ++w) r[w] = lds[16 * k + 8 + 2 * w + p];
-            }
-        }
-        __syncthreads();
-        if (act) {
-            uint32_t d[4];
-            hash_pair2(l, r, padded, odd, d);
-#pragma unroll
-            for (int w = 0; w < 4; ++w) lds[8 * k + 2 * w + p] = d[w];
-        }
-        __syncthreads();
-        c = (c + 1) / 2;
-        m = mn;
-        --left;
-        ++done;
-    }
-    uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
-    if (a.finalize) {
-        if (k == 0) {  // K(root || le64(n) || 0^24) on lanes 0/1
-            pair::Half s;
-            pair::zero(s);
-#pragma unroll
-            for (int w = 0; w < 4; ++w) s.v[w] = lds[2 * w + p];
-            s.v[4] = odd ? (uint32_t)(a.n_items >> 32) : (uint32_t)a.n_items;
-            if (!odd)
-                s.v[8] ^= 1u;
-            else
-                s.v[16] ^= 0x80000000u;
-            pair::keccak_f(s, odd);
-#pragma unroll
-            for (int w = 0; w < 4; ++w) out[2 * w + p] = s.v[w];
-        }
-    } else if (k < m) {
-        const uint64_t lo_out = lo1 >> done;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) out[8 * (lo_out + k) + 2 * w + p] = lds[8 * k + 2 * w + p];
-    }
-}
-
-template __global__ void k_wave2<true>(ReduceArgs);
-template __global__ void k_wave2<false>(ReduceArgs);
 
 // ----------------------------------------------------------------------------
 // Node pass of the latency form with BIT-INTERLEAVED lane pairs
@@ -2276,115 +2073,143 @@ __global__ __launch_bounds__(kRecThreads, MK_REC_WAVES) void k_keccak_rec(const 
 }
 template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 
-// Phase-locked records (MK_REC_LOCK): the k_leaf_lock_sc scheme for n
-// messages of NW 8-B words (8-B aligned, NW odd: 280-B deposits), n a
-// multiple of 1024 (the host runs the rest with k_keccak_rec).  1024-thread
-// workgroups, one per CU, persistent; lane m of wave w hashes record
-// g * 1024 + 64 w + m of group g with phase-locked permutations.  Each full
-// rate block b (136 B) of the wave's 64 records is staged in the wave's 9 KB
-// of LDS by 16-B DMA: record m's block starts 8 ((m + b) & 1) bytes into a
-// 16-B unit and ends inside the 9th, so the 9 covering units of every record
-// are flattened U = 9 m + u (9 instructions per block; consecutive lanes on
-// consecutive units of one record, where a record read as 8-B words per lane
-// touches one line per lane and every line ~16 times), and lane m reads its
-// 17 words back at byte 144 m + 8 ((m + b) & 1).  Block b + 1 is in flight
-// during block b's permutation, the next record's block 0 during this
-// record's last two; the tail words (< 17) are loaded per lane one group ahead.
-template <int NW>
-__device__ __forceinline__ void rec_dma_block(uint4* Bw, const uint8_t* __restrict__ region, int b, uint32_t lane) {
-    asm volatile("" : "+v"(lane));  // recompute the offsets here (see lock_dma_c)
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-        const uint32_t U = 64u * i + lane;
-        const uint32_t m = U / 9, u = U - m * 9;
-        const uint32_t start = m * (8 * NW) + 136 * b;  // block b of record m (8-B aligned)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(region + (start & ~15u) + 16 * u),
-                                         (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, 0);
-    }
-}
-
-template <int NW>
-__global__ __launch_bounds__(kLockThreads, 1) void k_keccak_rec_lock(const uint2* __restrict__ in, uint64_t ngroups,
-                                                                     uint4* __restrict__ out) {
-    constexpr int NFULL = NW / 17;  // full rate blocks (DMA-staged)
-    constexpr int NTAIL = NW % 17;  // words of the last block (per-lane loads)
-    static_assert(NFULL >= 1 && NTAIL < 16, "layout");
-    static_assert((8 * NW) % 16 == 8, "records alternate 16-B alignment");
-    __shared__ uint4 buf[kLockThreads / 64][9 * 64];
+// Phase-locked deposit-trie front (MK_TRIE_LOCK): the leaf hashes of 280-B
+// deposits (deposit_trie.go:32, Hash(depositData)) AND the trie levels above
+// them up to the node over DPT leaves (deposit_trie.go:33-38), in one launch.
+// Every thread owns DPT consecutive deposits: 3 permutations each (2 full
+// rate blocks + the 8-B tail), then DPT - 1 node permutations, all phase-
+// locked (two s_barriers per round) -- DPT = 4: 15 permutations,
+// levels 1-2.  Thread t of group g holds deposits DPT (g NT + t) + i; it
+// writes its leaves and nodes to levels 0..log2(DPT) of the trie (all kept:
+// GenerateMerkleBranch reads them), so the 2^20-leaf round trip through HBM
+// and the level launches of the free-running form go away.
+// Staging (the k_leaf_lock_sc scheme): block b of slot i of the wave's 64
+// lanes is DMA'd into the wave's 9 KB of LDS, the 9 16-B units covering each
+// lane's 136-B block flattened U = 9 m + u (consecutive lanes on consecutive
+// units of one deposit).  Deposit DPT m + i starts 8 (i & 1) bytes into a
+// 16-B unit (280 = 17.5 x 16, DPT even), so lane m's 17 words sit at byte
+// 144 m + 8 ((i + b) & 1) of the image.  Block 1 of slot i is in flight
+// during block 0's permutation, block 0 of slot i + 1 (or of the next group)
+// during block 1's; the 8-B tail words are loaded per lane one slot ahead.
+// Whole groups only (the host runs the rest with k_keccak_rec + k_trie_level).
+#ifndef MK_TRIE_LOCK_AUX
+#define MK_TRIE_LOCK_AUX 0  // global_load_lds policy of the deposit DMA (2 = nt)
+#endif
+template <uint32_t NT, int DPT>
+__global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict__ in, uint64_t ngroups,
+                                                         uint4* __restrict__ L0, uint4* __restrict__ L1,
+                                                         uint4* __restrict__ L2, uint4* __restrict__ L3) {
+    constexpr uint32_t NW = 35;  // 8-B words per deposit
+    constexpr int NLV = DPT == 8 ? 3 : DPT == 4 ? 2 : 1;
+    static_assert(DPT == 2 || DPT == 4 || DPT == 8, "deposits per thread");
+    __shared__ uint4 buf[NT / 64][9 * 64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint4* Bw = buf[wave];
     const uint2* Bw2 = reinterpret_cast<const uint2*>(Bw);
-    auto region = [&](uint64_t g) {
-        return reinterpret_cast<const uint8_t*>(in + (g * kLockThreads + 64 * wave) * NW);
-    };
-    // the tail words of a group are loaded with its block-0 DMA (one group
-    // ahead), and a group's digest is stored after the next group's first
-    // wait, so no wait covers a load or store issued just before it
-    uint2 tail[NTAIL > 0 ? NTAIL : 1];
-    auto load_tail = [&](uint64_t g) {
-        const uint64_t rec = g * kLockThreads + threadIdx.x;
+    uint4* const lv[4] = {L0, L1, L2, L3};
+    auto first = [&](uint64_t g) { return (g * NT + 64 * wave) * DPT; };  // lane 0's first deposit
+    auto dma = [&](uint64_t g, int i, int b) {
+        const uint8_t* region = reinterpret_cast<const uint8_t*>(in + first(g) * NW);
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));  // recompute the offsets here (see lock_dma_c)
 #pragma unroll
-        for (int w = 0; w < NTAIL; ++w) tail[w] = in[rec * NW + 17 * NFULL + w];
+        for (int k = 0; k < 9; ++k) {
+            const uint32_t U = 64u * k + ln;
+            const uint32_t m = U / 9, u = U - m * 9;
+            const uint32_t start = (DPT * m + i) * (8 * NW) + 136 * b;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(region + (start & ~15u) + 16 * u),
+                                             (__attribute__((address_space(3))) void*)(Bw + 64 * k), 16, 0,
+                                             MK_TRIE_LOCK_AUX);
+        }
+    };
+    auto tail = [&](uint64_t g, int i) { return in[(first(g) + DPT * lane + i) * NW + 34]; };
+    // a node is stored after the next slot's first wait, so no wait covers a
+    // store issued just before it (stores count in vmcnt)
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+    uint4* qp = nullptr;
+    auto flush = [&] {
+        if (qp) {
+            qp[0] = q0;
+            qp[1] = q1;
+        }
     };
     uint64_t g = blockIdx.x;
+    uint2 tnext = make_uint2(0, 0);
     if (g < ngroups) {
-        rec_dma_block<NW>(Bw, region(g), 0, lane);
-        load_tail(g);
+        dma(g, 0, 0);
+        tnext = tail(g, 0);
     }
-    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
-    uint64_t qi = 0;
-    bool pend = false;
 #pragma unroll 1
     for (; g < ngroups; g += gridDim.x) {
-        const uint64_t rec = g * kLockThreads + threadIdx.x;
         const uint64_t gn = g + gridDim.x;
-        uint2 tl[NTAIL > 0 ? NTAIL : 1];
-        State s;
-        zero(s);
+        const uint64_t r0 = first(g) + DPT * lane;  // this lane's first deposit (leaf index)
+        uint4 kl0[NLV], kl1[NLV];                   // the pending left node of each level
 #pragma unroll
-        for (int b = 0; b < NFULL; ++b) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block b (and the tail words) landed
-            if (b == 0) {
-#pragma unroll
-                for (int w = 0; w < NTAIL; ++w) tl[w] = tail[w];
-                if (pend) {
-                    out[2 * qi] = q0;
-                    out[2 * qi + 1] = q1;
-                }
-            }
+        for (int i = 0; i < DPT; ++i) {
+            State s;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 0 and the tail word landed
+            flush();
+            qp = nullptr;
+            const uint2 tl = tnext;
 #pragma unroll
             for (int w = 0; w < 17; ++w) {
-                const uint2 v = Bw2[18 * lane + ((lane + b) & 1) + w];
+                const uint2 v = Bw2[18 * lane + (i & 1) + w];
+                s.lo[w] = v.x;
+                s.hi[w] = v.y;
+            }
+#pragma unroll
+            for (int w = 17; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: block 1 may land
+            dma(g, i, 1);
+            keccak_f_lock(s);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 1 landed
+#pragma unroll
+            for (int w = 0; w < 17; ++w) {
+                const uint2 v = Bw2[18 * lane + ((i + 1) & 1) + w];
                 s.lo[w] ^= v.x;
                 s.hi[w] ^= v.y;
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: the next block may land
-            if (b + 1 < NFULL) {
-                rec_dma_block<NW>(Bw, region(g), b + 1, lane);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (i + 1 < DPT) {
+                dma(g, i + 1, 0);
+                tnext = tail(g, i + 1);
             } else if (gn < ngroups) {
-                rec_dma_block<NW>(Bw, region(gn), 0, lane);
-                load_tail(gn);
+                dma(gn, 0, 0);
+                tnext = tail(gn, 0);
             }
             keccak_f_lock(s);
-        }
+            s.lo[0] ^= tl.x;  // word 34, then the domain pad byte (word 35 = lane 1)
+            s.hi[0] ^= tl.y;
+            s.lo[1] ^= 1u;
+            s.hi[16] ^= 0x80000000u;
+            keccak_f_digest_lock(s);
+            uint4 d0, d1;
+            digest(s, d0, d1);
+            // fold: level l + 1 gets a node once slot i closes a pair at level l
+            uint4* dst = lv[0] + 2 * (r0 + i);
 #pragma unroll
-        for (int w = 0; w < NTAIL; ++w) {
-            s.lo[w] ^= tl[w].x;
-            s.hi[w] ^= tl[w].y;
+            for (int l = 0; l <= NLV; ++l) {
+                if (l == NLV || ((i >> l) & 1) == 0) {
+                    if (l < NLV) {
+                        kl0[l] = d0;
+                        kl1[l] = d1;
+                    }
+                    q0 = d0;  // stored after the next wait
+                    q1 = d1;
+                    qp = dst;
+                    break;
+                }
+                dst[0] = d0;  // covered by the node permutation below
+                dst[1] = d1;
+                hash_node_lock(kl0[l], kl1[l], d0, d1, d0, d1);
+                dst = lv[l + 1] + 2 * ((r0 + i) >> (l + 1));
+            }
         }
-        s.lo[NTAIL] ^= 1u;  // domain pad byte right after the message
-        s.hi[16] ^= 0x80000000u;
-        keccak_f_digest_lock(s);
-        digest(s, q0, q1);
-        qi = rec;
-        pend = true;
     }
-    if (pend) {
-        out[2 * qi] = q0;
-        out[2 * qi + 1] = q1;
-    }
+    flush();
 }
-template __global__ void k_keccak_rec_lock<35>(const uint2*, uint64_t, uint4*);
+template __global__ void k_trie_rec_lock<MK_TRIE_LOCK_NT, MK_TRIE_LOCK_DPT>(const uint2*, uint64_t, uint4*, uint4*,
+                                                                           uint4*, uint4*);
 
 // ----------------------------------------------------------------------------
 // Deposit trie level: node j = K(in[2j] || (2j+1 < cin ? in[2j+1] : 0^32)),

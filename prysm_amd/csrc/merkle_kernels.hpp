@@ -22,8 +22,7 @@ struct StructSpec {                 // flat fixed-layout record (hash.go:141-159
     uint32_t nfields, rec_len, msg_len;
 };
 
-// The leaf kernel's split window form (merkle_kernels.hip); the half-span
-// tail (ReduceArgs::half_from) exists only in it.
+// The free-running leaf kernel's split window form (merkle_kernels.hip).
 #ifndef MK_LEAF_SPLIT
 #define MK_LEAF_SPLIT 1
 #endif
@@ -34,11 +33,7 @@ __global__ void k_reduce(ReduceArgs a);
 // workgroup -> 1024 nodes three levels above the chunks.
 constexpr uint32_t kLockThreads = 1024;
 constexpr uint64_t kLockWindows = 4 * kLockThreads;
-__global__ void k_leaf_lock(ReduceArgs a, uint64_t ngroups);
 __global__ void k_leaf_lock_sc(ReduceArgs a, uint64_t ngroups);  // coalesced LDS-DMA staging, persistent grid
-#ifndef MK_LOCK_STAGE
-#define MK_LOCK_STAGE 2  // 0: k_leaf_lock (direct per-lane loads), 2: k_leaf_lock_sc (coalesced LDS-DMA)
-#endif
 #ifndef MK_LOCK_DMA_ROUND
 #define MK_LOCK_DMA_ROUND 12  // k_leaf_lock_sc: round of a window's second permutation after which the next block 1 is fetched
 #endif
@@ -67,8 +62,6 @@ __global__ void k_struct_split(const uint8_t* rec, uint64_t n, StructSpec sp, ui
 #define MK_STRUCT_SPLIT_MAX_N 32768
 #endif
 constexpr uint64_t kStructSplitMaxN = MK_STRUCT_SPLIT_MAX_N;  // k_struct_split at or below (0: never)
-template <bool LEAF>
-__global__ void k_wave2(ReduceArgs a);
 template <uint32_t NT, bool LEAF>
 __global__ void k_wave3(ReduceArgs a);
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
@@ -83,20 +76,24 @@ __global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
 __global__ void k_keccak_words(const uint2* in, uint64_t n, uint32_t nwords, uint4* out);
 template <int NW>
 __global__ void k_keccak_rec(const uint2* in, uint64_t n, uint4* out);
-template <int NW>
-__global__ void k_keccak_rec_lock(const uint2* in, uint64_t ngroups, uint4* out);  // n = 1024 * ngroups records
-// Off by default: one 2^20 trie builds 3 % faster with it, but the C5 bench's
-// stream of tries overlaps each trie's latency-bound top with the next
-// trie's leaves, and a CU-filling locked workgroup leaves no room for that
-// overlap (0.514 -> 0.612 ms/step, profiles/r03m/bench_c5.json).
-#ifndef MK_REC_LOCK
-#define MK_REC_LOCK 0
+// Phase-locked deposit-trie front: leaves + levels 1..log2(DPT) of a trie of
+// 280-B deposits, ngroups * NT * DPT deposits (the host runs the rest).
+template <uint32_t NT, int DPT>
+__global__ void k_trie_rec_lock(const uint2* in, uint64_t ngroups, uint4* L0, uint4* L1, uint4* L2, uint4* L3);
+#ifndef MK_TRIE_LOCK
+#define MK_TRIE_LOCK 1
 #endif
-#ifndef MK_REC_LOCK_GRID
-#define MK_REC_LOCK_GRID 256  // < 256 leaves CUs free for work overlapping the leaves (a stream of tries)
+#ifndef MK_TRIE_LOCK_NT
+#define MK_TRIE_LOCK_NT 1024  // threads per workgroup (one workgroup per CU)
 #endif
-#ifndef MK_REC_LOCK_MIN
-#define MK_REC_LOCK_MIN (1u << 18)  // records: at least one group per CU
+#ifndef MK_TRIE_LOCK_DPT
+#define MK_TRIE_LOCK_DPT 4  // deposits per thread: 4 = levels 1-2 fused, 8 = levels 1-3
+#endif
+#ifndef MK_TRIE_LOCK_GRID
+#define MK_TRIE_LOCK_GRID 256  // persistent grid cap
+#endif
+#ifndef MK_TRIE_LOCK_MIN
+#define MK_TRIE_LOCK_MIN (1u << 18)  // deposits: at least one group per CU
 #endif
 
 #ifndef MK_REC_THREADS

@@ -10,9 +10,8 @@ constexpr uint32_t kReduceThreads = 256;             // 4 waves
 constexpr uint64_t kReduceSpan1 = 4 * kReduceThreads;  // first-level nodes per workgroup
 constexpr uint64_t kReduceSpan2 = kReduceSpan1 / 2;    // level-2 nodes per workgroup (LDS)
 constexpr uint32_t kMaxPassLevels = 5;               // levels per non-final pass (1024 -> 64)
-constexpr uint32_t kWaveThreads = 64;                // k_wave2: one wave per workgroup
-constexpr uint32_t kWave2Span = kWaveThreads / 2;    // two lanes per state: 32 nodes per wave
-constexpr uint32_t kWave2Levels = 6;                 // first level + 5 in-wave levels (32 -> 1)
+constexpr uint32_t kWaveThreads = 64;                // smallest k_wave3 workgroup: one wave
+constexpr uint32_t kWave2Span = kWaveThreads / 2;    // lane pairs per wave: 32 nodes (dev_finish takes <= 64 roots)
 constexpr uint32_t kMidThreads = 1024;               // largest k_wave3: 16 waves, 512 lane pairs, 10 levels
 // Wide leaf passes of full windows run the phase-locked k_leaf_lock_sc
 // (merkle_kernels.hip, planner.cpp) instead of k_reduce's fused form.
@@ -39,7 +38,6 @@ struct ReduceArgs {
     uint64_t wg_base;      // workgroup index offset of this launch
     uint32_t in_ilv;       // k_wave3: input nodes are bit-interleaved lane pairs
     uint32_t out_ilv;      // k_wave3: write bit-interleaved output nodes
-    uint64_t half_from;    // k_reduce FAST leaf (split form): workgroups >= this take half a span (0 = none)
     uint32_t elem_len;     // LEAF, k_reduce_elem: `items` are n elements of elem_len bytes and the
                            // tree's 32-B items are their digests K(le32(elem_len) || element)
 };

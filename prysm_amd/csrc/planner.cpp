@@ -37,12 +37,8 @@ mk_call* swap_call(mk_call* c) {
 }
 
 // ---- configuration (compile-time knobs; A/B variants via the Makefile) ----------
-// latency passes: k_wave2 (two lanes per state, lo/hi halves) or, by default,
-// k_wave3 (bit-interleaved lane pairs, one state per wave at the top)
-#ifndef MK_WAVE3
-#define MK_WAVE3 1
-#endif
-constexpr bool kWave3 = MK_WAVE3 != 0;  // node latency passes bit-interleaved (k_wave3)
+// latency passes: k_wave3 (bit-interleaved lane pairs, one state per wave at
+// the top; round 4 removed the lo/hi-halves k_wave2 it replaced in round 1)
 #ifndef MK_NODE_WAVE_MAX_LOG2
 #define MK_NODE_WAVE_MAX_LOG2 17
 #endif
@@ -54,10 +50,6 @@ constexpr uint64_t kNodeWaveMaxC1 = 1ull << MK_NODE_WAVE_MAX_LOG2;
 #define MK_NODE_WAVE_WGS 256
 #endif
 constexpr uint64_t kNodeWaveWgs = MK_NODE_WAVE_WGS;
-#ifndef MK_LEAF_WAVE3
-#define MK_LEAF_WAVE3 1
-#endif
-constexpr bool kLeafWave3 = MK_LEAF_WAVE3 != 0;  // narrow leaf passes bit-interleaved too
 #ifndef MK_LEAF_WAVE_MAX_LOG2
 #define MK_LEAF_WAVE_MAX_LOG2 17
 #endif
@@ -89,7 +81,7 @@ constexpr uint32_t kW3MaxNt = MK_W3_MAX_NT < kMidThreads ? MK_W3_MAX_NT : kMidTh
 #endif
 constexpr uint64_t kSpreadLeafMaxC1 = MK_SPREAD_LEAF_MAX_LOG2 < 0 ? 0 : 1ull << MK_SPREAD_LEAF_MAX_LOG2;
 constexpr uint64_t kSpreadSpan = 16;  // windows per k_spread_leaf workgroup
-// Phase-locked leaf pass (k_leaf_lock, merkle_kernels.hip): wide leaf passes
+// Phase-locked leaf pass (k_leaf_lock_sc, merkle_kernels.hip): wide leaf passes
 // of full 256-B windows fold 3 levels (windows -> node pairs -> one node per
 // 4 windows) in 1024-thread workgroups whose Keccak rounds hold an s_barrier;
 // the next (node) pass takes the levels the leaf pass used to fuse in LDS.
@@ -102,7 +94,7 @@ constexpr bool kLeafLock = MK_LEAF_LOCK != 0;  // plan_types.hpp
 #endif
 constexpr uint64_t kLeafLockMinC1 = 1ull << MK_LEAF_LOCK_MIN_LOG2;  // windows (first-level nodes)
 constexpr uint32_t kLockLevels = 3;
-constexpr uint64_t kLockSpans = 4;  // k_reduce spans (1024 windows) per k_leaf_lock workgroup
+constexpr uint64_t kLockSpans = 4;  // k_reduce spans (1024 windows) per k_leaf_lock_sc workgroup
 
 uint32_t ilog2(uint64_t v) {
     uint32_t l = 0;
@@ -187,11 +179,11 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         }
         uint64_t c = c1;
         const bool sp = leaf && c1 <= kSpreadLeafMaxC1;
-        const bool wave = sp || c1 <= (leaf || !kWave3 ? kLeafWaveMaxC1 : kNodeWaveMaxC1);
-        const bool w3 = !sp && kWave3 && wave && (!leaf || kLeafWave3);
+        const bool wave = sp || c1 <= (leaf ? kLeafWaveMaxC1 : kNodeWaveMaxC1);
+        const bool w3 = !sp && wave;
         // k_wave3: the smallest workgroup (64..1024 threads, 2 per pair) that
         // keeps the pass within ~256 workgroups, one per CU
-        uint32_t nt = w3 ? kWaveThreads : (wave ? kWaveThreads : kReduceThreads);
+        uint32_t nt = w3 ? kWaveThreads : kReduceThreads;
         if (w3) {
             while (nt < kW3MaxNt && ceil_div(c1, nt / 2) > kNodeWaveWgs) nt *= 2;
             if (kTopOneWg)  // the last <= 512 pairs in one workgroup: one launch to the root
@@ -203,10 +195,10 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         const uint32_t ni = (!wave && leaf && (c1 < kReduceNi2MinC1 || leaf_ni1)) ? 1 : 2;
         if (sp) nt = 1024;
         const uint64_t span = sp ? kSpreadSpan
-                            : w3 ? nt / 2 : wave ? kWave2Span : (uint64_t)2 * ni * kReduceThreads;
+                            : w3 ? nt / 2 : (uint64_t)2 * ni * kReduceThreads;
         const bool final_pass = c1 <= span;
         const uint32_t max_lv = sp ? 1 + ilog2(kSpreadSpan)
-                              : w3 ? 1 + ilog2(nt / 2) : wave ? kWave2Levels : kMaxPassLevels;
+                              : w3 ? 1 + ilog2(nt / 2) : kMaxPassLevels;
         uint32_t lv = final_pass ? remaining : std::min<uint32_t>(max_lv, remaining);
         const bool lock = kLeafLock && leaf && !wave && !final_pass && !leaf_ni1 && ni == 2 &&
                           a.c1_full >= kLeafLockMinC1 && remaining > kLockLevels &&

@@ -103,8 +103,14 @@ def merkle_hash(items: torch.Tensor, n: int, item_len: int, out: torch.Tensor = 
     return out
 
 
-def tree_hash_bytes_list_workspace(n: int, elem_len: int, device) -> torch.Tensor:
+def tree_hash_bytes_list_workspace(n: int, elem_len: int, device, aligned16: bool = True) -> torch.Tensor:
+    """Workspace of mk_dev_ssz_tree_hash_bytes_list.  The library's query
+    plans for 16-B aligned elements; elements at another address take the
+    two-phase form (element digests in the workspace first), which needs
+    n x 32 more bytes (rounded to 256)."""
     nb = _lib.load().mk_ssz_tree_hash_bytes_list_workspace_bytes(n, elem_len)
+    if not aligned16:
+        nb += -(-n * 32 // 256) * 256
     return torch.empty(max(nb, 256), dtype=torch.uint8, device=device)
 
 
@@ -117,7 +123,7 @@ def tree_hash_bytes_list(elems: torch.Tensor, n: int, elem_len: int, out: torch.
     if out is None:
         out = torch.empty(32, dtype=torch.uint8, device=elems.device)
     if ws is None:
-        ws = tree_hash_bytes_list_workspace(n, elem_len, elems.device)
+        ws = tree_hash_bytes_list_workspace(n, elem_len, elems.device, aligned16=elems.data_ptr() % 16 == 0)
     _lib.invoke("mk_dev_ssz_tree_hash_bytes_list", _p(elems), n, elem_len, _p(out), _p(ws), ws.numel(),
                 _stream(elems.device), device=_dev(elems))
     return out

@@ -88,6 +88,94 @@ class SlotRing:
         self._i += 1
 
 
+class PhaseTimer:
+    """Per-step phases of one rank's sharded merkleHash step, for the N-GPU
+    bench record: marks recorded on the stream that runs each
+    phase (torch.cuda.Event = hipEvents on the GPU; the host clock on the
+    CPU), read once the timed steps are synchronised.
+
+      leaf    leaf0 -> leaf1     the rank's leaf pass (one-stream step: the
+                                 leaf pass and the node passes to the frontier,
+                                 one library call)
+      nodes   nodes0 -> nodes1   the node passes to the frontier (pipelined
+                                 step, side stream; 0 in the one-stream step)
+      gather  -> gather1         the frontier all-gather, from the end of the
+                                 phase before it
+      finish  gather1 -> finish1 rank 0's finisher (0 on the other ranks)
+
+    In the one-stream step the phases run back to back and sum to the step;
+    in the pipelined step nodes + gather + finish run on a side stream beside
+    the next leaf pass, so the step is the leaf pass plus whatever of the
+    side work does not hide."""
+
+    PHASES = ("leaf", "nodes", "gather", "finish")
+
+    def __init__(self, cuda: bool):
+        self.cuda = cuda
+        self.steps = []
+        self._cur = None
+
+    def start_step(self) -> None:
+        self._cur = {}
+        self.steps.append(self._cur)
+
+    def stop(self) -> None:
+        """No marks until the next start_step (steps outside the timed region)."""
+        self._cur = None
+
+    def mark(self, name: str, stream=None) -> None:
+        if self._cur is None:
+            return
+        if self.cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+            self._cur[name] = ev
+        else:
+            import time
+
+            self._cur[name] = time.perf_counter()
+
+    def _ms(self, a, b) -> float:
+        if self.cuda:
+            return a.elapsed_time(b)
+        return (b - a) * 1e3
+
+    def phases_ms(self) -> dict:
+        """Average ms per phase over the recorded steps (call after the
+        streams that ran them are synchronised)."""
+        tot = dict.fromkeys(self.PHASES, 0.0)
+        for m in self.steps:
+            if "leaf0" in m and "leaf1" in m:
+                tot["leaf"] += self._ms(m["leaf0"], m["leaf1"])
+            if "nodes0" in m and "nodes1" in m:
+                tot["nodes"] += self._ms(m["nodes0"], m["nodes1"])
+            prev = m.get("nodes1", m.get("leaf1"))
+            if prev is not None and "gather1" in m:
+                tot["gather"] += self._ms(prev, m["gather1"])
+            if "gather1" in m and "finish1" in m:
+                tot["finish"] += self._ms(m["gather1"], m["finish1"])
+        n = max(len(self.steps), 1)
+        return {k: v / n for k, v in tot.items()}
+
+    def record(self, world: int, device=None, group=None) -> dict:
+        """This rank's phases plus every rank's (all-gathered; a collective:
+        every rank calls it), for the bench JSON: {"phases_ms": {...,
+        "sum": ...}, "per_rank_phases_ms": [[leaf, nodes, gather, finish],
+        ...]}."""
+        mine = self.phases_ms()
+        vec = torch.tensor([mine[k] for k in self.PHASES], dtype=torch.float64,
+                           device=device if device is not None else "cpu")
+        if world > 1:
+            allv = torch.empty(world * len(self.PHASES), dtype=torch.float64, device=vec.device)
+            dist.all_gather_into_tensor(allv, vec, group=group)
+            rows = allv.view(world, len(self.PHASES)).tolist()
+        else:
+            rows = [vec.tolist()]
+        out = {k: round(v, 4) for k, v in mine.items()}
+        out["sum"] = round(sum(mine.values()), 4)
+        return {"phases_ms": out, "per_rank_phases_ms": [[round(x, 4) for x in r] for r in rows]}
+
+
 @dataclass
 class ShardPlan:
     height: int
@@ -113,7 +201,8 @@ def sharded_merkle_hash(local_items: torch.Tensor, n_total: int, item_len: int, 
                         gather_buf: Optional[torch.Tensor] = None,
                         finish_stream=None, frontier_log2: int = 0,
                         frontier_fn: Optional[Callable] = None,
-                        finish_nodes_fn: Optional[Callable] = None) -> Optional[torch.Tensor]:
+                        finish_nodes_fn: Optional[Callable] = None,
+                        timer: Optional[PhaseTimer] = None) -> Optional[torch.Tensor]:
     """Returns the 32-byte merkleHash root on rank 0 (None elsewhere).
 
     ``local_items`` holds this rank's items [begin[rank], begin[rank+1]).
@@ -129,7 +218,8 @@ def sharded_merkle_hash(local_items: torch.Tensor, n_total: int, item_len: int, 
     instead of its root (``frontier_fn(items, sn, il, h, k, pad)`` returns a
     32<<k-byte buffer holding the shard's nodes first;
     ``finish_nodes_fn(level, count, n_total)`` finishes); gather_buf then
-    holds world << k nodes."""
+    holds world << k nodes.  ``timer``: PhaseTimer marks of the step's
+    phases (leaf, gather, finish)."""
     if subtree_fn is None or full_fn is None or finish_fn is None:
         from . import device as D
         subtree_fn = subtree_fn or D.merkle_subtree
@@ -142,6 +232,9 @@ def sharded_merkle_hash(local_items: torch.Tensor, n_total: int, item_len: int, 
             return full_fn(local_items, n_total, item_len)
         return None
     k = frontier_log2 if 0 < frontier_log2 < sp.height else 0
+    cur = torch.cuda.current_stream(dev) if local_items.is_cuda else None
+    if timer is not None:
+        timer.mark("leaf0", cur)
     if k:
         if frontier_fn is None or finish_nodes_fn is None:
             from . import device as D
@@ -160,6 +253,8 @@ def sharded_merkle_hash(local_items: torch.Tensor, n_total: int, item_len: int, 
         root = subtree_fn(local_items, hi - lo, item_len, sp.height, True)
     else:
         root = torch.zeros(32, dtype=torch.uint8, device=dev)
+    if timer is not None:
+        timer.mark("leaf1", cur)
     if gather_buf is None:
         gather_buf = torch.empty(world * root.numel(), dtype=torch.uint8, device=dev)
     if finish_stream is not None:  # the previous finish still reads gather_buf
@@ -172,6 +267,8 @@ def sharded_merkle_hash(local_items: torch.Tensor, n_total: int, item_len: int, 
         gather_buf.copy_(host)
     else:
         dist.all_gather_into_tensor(gather_buf, root, group=group)
+    if timer is not None:
+        timer.mark("gather1", cur)
     if rank == 0:
         if k:
             last = sp.nonempty - 1
@@ -186,8 +283,14 @@ def sharded_merkle_hash(local_items: torch.Tensor, n_total: int, item_len: int, 
             # next allocation on the current stream meanwhile
             gather_buf.record_stream(finish_stream)
             with torch.cuda.stream(finish_stream):
-                return fin()
-        return fin()
+                r = fin()
+                if timer is not None:
+                    timer.mark("finish1", finish_stream)
+                return r
+        r = fin()
+        if timer is not None:
+            timer.mark("finish1", cur)
+        return r
     return None
 
 
@@ -231,8 +334,9 @@ class ShardedMerklePipeline:
                  gather_log2: int = 10, leaf_levels: int = 5, group=None,
                  frontier_fn: Optional[Callable] = None, node_frontier_fn: Optional[Callable] = None,
                  finish_nodes_fn: Optional[Callable] = None, workspace=None, slots: int = 3,
-                 wait_every: int = 1):
+                 wait_every: int = 1, timer: Optional[PhaseTimer] = None):
         self.n_total, self.item_len, self.sp = n_total, item_len, sp
+        self.timer = timer
         self.rank, self.world, self.group = rank, world, group
         self.device = torch.device(device)
         h = sp.height
@@ -279,9 +383,14 @@ class ShardedMerklePipeline:
         cur = torch.cuda.current_stream(self.device) if self.cuda else None
         slot = self._ring.acquire(cur)  # side work of `slots` trees back is done
         level = None
+        t = self.timer
+        if t is not None:
+            t.mark("leaf0", cur)
         if self.sn:
             level = self.frontier_fn(local_items, self.sn, self.item_len, self.sp.height, self.k_leaf, True,
                                      self.levels[slot])
+        if t is not None:
+            t.mark("leaf1", cur)
         if self.cuda:
             self.side.wait_stream(cur)
             with torch.cuda.stream(self.side):
@@ -296,10 +405,15 @@ class ShardedMerklePipeline:
 
     def _top(self, level, slot):
         blk = self.blocks[slot]
+        t, side = self.timer, (self.side if self.cuda else None)
+        if t is not None:
+            t.mark("nodes0", side)
         if level is not None:
             fr = self.node_frontier_fn(level, self.leaf_count, self.k_leaf, self.k, True, blk)
             if fr.data_ptr() != blk.data_ptr():  # an injected step may return its own buffer
                 blk[:fr.numel()].copy_(fr)
+        if t is not None:
+            t.mark("nodes1", side)
         # (an empty shard sends its zero block; only the counted nodes are read)
         g = self.gathered[slot]
         if blk.is_cuda and dist.get_backend(self.group) == "gloo":  # one-GPU rehearsal: gloo gathers host tensors
@@ -308,8 +422,13 @@ class ShardedMerklePipeline:
             g.copy_(host)
         else:
             dist.all_gather_into_tensor(g, blk, group=self.group)
+        if t is not None:
+            t.mark("gather1", side)
         if self.rank == 0:
-            return self.finish_nodes_fn(g, self.count, self.n_total, self.outs[slot])
+            r = self.finish_nodes_fn(g, self.count, self.n_total, self.outs[slot])
+            if t is not None:
+                t.mark("finish1", side)
+            return r
         return None
 
 

@@ -163,6 +163,9 @@ class DeviceStateHasher:
         D.struct_roots(records, n, 160, VALIDATOR_FIELDS, out=self.roots, ws=self.msg_ws)
         self.ev_roots.record(cur)
         self.side.wait_event(self.ev_roots)
+        # balances is read on the side stream after this call returns: keep the
+        # caching allocator from reusing its block on the caller's stream meanwhile
+        balances.record_stream(self.side)
         with torch.cuda.stream(self.side):
             D.merkle_hash(balances, n, 8, out=self.pair[32:], ws=self.bal_ws)
             self.ev_bal.record(self.side)

@@ -167,6 +167,111 @@ def test_pipelined_sharded_root_equals_full_root(world, n, k, leaf, slots):
     assert root == O.merkle_hash_gen(n, 32, SEED)
 
 
+def _phase_worker(rank, world, port, n, q, pipelined):
+    """bench.py's N-rank phase record on the CPU path: K steps of the sharded
+    step (one-stream or pipelined) with the oracle as the injected compute, a
+    host-clock parallel.PhaseTimer, and the record bench.py prints."""
+    import time
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from oracle import oracle as O
+        from prysm_amd import parallel as P
+
+        k, leaf = 3, 5
+        sp = P.plan(n, 32, world, plan_fn=_plan_cpu)
+        lo, hi = sp.items(rank)
+        local = torch.from_numpy(O.splitmix_bytes(n * 32, SEED)[lo * 32:hi * 32].copy())
+
+        def level_below(kk):  # the shard's level kk below its root = roots of its 2^kk sub-shards
+            cnt = P.frontier_count(hi - lo, 32, sp.height, kk)
+            nodes = b"".join(O.merkle_subtree_gen(n, 32, SEED, (rank << kk) + j, sp.height - kk)
+                             for j in range(cnt))
+            return torch.frombuffer(bytearray(nodes), dtype=torch.uint8)
+
+        def node_frontier(level, cnt, hh, kk, pad, out):
+            nodes = [bytes(level[32 * i:32 * i + 32].numpy()) for i in range(cnt)]
+            for _ in range(hh - kk):
+                if len(nodes) % 2:
+                    nodes = nodes + [bytes(128)]
+                nodes = [O.keccak256(nodes[i] + nodes[i + 1]) for i in range(0, len(nodes), 2)]
+            return torch.frombuffer(bytearray(b"".join(nodes)), dtype=torch.uint8)
+
+        def finish_nodes(g, count, nt):
+            level = [bytes(g[32 * i:32 * i + 32].numpy()) for i in range(count)]
+            while len(level) > 1:
+                if len(level) % 2:
+                    level = level + [bytes(128)]
+                level = [O.keccak256(level[i] + level[i + 1]) for i in range(0, len(level), 2)]
+            return torch.frombuffer(bytearray(O.keccak256(level[0] + nt.to_bytes(8, "little") + bytes(24))),
+                                    dtype=torch.uint8)
+
+        timer = P.PhaseTimer(cuda=False)
+        if pipelined:
+            pl = P.ShardedMerklePipeline(
+                n, 32, sp, rank, world, "cpu", gather_log2=k, leaf_levels=leaf,
+                frontier_fn=lambda it, sn, il, h, kk, pad, out: level_below(kk),
+                node_frontier_fn=node_frontier, finish_nodes_fn=lambda g, c, nt, out: finish_nodes(g, c, nt),
+                timer=timer)
+            assert pl.ok
+            step = lambda: pl.submit(local)  # noqa: E731
+        else:
+            step = lambda: P.sharded_merkle_hash(  # noqa: E731
+                local, n, 32, sp, rank, world, subtree_fn=lambda *a: None, full_fn=lambda *a: None,
+                finish_fn=lambda *a: None, frontier_log2=k, frontier_fn=lambda it, sn, il, h, kk, pad: level_below(kk),
+                finish_nodes_fn=finish_nodes, timer=timer)
+        step()  # warmup: not marked
+        dist.barrier()
+        steps = 6
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            timer.start_step()
+            r = step()
+        dist.barrier()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        timer.stop()
+        rec = timer.record(world)
+        if rank == 0:
+            rec["ms_per_step"] = ms
+            rec["root"] = bytes(r.numpy())
+            q.put(rec)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_bench_phase_record_world2(pipelined):
+    """bench.py's N > 1 record breaks the step into phases (leaf pass, node
+    passes to the frontier, all-gather, finisher; parallel.PhaseTimer) for
+    rank 0 and every rank.  On the CPU path (gloo, world 2, oracle compute)
+    the phases run back to back, so they sum to within 10 % of the step."""
+    from oracle import oracle as O
+
+    n = 1 << 15
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_phase_worker, args=(r, 2, port, n, q, pipelined)) for r in range(2)]
+    for p in procs:
+        p.start()
+    rec = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert rec["root"] == O.merkle_hash_gen(n, 32, SEED)
+    ph = rec["phases_ms"]
+    assert set(ph) == {"leaf", "nodes", "gather", "finish", "sum"}
+    assert len(rec["per_rank_phases_ms"]) == 2 and all(len(r) == 4 for r in rec["per_rank_phases_ms"])
+    assert rec["per_rank_phases_ms"][0] == [ph[k] for k in ("leaf", "nodes", "gather", "finish")]
+    assert ph["leaf"] > 0 and ph["finish"] > 0 and rec["per_rank_phases_ms"][1][3] == 0
+    assert (ph["nodes"] > 0) == pipelined
+    assert abs(ph["sum"] - rec["ms_per_step"]) <= 0.1 * rec["ms_per_step"], (ph, rec["ms_per_step"])
+
+
 @pytest.mark.parametrize("n,item_len,world", [(4099, 32, 8), (1000, 8, 3), (41 * 4 + 3, 32, 4), (5, 32, 8),
                                               (100, 200, 8), (10**6, 32, 8), (1 << 28, 32, 8)])
 def test_python_plan_matches_c_planner(n, item_len, world):

@@ -546,10 +546,12 @@ def test_dev_struct_roots(gpu, layout, n):
 
 
 @pytest.mark.parametrize("n", [1 << 25, (1 << 25) + 12_345, (1 << 24) + 7 * 4096])
-def test_merkle_hash_half_span_tail(gpu, n):
-    """Leaf passes of 1,024..8,192 full workgroups end in half-span
-    workgroups (MK_HALF_TAIL, k_reduce a.half_from): the per-rank shard sizes
-    of a multi-GPU tree.  Unsharded and as an 8-shard frontier level."""
+def test_merkle_hash_shard_sized_leaf_pass(gpu, n):
+    """The per-rank shard sizes of a multi-GPU tree (2^24..2^25 items): the
+    phase-locked leaf pass (k_leaf_lock_sc, 4 spans per workgroup) plus the
+    k_reduce spans after the last whole group.  Unsharded and as an 8-shard
+    frontier level.  (Round 3's half-span tail of the free-running leaf pass
+    could not run beside the locked pass and was removed in round 4.)"""
     import torch
 
     from oracle import oracle as O

@@ -92,6 +92,10 @@ def test_tree_hash_unaligned_32b_fused_size(gpu):
         out = D.tree_hash_bytes_list(buf[off:], n, 32, ws=ws)
         torch.cuda.synchronize()
         assert bytes(out.cpu().numpy()) == want, off
+        # the default workspace covers the two-phase form's digest array
+        out = D.tree_hash_bytes_list(buf[off:], n, 32)
+        torch.cuda.synchronize()
+        assert bytes(out.cpu().numpy()) == want, ("default ws", off)
 
 
 def test_tree_hash_workspace_too_small(gpu):

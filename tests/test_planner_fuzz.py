@@ -14,7 +14,7 @@ from tests.test_distributed import _plan_cpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-# the default build, and one with the phase-locked leaf pass (k_leaf_lock)
+# the default build, and one with the phase-locked leaf pass (k_leaf_lock_sc)
 # enabled down to 2^12 windows so the fuzz sizes reach it
 @pytest.fixture(scope="module", params=[(), ("-DMK_LEAF_LOCK=1", "-DMK_LEAF_LOCK_MIN_LOG2=12")],
                 ids=["default", "leaf_lock"])

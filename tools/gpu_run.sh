@@ -7,6 +7,8 @@
 #   bash tools/gpu_run.sh TAG STEP [STEP ...]
 #
 #   tests                   pytest -m gpu (every GPU test) + __graft_entry__.smoke()
+#   ktests                  the same under rocprofv3 --kernel-trace --stats, then
+#                           tools/kernel_coverage.py: kernels compiled but never launched
 #   pytest:PATH             one test file / node id
 #   bench:CFG               bench.py --config CFG (c1 c2 c3 c4 c4tree c5), JSON line kept
 #   profile:CFG:KERNEL      rocprofv3 kernel-trace stats + separate PMC passes of CFG's
@@ -34,6 +36,14 @@ for step in "$@"; do
       tail -1 $O/pytest_gpu.log
       timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
       tail -1 $O/smoke.log ;;
+    ktests)
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $O/ktests -o run --output-format csv -- \
+        python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+      tail -1 $O/pytest_gpu.log
+      timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+      tail -1 $O/smoke.log
+      python3 tools/kernel_coverage.py $O/ktests > $O/kernel_coverage.json; tail -12 $O/kernel_coverage.json ;;
     pytest)
       timeout -k 10 600 python -u -m pytest "$a" -x -v --timeout 200 --timeout-method thread \
         > $O/$name.log 2>&1 || { tail -30 $O/$name.log; exit 1; }
