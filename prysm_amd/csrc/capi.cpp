@@ -843,7 +843,8 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
     if (kStructReg && layout && nb == 3 && nraw == 6) {
         if (MK_STRUCT_LOCK && vec16 && validator_layout(sp) && n >= (1u << 18))  // phase-locked, partial last group
             hipLaunchKernelGGL(mk::k_struct_lock, dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), lock_grid_cap(st))),
-                               dim3(mk::kLockThreads), 0, st, (const uint8_t*)d_rec, n, (uint4*)d_roots);
+                               dim3(mk::kLockThreads), 0, st, (const uint8_t*)d_rec, n, (uint4*)d_roots, 0u,
+                               (uint4*)nullptr);
         else
             hipLaunchKernelGGL((mk::k_struct_reg<3, 6>), dim3(ceil_div(n, mk::kStructThreads)),
                                dim3(mk::kStructThreads), 0, st, (const uint8_t*)d_rec, n, sp, vec16 ? 1u : 0u,
@@ -894,6 +895,38 @@ uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 #endif
 constexpr uint64_t kH2dChunks = MK_H2D_CHUNKS;
 constexpr uint64_t kH2dMinChunk = MK_H2D_MIN_CHUNK;
+
+// The registry list root with the merkleHash leaf pass fused into the
+// phase-locked struct kernel (k_struct_lock gpw > 0): whole ValidatorRecord
+// registries of >= 2^18 records at a 16-B aligned address.  The kernel writes
+// the roots and the level-1 windows; the node passes and the length mix-in
+// finish from the windows (dev_finish_nodes: the same odd rule at every
+// level, hash.go:225-237).  false: not this layout / size (caller takes the
+// two-launch path).
+#ifndef MK_STRUCT_WIN
+#define MK_STRUCT_WIN 1
+#endif
+bool struct_win_ok(const void* d_rec, uint64_t n, const mk::StructSpec& sp) {
+    if (!MK_STRUCT_WIN || !MK_STRUCT_LOCK || !kStructReg || n < (1u << 18)) return false;
+    if (((uintptr_t)d_rec % 16) != 0 || sp.rec_len % 16 != 0 || !validator_layout(sp)) return false;
+    for (uint32_t f = 0; f < sp.nfields; ++f)
+        if (sp.kind[f] == MK_FIELD_BYTES && (sp.off[f] % 16 || sp.off[f] + ((sp.len[f] + 15) & ~15u) > sp.rec_len))
+            return false;
+    return true;
+}
+
+int dev_struct_list_root_win(const void* d_rec, uint64_t n, void* d_roots, void* d_wins, void* d_out32,
+                             void* d_ws, uint64_t ws_bytes, hipStream_t st) {
+    const uint64_t ngroups = ceil_div(n, mk::kLockThreads);
+    const uint64_t cap = lock_grid_cap(st);
+    const uint32_t gpw = (uint32_t)ceil_div(ngroups, cap);  // contiguous groups per workgroup
+    hipLaunchKernelGGL(mk::k_struct_lock, dim3(ceil_div(ngroups, gpw)), dim3(mk::kLockThreads), 0, st,
+                       (const uint8_t*)d_rec, n, (uint4*)d_roots, gpw, (uint4*)d_wins);
+    HIPCHK(hipGetLastError());
+    const uint64_t c1 = ceil_div(n, 8);  // windows: ceil(ceil(n / 4) / 2) chunk pairs
+    if (ws_bytes < finish_ws_bytes(c1)) return fail(MK_ENOMEM, "workspace too small for the registry top");
+    return dev_finish_nodes(d_wins, c1, n, d_out32, d_ws, ws_bytes, st);
+}
 
 uint64_t struct_list_ws(uint64_t n, const mk::StructSpec& sp) {
     Plan p;
@@ -1821,6 +1854,9 @@ int mk_dev_ssz_struct_list_root(mk_call* call, const void* d_records, uint64_t n
     uint8_t* roots = ws + align256(n * sp.msg_len);
     uint8_t* mws = roots + align256(32 * n);
     hipStream_t st = (hipStream_t)stream;
+    if (struct_win_ok(d_records, n, sp))  // the windows go where the two-launch path keeps its messages
+        return S.done(dev_struct_list_root_win(d_records, n, roots, msg, d_out32, mws,
+                                               ws_bytes - (uint64_t)(mws - ws), st));
     rc = launch_struct_roots(d_records, n, sp, msg, roots, st);
     if (rc) return S.done(rc);
     return S.done(dev_merkle_hash(roots, n, 32, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), st));

@@ -1773,8 +1773,18 @@ template __global__ void k_struct_reg<3, 6>(const uint8_t*, uint64_t, StructSpec
 // struct-message permutations).
 __device__ constexpr uint32_t kValOff[9] = {0, 48, 80, 112, 120, 128, 136, 144, 152};
 __device__ constexpr uint32_t kValLen[9] = {48, 32, 32, 8, 8, 8, 8, 8, 8};
+//
+// gpw > 0 (the list root, mk_dev_ssz_struct_list_root): workgroup b takes the
+// CONTIGUOUS groups [gpw b, gpw b + gpw) instead of striding over the grid,
+// and after its last group hashes the level-1 windows of the registry's
+// merkleHash (hash.go:194-239 over the 32-B roots: 8 roots = 2 chunks per
+// window) from the roots it has just written -- one window per lane on waves
+// 0..(gpw*2 - 1), free-running (the other waves have left), into `wins`.  That
+// replaces the merkleHash leaf pass, a latency-bound pass over the whole
+// roots array.
 __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* __restrict__ rec, uint64_t n,
-                                                                 uint4* __restrict__ roots) {
+                                                                 uint4* __restrict__ roots, uint32_t gpw,
+                                                                 uint4* __restrict__ wins) {
     constexpr uint32_t kRecLen = 160, kRw = kRecLen / 4, kNinstr = kRecLen / 16;
     __shared__ uint32_t buf[kLockThreads / 64][64 * kRw];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -1794,13 +1804,16 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
                                              kSideAux);
         }
     };
-    uint64_t g = blockIdx.x;
-    if (g < ngroups) dma(g);
+    const uint64_t g_begin = gpw ? (uint64_t)blockIdx.x * gpw : blockIdx.x;
+    const uint64_t g_end = gpw ? (g_begin + gpw < ngroups ? g_begin + gpw : ngroups) : ngroups;
+    const uint64_t g_step = gpw ? 1 : gridDim.x;
+    uint64_t g = g_begin;
+    if (g < g_end) dma(g);
     uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;  // the previous group's root, stored after the next wait
     uint64_t qi = 0;
     bool pend = false;
 #pragma unroll 1
-    for (; g < ngroups; g += gridDim.x) {
+    for (; g < g_end; g += g_step) {
         uint32_t* R = Bw + lane * kRw;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's records have landed
         if (pend && qi < n) {
@@ -1843,7 +1856,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
         for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
         const uint32_t t0 = R[kValOff[3] / 4 + 10], t1 = R[kValOff[3] / 4 + 11];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // record read: the next group's copy may land
-        if (g + gridDim.x < ngroups) dma(g + gridDim.x);
+        if (g + g_step < g_end) dma(g + g_step);
         keccak_f_lock(s);
         s.lo[0] ^= t0;
         s.hi[0] ^= t1;
@@ -1857,6 +1870,48 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     if (pend && qi < n) {
         roots[2 * qi] = q0;
         roots[2 * qi + 1] = q1;
+    }
+    if (!wins || g_begin >= g_end) return;
+    // the workgroup's roots are in L2 (written above; this CU never read those
+    // lines, and its L1 was invalidated at dispatch): every wave's stores
+    // complete, then one window per lane
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint64_t r0 = g_begin * kLockThreads, r1 = g_end * kLockThreads < n ? g_end * kLockThreads : n;
+    const uint64_t w0 = r0 / 8, nw = (r1 - r0 + 7) / 8;
+#pragma unroll 1
+    for (uint64_t j = threadIdx.x; j < nw; j += kLockThreads) {
+        const uint64_t w = w0 + j;
+        uint4 d0, d1;
+        if (8 * w + 8 <= n) {
+            hash_window256(roots + 16 * w, d0, d1);
+        } else {  // the ragged last window: r roots, one chunk + 0^128 when r <= 4 (hash.go:225-228)
+            const uint32_t r = (uint32_t)(n - 8 * w);
+            const uint32_t nw = 4 * r, len = 32 * r + (r <= 4 ? 128u : 0u);  // 160..256 B: two blocks
+            const uint2* p = reinterpret_cast<const uint2*>(roots + 16 * w);
+            State s;
+            zero(s);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+#pragma unroll
+                for (int k = 0; k < 17; ++k) {
+                    const uint32_t q = 17 * b + k;
+                    uint2 v = q < nw ? p[q] : make_uint2(0, 0);
+                    if (q == len / 8) v.x ^= 1u;  // domain pad (len % 8 == 0)
+                    s.lo[k] ^= v.x;
+                    s.hi[k] ^= v.y;
+                }
+                if (b == 0) {
+                    keccak_f(s);
+                } else {
+                    s.hi[16] ^= 0x80000000u;
+                    keccak_f_digest(s);
+                }
+            }
+            digest(s, d0, d1);
+        }
+        wins[2 * w] = d0;
+        wins[2 * w + 1] = d1;
     }
 }
 

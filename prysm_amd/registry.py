@@ -132,18 +132,26 @@ class DeviceStateHasher:
     ~90 us of the struct kernel's issue slots for a tree that needs ~10 us of
     them (profiles/r03b: k_struct_reg 441 us alone, 533 us beside it)."""
 
-    def __init__(self, n: int, device):
+    def __init__(self, n: int, device, fused: bool = True):
+        """``fused``: the registry root in one library call
+        (mk_dev_ssz_struct_list_root: for >= 2^18 ValidatorRecords the struct
+        kernel also hashes the registry tree's level-1 windows, and the
+        balances tree starts at once beside it on the CUs its 245-workgroup
+        grid leaves free); False: round 3's two-call schedule (struct roots
+        alone, then the two trees side by side)."""
         import torch
 
         from . import device as D
 
-        self.n, self.dev = n, device
+        self.n, self.dev, self.fused = n, device, fused
         L = _lib.load()
         f = _fields(VALIDATOR_FIELDS)
         self.roots = torch.empty(max(32, 32 * n), dtype=torch.uint8, device=device)
         self.msg_ws = torch.empty(max(256, n * L.mk_ssz_struct_msg_len(f, len(VALIDATOR_FIELDS))), dtype=torch.uint8,
                                   device=device)
         self.reg_ws = D.merkle_workspace(n, 32, device)
+        self.list_ws = torch.empty(L.mk_ssz_struct_list_workspace_bytes(n, f, len(VALIDATOR_FIELDS)) + 256,
+                                   dtype=torch.uint8, device=device) if fused else None
         self.bal_ws = D.merkle_workspace(n, 8, device)
         self.pair = torch.empty(64, dtype=torch.uint8, device=device)  # reg_root || bal_root
         self.out = torch.empty(32, dtype=torch.uint8, device=device)
@@ -160,6 +168,17 @@ class DeviceStateHasher:
 
         n = self.n
         cur = torch.cuda.current_stream(self.dev)
+        if self.fused:
+            self.ev_roots.record(cur)  # the inputs are ready
+            self.side.wait_event(self.ev_roots)
+            balances.record_stream(self.side)
+            with torch.cuda.stream(self.side):
+                D.merkle_hash(balances, n, 8, out=self.pair[32:], ws=self.bal_ws)
+                self.ev_bal.record(self.side)
+            D.struct_list_root(records, n, 160, VALIDATOR_FIELDS, out=self.pair[:32], ws=self.list_ws)
+            cur.wait_event(self.ev_bal)
+            D.hash_batch(self.pair, 1, 64, out=self.out)
+            return self.out
         D.struct_roots(records, n, 160, VALIDATOR_FIELDS, out=self.roots, ws=self.msg_ws)
         self.ev_roots.record(cur)
         self.side.wait_event(self.ev_roots)

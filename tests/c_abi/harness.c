@@ -9,6 +9,13 @@
  *
  *   harness <threads> <rounds> <merkle_hex x8> <batch_hex x8> <trie_root_hex> <branch_hex> <many_hex x3>
  *   MK_INJECT_EHIP=1 harness inject
+ *   harness cgo <m0> <m1> <m2> <m5> <m10x16> <m10x32> <t0> <tz4> <t1x6>
+ *
+ * `cgo` replays the call sequences of INTEGRATION.md's Go wrappers exactly,
+ * including the pointers cgo passes for empty slices (ptr(b) == NULL when
+ * len(b) == 0) and every early-return branch of the Go code, against the
+ * reference's own vectors (shared/ssz/hash_test.go:80-90,151-178) and oracle
+ * fixtures (tests/golden/c_abi_fixture.json "cgo").
  *
  * `inject` runs with the library's failure-injection hook on: every compute
  * call must come back with MK_EHIP and the detail in its own mk_call (the
@@ -221,8 +228,107 @@ static int inject_check(void) {
     return bad;
 }
 
+/* ---- cgo replay (gpu/merkle) --------------------------- */
+/* ptr(b): cgo passes NULL for an empty Go slice */
+static const uint8_t* gptr(const uint8_t* b, size_t len) { return len ? b : NULL; }
+
+static int g_bad = 0;
+static void expect_root(const char* what, int rc, const mk_call* call, const uint8_t* out, const char* want) {
+    char h[65];
+    hex(out, h);
+    int ok = rc == MK_OK && call->code == MK_OK && strcmp(h, want) == 0;
+    printf("%-58s rc=%d %s\n", what, rc, ok ? "ok" : "MISMATCH");
+    if (!ok) {
+        printf("   got %s\n  want %s  (%s)\n", h, want, call->err);
+        g_bad = 1;
+    }
+}
+static void expect_rc(const char* what, int rc, const mk_call* call, int want_rc, const char* want_err) {
+    int ok = rc == want_rc && call->code == want_rc && (!want_err || strstr(call->err, want_err));
+    printf("%-58s rc=%d %s\n", what, rc, ok ? "ok" : "MISMATCH");
+    if (!ok) {
+        printf("   want rc %d '%s', err '%s'\n", want_rc, want_err ? want_err : "", call->err);
+        g_bad = 1;
+    }
+}
+
+/* merkle.MerkleHashFlat(items, n, itemLen): one mk_ssz_merkle_hash, ptr(items) */
+static int go_merkle_hash_flat(mk_call* call, const uint8_t* flat, size_t flat_len, uint64_t n, uint32_t item_len,
+                               uint8_t out[32]) {
+    call->device = -1;
+    return mk_ssz_merkle_hash(call, gptr(flat, flat_len), n, item_len, out);
+}
+
+static int cgo_replay(char** want) {
+    mk_call call;
+    uint8_t out[32];
+    memset(&call, 0, sizeof call);
+    /* ssz.merkleHash(list) -> MerkleHashFlat(flatten(list), len(list), len(list[0])) */
+    expect_root("merkleHash n=0 (flat=nil, itemLen 32)", go_merkle_hash_flat(&call, NULL, 0, 0, 32, out), &call,
+                out, want[0]);
+    const uint8_t one[2] = {1, 0}; /* []uint16{1}: le16 items */
+    expect_root("merkleHash n=1 (2-B item)", go_merkle_hash_flat(&call, one, 2, 1, 2, out), &call, out, want[1]);
+    const uint8_t two[4] = {1, 2, 3, 4};
+    expect_root("merkleHash n=2 ([0102 0304])", go_merkle_hash_flat(&call, two, 4, 2, 2, out), &call, out, want[2]);
+    uint8_t five[5 * 32];
+    fill(five, sizeof five, SEED_BASE + 0x400, 0);
+    expect_root("merkleHash n=5 (32-B items)", go_merkle_hash_flat(&call, five, sizeof five, 5, 32, out), &call, out,
+                want[3]);
+    uint8_t ten16[10 * 16], ten32[10 * 32];
+    for (int i = 0; i < 10; ++i) {
+        memset(ten16 + 16 * i, i + 1, 16);
+        memset(ten32 + 32 * i, i + 1, 32);
+    }
+    expect_root("merkleHash n=10 (16-B items)", go_merkle_hash_flat(&call, ten16, sizeof ten16, 10, 16, out), &call,
+                out, want[4]);
+    expect_root("merkleHash n=10 (32-B items)", go_merkle_hash_flat(&call, ten32, sizeof ten32, 10, 32, out), &call,
+                out, want[5]);
+    /* len(list[0]) == 0: every item empty, flat == nil, itemLen 0 (the
+     * reference divides by zero; the wrapper gets MK_EINVAL with that text) */
+    expect_rc("merkleHash len(list[0])==0 (flat=nil, n=3)", go_merkle_hash_flat(&call, NULL, 0, 3, 0, out), &call,
+              MK_EINVAL, "divide by zero");
+    /* merkle.TreeHashBytesList(flat, n, elemLen) */
+    call.device = -1;
+    expect_root("TreeHashBytesList n=0 (elems=nil)", mk_ssz_tree_hash_bytes_list(&call, NULL, 0, 32, out), &call, out,
+                want[6]);
+    expect_root("TreeHashBytesList elemLen=0 (elems=nil, n=4)", mk_ssz_tree_hash_bytes_list(&call, NULL, 4, 0, out),
+                &call, out, want[7]);
+    const uint8_t six[6] = {1, 2, 3, 4, 5, 6};
+    expect_root("TreeHashBytesList n=1 elemLen=6", mk_ssz_tree_hash_bytes_list(&call, six, 1, 6, out), &call, out,
+                want[8]);
+    /* merkle.MerkleHashMany with k == 0 returns before the call; the call
+     * itself must also be a no-op (no list, nil slices) */
+    int rc = mk_ssz_merkle_many(&call, NULL, NULL, NULL, NULL, 0, NULL);
+    expect_rc("MerkleHashMany k=0 (nil slices)", rc, &call, MK_OK, NULL);
+    /* merkle.HashBatch with n == 0 returns before the call; likewise a no-op */
+    rc = mk_hash_batch(&call, NULL, 0, 64, NULL);
+    expect_rc("HashBatch n=0 (nil slices)", rc, &call, MK_OK, NULL);
+    /* Trie.Append / SaveLogs of zero deposits: flat == nil, offs == [0] */
+    mk_trie* t = NULL;
+    rc = mk_deposit_trie_new(&call, 32, 0, &t);
+    expect_rc("NewTrie(32)", rc, &call, MK_OK, NULL);
+    if (rc == MK_OK) {
+        uint64_t offs0[1] = {0};
+        uint8_t r0[32], r1[32];
+        rc = mk_deposit_trie_root(&call, t, r0);
+        expect_rc("Trie.Root() empty", rc, &call, MK_OK, NULL);
+        rc = mk_deposit_trie_append(&call, t, NULL, offs0, 0);
+        expect_rc("Trie.Append(no deposits)", rc, &call, MK_OK, NULL);
+        rc = mk_deposit_trie_save_logs(&call, t, NULL, offs0, 0, NULL, NULL);
+        expect_rc("Trie.SaveLogs(no logs)", rc, &call, MK_OK, NULL);
+        rc = mk_deposit_trie_root(&call, t, r1);
+        int same_root = rc == MK_OK && memcmp(r0, r1, 32) == 0 && mk_deposit_trie_count(t) == 0;
+        printf("%-58s %s\n", "Trie root/count unchanged", same_root ? "ok" : "MISMATCH");
+        g_bad |= !same_root;
+        mk_deposit_trie_free(t);
+    }
+    printf(g_bad ? "FAIL: cgo replay\n" : "ok: cgo replay\n");
+    return g_bad;
+}
+
 int main(int argc, char** argv) {
     if (argc == 2 && strcmp(argv[1], "inject") == 0) return inject_check();
+    if (argc == 11 && strcmp(argv[1], "cgo") == 0) return cgo_replay(argv + 2);
     if (argc != 3 + NT_MAX + NT_MAX + 2 + 3) {
         fprintf(stderr, "usage: %s threads rounds merkle x8 batch x8 trie_root branch many x3\n", argv[0]);
         return 2;

@@ -131,3 +131,52 @@ def test_deposit_trie_lock_vs_oracle(gpu):
     k = n - 2
     branch = trie.GenerateMerkleBranch(k)
     assert branch[0] == levels[0][k ^ 1]
+
+
+# registry list root with the merkleHash leaf pass fused into the locked
+# struct kernel (k_struct_lock gpw > 0): contiguous groups per workgroup, then
+# one level-1 window per lane; the ragged last window (n % 8 != 0) hashes its
+# r roots, plus 0^128 when they fill one chunk only (r <= 4)
+@pytest.mark.parametrize("n", [
+    1 << 18,                 # 256 groups, one per workgroup, 128 windows each
+    (1 << 18) + 5,           # a partial group; last window 5 roots (two chunks)
+    (1 << 18) + 1024 + 3,    # last window 3 roots: one chunk + 0^128
+    1_000_000,               # C3: 977 groups, 4 per workgroup (245 workgroups)
+    (1 << 20) + 7 * 1024 + 1,
+])
+def test_struct_list_root_windows_vs_oracle(gpu, n):
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+    from prysm_amd import registry as R
+
+    reg = R.synthetic_registry(n, SEED + 47 + n % 13)
+    raw = reg.records.view(np.uint8).reshape(-1)
+    spec = [(k, o, l) for k, o, l in R.VALIDATOR_FIELDS]
+    roots = O.struct_roots(raw, n, 160, spec, nthreads=16)
+    want = O.merkle_hash_flat(roots.reshape(-1), n, 32, nthreads=16)
+    got = D.struct_list_root(torch.from_numpy(raw.copy()).to(gpu), n, 160, R.VALIDATOR_FIELDS)
+    torch.cuda.synchronize()
+    assert bytes(got.cpu().numpy()) == want
+
+
+def test_state_hasher_fused_and_two_call_agree(gpu):
+    """registry.DeviceStateHasher, fused (default) and round 3's two-call
+    schedule, against the host-buffer state root, three submits each."""
+    import torch
+
+    from prysm_amd import registry as R
+
+    n = (1 << 18) + 77
+    reg = R.synthetic_registry(n, SEED + 48)
+    bal = R.synthetic_balances(n, SEED + 48)
+    want = R.state_root(reg, bal)
+    rec = torch.from_numpy(reg.records.view(np.uint8).reshape(-1).copy()).to(gpu)
+    dbal = torch.from_numpy(bal.view(np.uint8).copy()).to(gpu)
+    for fused in (True, False):
+        h = R.DeviceStateHasher(n, gpu, fused=fused)
+        for _ in range(3):
+            out = h.submit(rec, dbal)
+        torch.cuda.synchronize()
+        assert bytes(out.cpu().numpy()) == want, fused

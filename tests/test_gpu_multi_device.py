@@ -200,6 +200,23 @@ def test_c_abi_harness_8_threads(gpu):
     assert "ok: 8 threads x 2 rounds" in r.stdout
 
 
+def test_c_abi_cgo_replay(gpu):
+    """`harness cgo`: the call sequences of INTEGRATION.md's Go wrappers
+    replayed from C99 exactly as cgo makes them (NULL for an empty Go slice),
+    every early-return branch included -- merkleHash over a flattened
+    [][]byte with n = 0, 1, 2, 5, 10 and len(list[0]) == 0;
+    TreeHashBytesList with n = 0 and elemLen = 0; MerkleHashMany with k = 0;
+    HashBatch with n = 0; trie Append / SaveLogs of nothing -- against the
+    reference's vectors (hash_test.go:80-81,151-178) and oracle fixtures."""
+    exe = _build_harness()
+    with open(os.path.join(ROOT, "tests", "golden", "c_abi_fixture.json")) as f:
+        cg = json.load(f)["cgo"]
+    keys = ["m0", "m1", "m2", "m5", "m10x16", "m10x32", "t0", "tz4", "t1x6"]
+    r = subprocess.run([exe, "cgo"] + [cg[k] for k in keys], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ok: cgo replay" in r.stdout and "MISMATCH" not in r.stdout
+
+
 def test_c_abi_injected_failure_surfaces(gpu):
     """With the library's failure-injection hook (MK_INJECT_EHIP=1), every
     compute family returns MK_EHIP with the detail in its own mk_call: the
