@@ -237,6 +237,20 @@ int mk_dev_ssz_struct_list_root(mk_call* call, const void* d_records, uint64_t n
                                 uint64_t ws_bytes, void* stream);
 int mk_ssz_struct_list_root(mk_call* call, const uint8_t* records, uint64_t n, uint32_t record_len,
                             const mk_field* fields, uint32_t nfields, uint8_t out[32]);
+/* The list root's first tree level in the struct-roots launch: d_roots (n x
+ * 32) and the level-1 nodes of merkleHash over them, d_nodes (ceil(n/8) x 32:
+ * node j = Keccak of roots 8j..8j+7, the ragged last window as merkleHash
+ * hashes it, hash.go:205-228).  Finish with mk_dev_ssz_merkle_finish_nodes(
+ * d_nodes, ceil(n/8), n) -- the split lets a caller run another tree beside
+ * the latency-bound levels (the State's balances).
+ * mk_ssz_struct_list_level1_ok says whether the records qualify (the
+ * ValidatorRecord layout at a 16-B aligned address, n >= 2^18); otherwise
+ * mk_dev_ssz_struct_list_level1 returns MK_EINVAL. */
+int mk_ssz_struct_list_level1_ok(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
+                                 uint32_t nfields);
+int mk_dev_ssz_struct_list_level1(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
+                                  const mk_field* fields, uint32_t nfields, void* d_roots, void* d_nodes,
+                                  void* stream);
 
 /* ---- hashutil.MerkleRoot (merkleRoot.go:12-30) -------------------------- */
 /* Root of the heap o[i] = Hash(o[2i] || o[2i+1]) over leaves

@@ -915,14 +915,20 @@ bool struct_win_ok(const void* d_rec, uint64_t n, const mk::StructSpec& sp) {
     return true;
 }
 
-int dev_struct_list_root_win(const void* d_rec, uint64_t n, void* d_roots, void* d_wins, void* d_out32,
-                             void* d_ws, uint64_t ws_bytes, hipStream_t st) {
+int dev_struct_level1(const void* d_rec, uint64_t n, void* d_roots, void* d_wins, hipStream_t st) {
+    if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
     const uint64_t ngroups = ceil_div(n, mk::kLockThreads);
     const uint64_t cap = lock_grid_cap(st);
     const uint32_t gpw = (uint32_t)ceil_div(ngroups, cap);  // contiguous groups per workgroup
     hipLaunchKernelGGL(mk::k_struct_lock, dim3(ceil_div(ngroups, gpw)), dim3(mk::kLockThreads), 0, st,
                        (const uint8_t*)d_rec, n, (uint4*)d_roots, gpw, (uint4*)d_wins);
     HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
+int dev_struct_list_root_win(const void* d_rec, uint64_t n, void* d_roots, void* d_wins, void* d_out32,
+                             void* d_ws, uint64_t ws_bytes, hipStream_t st) {
+    TRY(dev_struct_level1(d_rec, n, d_roots, d_wins, st));
     const uint64_t c1 = ceil_div(n, 8);  // windows: ceil(ceil(n / 4) / 2) chunk pairs
     if (ws_bytes < finish_ws_bytes(c1)) return fail(MK_ENOMEM, "workspace too small for the registry top");
     return dev_finish_nodes(d_wins, c1, n, d_out32, d_ws, ws_bytes, st);
@@ -1121,12 +1127,15 @@ int trie_suffix_levels(void* d_levels, uint64_t cap, uint64_t n, uint64_t done, 
 // fills its CU, so the top could not co-run (one process, same box,
 // profiles/r04c-r04d: one trie 0.596 -> 0.582 ms locked, the stream of
 // tries 0.514 -> 0.604 ms/step).
+#ifndef MK_TRIE_FUSED_SPLIT
+#define MK_TRIE_FUSED_SPLIT 0  // 1: the fused front for split fronts too (A/B probe)
+#endif
 int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t* d_offs, uint64_t n,
                uint32_t fixed_len, uint32_t d_to, uint32_t depth, void* d_root32, hipStream_t st) {
     constexpr uint32_t NT = MK_TRIE_LOCK_NT, DPT = MK_TRIE_LOCK_DPT;
     constexpr uint32_t nlv = DPT == 8 ? 3 : DPT == 4 ? 2 : 1;
     const uint64_t ng = (MK_TRIE_LOCK && !d_offs && fixed_len == 280 && ((uintptr_t)d_data % 16) == 0 &&
-                         n >= MK_TRIE_LOCK_MIN && d_to == depth && depth >= nlv)
+                         n >= MK_TRIE_LOCK_MIN && (d_to == depth || MK_TRIE_FUSED_SPLIT) && d_to >= nlv)
                             ? n / (NT * DPT)
                             : 0;
     if (!ng) {
@@ -1137,7 +1146,8 @@ int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t*
     uint4* L[4] = {nullptr, nullptr, nullptr, nullptr};
     for (uint32_t d = 0; d <= nlv; ++d) L[d] = trie_level(d_levels, cap, d);
     // persistent: every workgroup runs the same number of groups where possible
-    const uint64_t cap_wg = std::min<uint64_t>(MK_TRIE_LOCK_GRID, lock_grid_cap(st));
+    const uint64_t cap_wg =
+        MK_TRIE_LOCK_ROUNDS ? std::min<uint64_t>(MK_TRIE_LOCK_GRID, lock_grid_cap(st)) : (uint64_t)MK_TRIE_LOCK_GRID;
     const uint64_t grid = ceil_div(ng, ceil_div(ng, cap_wg));
     hipLaunchKernelGGL((mk::k_trie_rec_lock<NT, DPT>), dim3(grid), dim3(NT), 0, st, (const uint2*)d_data, ng, L[0],
                        L[1], L[2], L[3]);
@@ -1860,6 +1870,29 @@ int mk_dev_ssz_struct_list_root(mk_call* call, const void* d_records, uint64_t n
     rc = launch_struct_roots(d_records, n, sp, msg, roots, st);
     if (rc) return S.done(rc);
     return S.done(dev_merkle_hash(roots, n, 32, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), st));
+}
+
+int mk_ssz_struct_list_level1_ok(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
+                                 uint32_t nfields) {
+    Scope S(nullptr, false);
+    mk::StructSpec sp;
+    if (make_spec(fields, nfields, record_len, sp) != MK_OK) return 0;
+    return struct_win_ok(d_records, n, sp) ? 1 : 0;
+}
+
+int mk_dev_ssz_struct_list_level1(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
+                                  const mk_field* fields, uint32_t nfields, void* d_roots, void* d_nodes,
+                                  void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    mk::StructSpec sp;
+    rc = make_spec(fields, nfields, record_len, sp);
+    if (rc) return S.done(rc);
+    if (!d_records || !d_roots || !d_nodes) return S.done(fail(MK_EINVAL, "null pointer"));
+    if (!struct_win_ok(d_records, n, sp))
+        return S.done(fail(MK_EINVAL, "level-1 front needs >= 2^18 ValidatorRecords at a 16-B aligned address"));
+    return S.done(dev_struct_level1(d_records, n, d_roots, d_nodes, (hipStream_t)stream));
 }
 
 int mk_dev_ssz_struct_roots(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,

@@ -2150,6 +2150,7 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 #ifndef MK_TRIE_LOCK_AUX
 #define MK_TRIE_LOCK_AUX 0  // global_load_lds policy of the deposit DMA (2 = nt)
 #endif
+
 template <uint32_t NT, int DPT>
 __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict__ in, uint64_t ngroups,
                                                          uint4* __restrict__ L0, uint4* __restrict__ L1,
@@ -2216,7 +2217,7 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
             for (int w = 17; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: block 1 may land
             dma(g, i, 1);
-            keccak_f_lock(s);
+            if constexpr (MK_TRIE_LOCK_ROUNDS) keccak_f_lock(s); else keccak_f(s);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 1 landed
 #pragma unroll
             for (int w = 0; w < 17; ++w) {
@@ -2232,12 +2233,12 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                 dma(gn, 0, 0);
                 tnext = tail(gn, 0);
             }
-            keccak_f_lock(s);
+            if constexpr (MK_TRIE_LOCK_ROUNDS) keccak_f_lock(s); else keccak_f(s);
             s.lo[0] ^= tl.x;  // word 34, then the domain pad byte (word 35 = lane 1)
             s.hi[0] ^= tl.y;
             s.lo[1] ^= 1u;
             s.hi[16] ^= 0x80000000u;
-            keccak_f_digest_lock(s);
+            if constexpr (MK_TRIE_LOCK_ROUNDS) keccak_f_digest_lock(s); else keccak_f_digest(s);
             uint4 d0, d1;
             digest(s, d0, d1);
             // fold: level l + 1 gets a node once slot i closes a pair at level l
@@ -2256,7 +2257,10 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                 }
                 dst[0] = d0;  // covered by the node permutation below
                 dst[1] = d1;
-                hash_node_lock(kl0[l], kl1[l], d0, d1, d0, d1);
+                if constexpr (MK_TRIE_LOCK_ROUNDS)
+                    hash_node_lock(kl0[l], kl1[l], d0, d1, d0, d1);
+                else
+                    hash_pair(kl0[l], kl1[l], d0, d1, false, d0, d1);
                 dst = lv[l + 1] + 2 * ((r0 + i) >> (l + 1));
             }
         }

@@ -82,6 +82,29 @@ def struct_list_root(records: torch.Tensor, n: int, record_len: int, spec, out: 
     return out
 
 
+def struct_list_level1_ok(records: torch.Tensor, n: int, record_len: int, spec) -> bool:
+    """Whether struct_list_level1 takes these records (the ValidatorRecord
+    layout at a 16-B aligned address, n >= 2^18)."""
+    from .registry import _fields
+
+    return bool(_lib.load().mk_ssz_struct_list_level1_ok(_p(records), n, record_len, _fields(spec), len(spec)))
+
+
+def struct_list_level1(records: torch.Tensor, n: int, record_len: int, spec, roots: torch.Tensor,
+                       nodes: torch.Tensor) -> torch.Tensor:
+    """The list root's first tree level in the struct-roots launch: the n
+    struct roots into ``roots`` and the ceil(n/8) level-1 nodes of their
+    merkleHash into ``nodes`` (finish with merkle_finish_nodes(nodes,
+    ceil(n/8), n))."""
+    from .registry import _fields
+
+    if roots.numel() < 32 * n or nodes.numel() < 32 * -(-n // 8):
+        raise ValueError("roots / nodes buffers too small")
+    _lib.invoke("mk_dev_ssz_struct_list_level1", _p(records), n, record_len, _fields(spec), len(spec), _p(roots),
+                _p(nodes), _stream(records.device), device=_dev(records))
+    return nodes
+
+
 def merkle_workspace(n: int, item_len: int, device) -> torch.Tensor:
     nbytes = _lib.load().mk_ssz_merkle_workspace_bytes(n, item_len)
     return torch.empty(max(256, nbytes), dtype=torch.uint8, device=device)

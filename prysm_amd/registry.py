@@ -132,18 +132,28 @@ class DeviceStateHasher:
     ~90 us of the struct kernel's issue slots for a tree that needs ~10 us of
     them (profiles/r03b: k_struct_reg 441 us alone, 533 us beside it)."""
 
-    def __init__(self, n: int, device, fused: bool = True):
-        """``fused``: the registry root in one library call
-        (mk_dev_ssz_struct_list_root: for >= 2^18 ValidatorRecords the struct
-        kernel also hashes the registry tree's level-1 windows, and the
-        balances tree starts at once beside it on the CUs its 245-workgroup
-        grid leaves free); False: round 3's two-call schedule (struct roots
-        alone, then the two trees side by side)."""
+    def __init__(self, n: int, device, schedule: str = "list"):
+        """``schedule``:
+        "list" (default): the registry root in one call
+            (mk_dev_ssz_struct_list_root: the struct kernel also hashes the
+            registry tree's level-1 windows) with the balances tree started
+            at once beside it, on the CUs the struct kernel's 245-workgroup
+            grid leaves free;
+        "level1": the same kernel through mk_dev_ssz_struct_list_level1,
+            then the registry's latency-bound levels (merkle_finish_nodes)
+            and the balances tree side by side (measured equal to "list":
+            0.637-0.657 vs 0.645-0.661 ms, profiles/r04/c3_sched/);
+        "two": round 3's schedule (struct roots alone, then the two trees
+            side by side).
+        Registries the fused kernel does not take (fewer than 2^18 records)
+        run "two"."""
         import torch
 
         from . import device as D
 
-        self.n, self.dev, self.fused = n, device, fused
+        if schedule not in ("level1", "list", "two"):
+            raise ValueError(f"unknown schedule {schedule!r}")
+        self.n, self.dev, self.schedule = n, device, schedule
         L = _lib.load()
         f = _fields(VALIDATOR_FIELDS)
         self.roots = torch.empty(max(32, 32 * n), dtype=torch.uint8, device=device)
@@ -151,7 +161,10 @@ class DeviceStateHasher:
                                   device=device)
         self.reg_ws = D.merkle_workspace(n, 32, device)
         self.list_ws = torch.empty(L.mk_ssz_struct_list_workspace_bytes(n, f, len(VALIDATOR_FIELDS)) + 256,
-                                   dtype=torch.uint8, device=device) if fused else None
+                                   dtype=torch.uint8, device=device) if schedule == "list" else None
+        self.c1 = -(-n // 8)  # level-1 nodes of the registry tree
+        self.nodes = torch.empty(max(32, 32 * self.c1), dtype=torch.uint8, device=device)
+        self.fin_ws = D.finish_workspace(self.c1, device) if schedule == "level1" else None
         self.bal_ws = D.merkle_workspace(n, 8, device)
         self.pair = torch.empty(64, dtype=torch.uint8, device=device)  # reg_root || bal_root
         self.out = torch.empty(32, dtype=torch.uint8, device=device)
@@ -168,7 +181,22 @@ class DeviceStateHasher:
 
         n = self.n
         cur = torch.cuda.current_stream(self.dev)
-        if self.fused:
+        sched = self.schedule
+        if sched != "two" and not D.struct_list_level1_ok(records, n, 160, VALIDATOR_FIELDS):
+            sched = "two"
+        if sched == "level1":
+            D.struct_list_level1(records, n, 160, VALIDATOR_FIELDS, self.roots, self.nodes)
+            self.ev_roots.record(cur)
+            self.side.wait_event(self.ev_roots)
+            balances.record_stream(self.side)
+            with torch.cuda.stream(self.side):
+                D.merkle_hash(balances, n, 8, out=self.pair[32:], ws=self.bal_ws)
+                self.ev_bal.record(self.side)
+            D.merkle_finish_nodes(self.nodes, self.c1, n, out=self.pair[:32], ws=self.fin_ws)
+            cur.wait_event(self.ev_bal)
+            D.hash_batch(self.pair, 1, 64, out=self.out)
+            return self.out
+        if sched == "list":
             self.ev_roots.record(cur)  # the inputs are ready
             self.side.wait_event(self.ev_roots)
             balances.record_stream(self.side)

@@ -156,14 +156,27 @@ def test_struct_list_root_windows_vs_oracle(gpu, n):
     spec = [(k, o, l) for k, o, l in R.VALIDATOR_FIELDS]
     roots = O.struct_roots(raw, n, 160, spec, nthreads=16)
     want = O.merkle_hash_flat(roots.reshape(-1), n, 32, nthreads=16)
-    got = D.struct_list_root(torch.from_numpy(raw.copy()).to(gpu), n, 160, R.VALIDATOR_FIELDS)
+    drec = torch.from_numpy(raw.copy()).to(gpu)
+    got = D.struct_list_root(drec, n, 160, R.VALIDATOR_FIELDS)
     torch.cuda.synchronize()
     assert bytes(got.cpu().numpy()) == want
+    # the split form: roots + level-1 nodes, then the finisher
+    assert D.struct_list_level1_ok(drec, n, 160, R.VALIDATOR_FIELDS)
+    c1 = -(-n // 8)
+    roots_d = torch.empty(32 * n, dtype=torch.uint8, device=gpu)
+    nodes = torch.empty(32 * c1, dtype=torch.uint8, device=gpu)
+    D.struct_list_level1(drec, n, 160, R.VALIDATOR_FIELDS, roots_d, nodes)
+    got2 = D.merkle_finish_nodes(nodes, c1, n)
+    torch.cuda.synchronize()
+    assert bytes(got2.cpu().numpy()) == want
+    assert np.array_equal(roots_d.cpu().numpy().reshape(n, 32), roots.reshape(n, 32))
 
 
-def test_state_hasher_fused_and_two_call_agree(gpu):
-    """registry.DeviceStateHasher, fused (default) and round 3's two-call
-    schedule, against the host-buffer state root, three submits each."""
+def test_state_hasher_schedules_agree(gpu):
+    """registry.DeviceStateHasher under its three schedules (level-1 front +
+    finish beside the balances tree, the one-call list root, round 3's
+    two-call schedule) against the host-buffer state root, three submits
+    each."""
     import torch
 
     from prysm_amd import registry as R
@@ -174,9 +187,9 @@ def test_state_hasher_fused_and_two_call_agree(gpu):
     want = R.state_root(reg, bal)
     rec = torch.from_numpy(reg.records.view(np.uint8).reshape(-1).copy()).to(gpu)
     dbal = torch.from_numpy(bal.view(np.uint8).copy()).to(gpu)
-    for fused in (True, False):
-        h = R.DeviceStateHasher(n, gpu, fused=fused)
+    for sched in ("level1", "list", "two"):
+        h = R.DeviceStateHasher(n, gpu, schedule=sched)
         for _ in range(3):
             out = h.submit(rec, dbal)
         torch.cuda.synchronize()
-        assert bytes(out.cpu().numpy()) == want, fused
+        assert bytes(out.cpu().numpy()) == want, sched

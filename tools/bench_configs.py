@@ -181,8 +181,8 @@ def run_config(args):
         # registry.DeviceStateHasher: struct kernel alone, then the registry
         # and balances trees side by side (two latency-bound trees on two
         # high-priority queues), then Keccak(reg_root || bal_root)
-        # PRYSM_C3_FUSED=0: round 3's schedule (A/B only)
-        hasher = R.DeviceStateHasher(n, dev, fused=os.environ.get("PRYSM_C3_FUSED", "1") != "0")
+        # PRYSM_C3_SCHED=level1|two: the other schedules (A/B only)
+        hasher = R.DeviceStateHasher(n, dev, schedule=os.environ.get("PRYSM_C3_SCHED", "list"))
 
         def step():
             return hasher.submit(rec, dbal)

@@ -1,12 +1,12 @@
 #!/bin/bash
-# C3 A/B: fused registry windows (default) vs round 3's two-call schedule, alternating processes
+# C3 A/B over registry.DeviceStateHasher's schedules (level1 = default, list, two = round 3), alternating processes
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 O=gpurun_out/$1
 mkdir -p $O
 for r in 1 2 3; do
-  for f in 1 0; do
-    PRYSM_C3_FUSED=$f timeout -k 10 200 python bench.py --config c3 --no-cpu-baseline > $O/c3_f${f}_$r.json 2> $O/c3_f${f}_$r.err || { tail -5 $O/c3_f${f}_$r.err; exit 1; }
-    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('fused', sys.argv[2], 'round', sys.argv[3], round(d['ms_per_step'], 4))" $O/c3_f${f}_$r.json $f $r | tee -a $O/summary.txt
+  for f in level1 list two; do
+    PRYSM_C3_SCHED=$f timeout -k 10 200 python bench.py --config c3 --no-cpu-baseline > $O/c3_f${f}_$r.json 2> $O/c3_f${f}_$r.err || { tail -5 $O/c3_f${f}_$r.err; exit 1; }
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('schedule', sys.argv[2], 'round', sys.argv[3], round(d['ms_per_step'], 4))" $O/c3_f${f}_$r.json $f $r | tee -a $O/summary.txt
   done
 done

@@ -52,7 +52,7 @@ for step in "$@"; do
       timeout -k 10 400 python bench.py --config $a > $O/bench_$a.json 2> $O/bench_$a.err || { tail -5 $O/bench_$a.err; exit 1; }
       cat $O/bench_$a.json ;;
     profile)
-      if [ -n "$b" ]; then export KERNEL="$b"; else unset KERNEL; fi  # empty: the C4 leaf kernel
+      export KERNEL="${b:-k_leaf_lock_sc}"  # empty: the C4 leaf kernel
       TAG=${TAG}_$a PROF_ARGS="--config $a --steps 10 --warmup 20 --no-cpu-baseline" \
         bash tools/profile.sh > $O/profile_$a.log 2>&1 || { tail -8 $O/profile_$a.log; exit 1; }
       cp gpurun_out/prof_${TAG}_$a/summary.json $O/pmc_$a.json && echo "profile $a ok" ;;

@@ -10,7 +10,7 @@ import os
 import sys
 from collections import defaultdict
 
-LEAF = os.environ.get("KERNEL", "k_reduce<true, true, 2>")
+LEAF = os.environ.get("KERNEL", "k_leaf_lock_sc")
 
 
 def counters(d):
