@@ -1127,15 +1127,12 @@ int trie_suffix_levels(void* d_levels, uint64_t cap, uint64_t n, uint64_t done, 
 // fills its CU, so the top could not co-run (one process, same box,
 // profiles/r04c-r04d: one trie 0.596 -> 0.582 ms locked, the stream of
 // tries 0.514 -> 0.604 ms/step).
-#ifndef MK_TRIE_FUSED_SPLIT
-#define MK_TRIE_FUSED_SPLIT 0  // 1: the fused front for split fronts too (A/B probe)
-#endif
 int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t* d_offs, uint64_t n,
                uint32_t fixed_len, uint32_t d_to, uint32_t depth, void* d_root32, hipStream_t st) {
     constexpr uint32_t NT = MK_TRIE_LOCK_NT, DPT = MK_TRIE_LOCK_DPT;
     constexpr uint32_t nlv = DPT == 8 ? 3 : DPT == 4 ? 2 : 1;
     const uint64_t ng = (MK_TRIE_LOCK && !d_offs && fixed_len == 280 && ((uintptr_t)d_data % 16) == 0 &&
-                         n >= MK_TRIE_LOCK_MIN && (d_to == depth || MK_TRIE_FUSED_SPLIT) && d_to >= nlv)
+                         n >= MK_TRIE_LOCK_MIN && d_to == depth && depth >= nlv)
                             ? n / (NT * DPT)
                             : 0;
     if (!ng) {
@@ -1146,8 +1143,7 @@ int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t*
     uint4* L[4] = {nullptr, nullptr, nullptr, nullptr};
     for (uint32_t d = 0; d <= nlv; ++d) L[d] = trie_level(d_levels, cap, d);
     // persistent: every workgroup runs the same number of groups where possible
-    const uint64_t cap_wg =
-        MK_TRIE_LOCK_ROUNDS ? std::min<uint64_t>(MK_TRIE_LOCK_GRID, lock_grid_cap(st)) : (uint64_t)MK_TRIE_LOCK_GRID;
+    const uint64_t cap_wg = std::min<uint64_t>(MK_TRIE_LOCK_GRID, lock_grid_cap(st));
     const uint64_t grid = ceil_div(ng, ceil_div(ng, cap_wg));
     hipLaunchKernelGGL((mk::k_trie_rec_lock<NT, DPT>), dim3(grid), dim3(NT), 0, st, (const uint2*)d_data, ng, L[0],
                        L[1], L[2], L[3]);

@@ -2217,7 +2217,7 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
             for (int w = 17; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: block 1 may land
             dma(g, i, 1);
-            if constexpr (MK_TRIE_LOCK_ROUNDS) keccak_f_lock(s); else keccak_f(s);
+            keccak_f_lock(s);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 1 landed
 #pragma unroll
             for (int w = 0; w < 17; ++w) {
@@ -2233,12 +2233,12 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                 dma(gn, 0, 0);
                 tnext = tail(gn, 0);
             }
-            if constexpr (MK_TRIE_LOCK_ROUNDS) keccak_f_lock(s); else keccak_f(s);
+            keccak_f_lock(s);
             s.lo[0] ^= tl.x;  // word 34, then the domain pad byte (word 35 = lane 1)
             s.hi[0] ^= tl.y;
             s.lo[1] ^= 1u;
             s.hi[16] ^= 0x80000000u;
-            if constexpr (MK_TRIE_LOCK_ROUNDS) keccak_f_digest_lock(s); else keccak_f_digest(s);
+            keccak_f_digest_lock(s);
             uint4 d0, d1;
             digest(s, d0, d1);
             // fold: level l + 1 gets a node once slot i closes a pair at level l
@@ -2257,10 +2257,7 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                 }
                 dst[0] = d0;  // covered by the node permutation below
                 dst[1] = d1;
-                if constexpr (MK_TRIE_LOCK_ROUNDS)
-                    hash_node_lock(kl0[l], kl1[l], d0, d1, d0, d1);
-                else
-                    hash_pair(kl0[l], kl1[l], d0, d1, false, d0, d1);
+                hash_node_lock(kl0[l], kl1[l], d0, d1, d0, d1);
                 dst = lv[l + 1] + 2 * ((r0 + i) >> (l + 1));
             }
         }

@@ -93,9 +93,6 @@ __global__ void k_trie_rec_lock(const uint2* in, uint64_t ngroups, uint4* L0, ui
 #ifndef MK_TRIE_LOCK_GRID
 #define MK_TRIE_LOCK_GRID 256  // persistent grid cap
 #endif
-#ifndef MK_TRIE_LOCK_ROUNDS
-#define MK_TRIE_LOCK_ROUNDS 1  // 0: the same staging with free-running rounds (A/B probe)
-#endif
 #ifndef MK_TRIE_LOCK_MIN
 #define MK_TRIE_LOCK_MIN (1u << 18)  // deposits: at least one group per CU
 #endif

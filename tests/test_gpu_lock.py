@@ -193,3 +193,4 @@ def test_state_hasher_schedules_agree(gpu):
             out = h.submit(rec, dbal)
         torch.cuda.synchronize()
         assert bytes(out.cpu().numpy()) == want, sched
+

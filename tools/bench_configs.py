@@ -178,10 +178,11 @@ def run_config(args):
         bal = R.synthetic_balances(n, seed + 3)
         rec = torch.from_numpy(reg.records.view(np.uint8).reshape(-1).copy()).to(dev)
         dbal = torch.from_numpy(bal.view(np.uint8).copy()).to(dev)
-        # registry.DeviceStateHasher: struct kernel alone, then the registry
-        # and balances trees side by side (two latency-bound trees on two
-        # high-priority queues), then Keccak(reg_root || bal_root)
-        # PRYSM_C3_SCHED=level1|two: the other schedules (A/B only)
+        # registry.DeviceStateHasher (schedule "list"): the registry root in one
+        # call (the struct kernel also hashes the registry tree's level-1
+        # windows), the balances tree beside it on a high-priority stream, then
+        # Keccak(reg_root || bal_root).  PRYSM_C3_SCHED=level1|two: the other
+        # schedules (A/B only)
         hasher = R.DeviceStateHasher(n, dev, schedule=os.environ.get("PRYSM_C3_SCHED", "list"))
 
         def step():
@@ -209,7 +210,7 @@ def run_config(args):
                    "sample": f"oracle struct_roots + merkleHash, 2^17 validators + balances, 1 thread, {dt:.1f} s"}
         _line("TreeHash of a 1M-validator State (registry + balances)", n / sec, "validators/s", args, sec, perms, hashes,
               {"workload": "C3: synthetic State{[]*ValidatorRecord, []uint64}, 1,000,000 validators",
-               "n": n, "root": got.hex()}, cpu)
+               "n": n, "root": got.hex(), "schedule": hasher.schedule}, cpu)
         return
 
     if args.config == "c4tree":
