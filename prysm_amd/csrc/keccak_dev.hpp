@@ -342,6 +342,17 @@ __device__ __forceinline__ void keccak_f_lock(State& s) {
 #pragma unroll kRoundUnroll
     for (int r = 0; r < 24; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
 }
+// Locked permutation with `mid` run after round K (K = 0: before it).
+template <int K, typename F>
+__device__ __forceinline__ void keccak_f_lock_mid(State& s, F&& mid) {
+    static_assert(K >= 0 && K <= 24, "mid point");
+    if constexpr (K == 0) mid();
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < K; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    if constexpr (K > 0) mid();
+#pragma unroll kRoundUnroll
+    for (int r = K; r < 24; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+}
 // `mid` runs after round K (K = 0: before the permutation), e.g. the issue of
 // the next window's DMA in k_leaf_lock_sc.
 template <int K = 0, typename F>

@@ -2150,6 +2150,9 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 #ifndef MK_TRIE_LOCK_AUX
 #define MK_TRIE_LOCK_AUX 0  // global_load_lds policy of the deposit DMA (2 = nt)
 #endif
+#ifndef MK_TRIE_DMA_ROUND
+#define MK_TRIE_DMA_ROUND 0  // round of a block's permutation after which the next block's DMA goes out
+#endif
 
 template <uint32_t NT, int DPT>
 __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict__ in, uint64_t ngroups,
@@ -2216,8 +2219,7 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
 #pragma unroll
             for (int w = 17; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: block 1 may land
-            dma(g, i, 1);
-            keccak_f_lock(s);
+            keccak_f_lock_mid<MK_TRIE_DMA_ROUND>(s, [&] { dma(g, i, 1); });
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 1 landed
 #pragma unroll
             for (int w = 0; w < 17; ++w) {
@@ -2226,14 +2228,15 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                 s.hi[w] ^= v.y;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (i + 1 < DPT) {
-                dma(g, i + 1, 0);
-                tnext = tail(g, i + 1);
-            } else if (gn < ngroups) {
-                dma(gn, 0, 0);
-                tnext = tail(gn, 0);
-            }
-            keccak_f_lock(s);
+            keccak_f_lock_mid<MK_TRIE_DMA_ROUND>(s, [&] {
+                if (i + 1 < DPT) {
+                    dma(g, i + 1, 0);
+                    tnext = tail(g, i + 1);
+                } else if (gn < ngroups) {
+                    dma(gn, 0, 0);
+                    tnext = tail(gn, 0);
+                }
+            });
             s.lo[0] ^= tl.x;  // word 34, then the domain pad byte (word 35 = lane 1)
             s.hi[0] ^= tl.y;
             s.lo[1] ^= 1u;
