@@ -240,9 +240,13 @@ int mk_ssz_struct_list_root(mk_call* call, const uint8_t* records, uint64_t n, u
 /* The list root's first tree level in the struct-roots launch: d_roots (n x
  * 32) and the level-1 nodes of merkleHash over them, d_nodes (ceil(n/8) x 32:
  * node j = Keccak of roots 8j..8j+7, the ragged last window as merkleHash
- * hashes it, hash.go:205-228).  Finish with mk_dev_ssz_merkle_finish_nodes(
- * d_nodes, ceil(n/8), n) -- the split lets a caller run another tree beside
- * the latency-bound levels (the State's balances).
+ * hashes it, hash.go:205-228).  Optionally (nvalues > 0) the same launch
+ * also writes the level-1 nodes of merkleHash over a second list -- nvalues
+ * items of value_len bytes (8, 16, 32, 64 or 128) at a 16-B aligned
+ * d_values, more than one chunk: ceil(nvalues * value_len / 256) nodes to
+ * d_value_nodes (the State's balances, BASELINE config 3).  Finish each with
+ * mk_dev_ssz_merkle_finish_nodes(nodes, count, n) -- the split lets the two
+ * trees' latency-bound levels run side by side.
  * mk_ssz_struct_list_level1_ok says whether the records qualify (the
  * ValidatorRecord layout at a 16-B aligned address, n >= 2^18); otherwise
  * mk_dev_ssz_struct_list_level1 returns MK_EINVAL. */
@@ -250,6 +254,7 @@ int mk_ssz_struct_list_level1_ok(const void* d_records, uint64_t n, uint32_t rec
                                  uint32_t nfields);
 int mk_dev_ssz_struct_list_level1(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
                                   const mk_field* fields, uint32_t nfields, void* d_roots, void* d_nodes,
+                                  const void* d_values, uint64_t nvalues, uint32_t value_len, void* d_value_nodes,
                                   void* stream);
 
 /* ---- hashutil.MerkleRoot (merkleRoot.go:12-30) -------------------------- */

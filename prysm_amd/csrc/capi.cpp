@@ -844,7 +844,7 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
         if (MK_STRUCT_LOCK && vec16 && validator_layout(sp) && n >= (1u << 18))  // phase-locked, partial last group
             hipLaunchKernelGGL(mk::k_struct_lock, dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), lock_grid_cap(st))),
                                dim3(mk::kLockThreads), 0, st, (const uint8_t*)d_rec, n, (uint4*)d_roots, 0u,
-                               (uint4*)nullptr);
+                               (uint4*)nullptr, (const uint8_t*)nullptr, (uint64_t)0, (uint4*)nullptr);
         else
             hipLaunchKernelGGL((mk::k_struct_reg<3, 6>), dim3(ceil_div(n, mk::kStructThreads)),
                                dim3(mk::kStructThreads), 0, st, (const uint8_t*)d_rec, n, sp, vec16 ? 1u : 0u,
@@ -915,13 +915,17 @@ bool struct_win_ok(const void* d_rec, uint64_t n, const mk::StructSpec& sp) {
     return true;
 }
 
-int dev_struct_level1(const void* d_rec, uint64_t n, void* d_roots, void* d_wins, hipStream_t st) {
+// d_vals (nullable): a second list of vbytes bytes whose level-1 windows the
+// kernel hashes on its leftover lanes (item length dividing 128, 16-B aligned)
+int dev_struct_level1(const void* d_rec, uint64_t n, void* d_roots, void* d_wins, hipStream_t st,
+                      const void* d_vals = nullptr, uint64_t vbytes = 0, void* d_vwins = nullptr) {
     if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
     const uint64_t ngroups = ceil_div(n, mk::kLockThreads);
     const uint64_t cap = lock_grid_cap(st);
     const uint32_t gpw = (uint32_t)ceil_div(ngroups, cap);  // contiguous groups per workgroup
     hipLaunchKernelGGL(mk::k_struct_lock, dim3(ceil_div(ngroups, gpw)), dim3(mk::kLockThreads), 0, st,
-                       (const uint8_t*)d_rec, n, (uint4*)d_roots, gpw, (uint4*)d_wins);
+                       (const uint8_t*)d_rec, n, (uint4*)d_roots, gpw, (uint4*)d_wins,
+                       (const uint8_t*)(vbytes ? d_vals : nullptr), vbytes, (uint4*)d_vwins);
     HIPCHK(hipGetLastError());
     return MK_OK;
 }
@@ -1878,6 +1882,7 @@ int mk_ssz_struct_list_level1_ok(const void* d_records, uint64_t n, uint32_t rec
 
 int mk_dev_ssz_struct_list_level1(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
                                   const mk_field* fields, uint32_t nfields, void* d_roots, void* d_nodes,
+                                  const void* d_values, uint64_t nvalues, uint32_t value_len, void* d_value_nodes,
                                   void* stream) {
     Scope S(call);
     int rc = bind_stream((hipStream_t)stream);
@@ -1888,7 +1893,15 @@ int mk_dev_ssz_struct_list_level1(mk_call* call, const void* d_records, uint64_t
     if (!d_records || !d_roots || !d_nodes) return S.done(fail(MK_EINVAL, "null pointer"));
     if (!struct_win_ok(d_records, n, sp))
         return S.done(fail(MK_EINVAL, "level-1 front needs >= 2^18 ValidatorRecords at a 16-B aligned address"));
-    return S.done(dev_struct_level1(d_records, n, d_roots, d_nodes, (hipStream_t)stream));
+    if (nvalues) {
+        if (!d_values || !d_value_nodes) return S.done(fail(MK_EINVAL, "null pointer"));
+        if (value_len % 8 || value_len == 0 || 128 % value_len || ((uintptr_t)d_values % 16))
+            return S.done(fail(MK_EINVAL, "second list: items of 8, 16, 32, 64 or 128 B at a 16-B aligned address"));
+        if (nvalues * value_len <= 128)
+            return S.done(fail(MK_EINVAL, "second list of one chunk has no level-1 window"));
+    }
+    return S.done(dev_struct_level1(d_records, n, d_roots, d_nodes, (hipStream_t)stream, d_values,
+                                    nvalues * (uint64_t)value_len, d_value_nodes));
 }
 
 int mk_dev_ssz_struct_roots(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,

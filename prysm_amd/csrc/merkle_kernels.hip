@@ -1771,6 +1771,41 @@ template __global__ void k_struct_reg<3, 6>(const uint8_t*, uint64_t, StructSpec
 // they are absorbed, and the struct message is read back from the record's
 // slot; the next group's copy goes out once it is (before the two
 // struct-message permutations).
+// Level-1 window w of merkleHash over `total` bytes of items whose length
+// divides 128 (chunks of 128 B, windows of 256 B) at a 16-B aligned `base`
+// (total % 8 == 0): a full window streams its 256 B; the ragged last one
+// hashes its r bytes, plus 0^128 when they fill one chunk only (hash.go:225-228).
+__device__ __forceinline__ void window256_or_ragged(const uint8_t* __restrict__ base, uint64_t total, uint64_t w,
+                                                    uint4& d0, uint4& d1) {
+    if (256 * w + 256 <= total) {
+        hash_window256(reinterpret_cast<const uint4*>(base) + 16 * w, d0, d1);
+        return;
+    }
+    const uint32_t r = (uint32_t)(total - 256 * w);                // 8..248 bytes
+    const uint32_t nwd = r / 8, len = r + (r <= 128 ? 128u : 0u);  // 136..256 B: two blocks
+    const uint2* p = reinterpret_cast<const uint2*>(base + 256 * w);
+    State s;
+    zero(s);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int k = 0; k < 17; ++k) {
+            const uint32_t q = 17 * b + k;
+            uint2 v = q < nwd ? p[q] : make_uint2(0, 0);
+            if (q == len / 8) v.x ^= 1u;  // domain pad (len % 8 == 0)
+            s.lo[k] ^= v.x;
+            s.hi[k] ^= v.y;
+        }
+        if (b == 0) {
+            keccak_f(s);
+        } else {
+            s.hi[16] ^= 0x80000000u;
+            keccak_f_digest(s);
+        }
+    }
+    digest(s, d0, d1);
+}
+
 __device__ constexpr uint32_t kValOff[9] = {0, 48, 80, 112, 120, 128, 136, 144, 152};
 __device__ constexpr uint32_t kValLen[9] = {48, 32, 32, 8, 8, 8, 8, 8, 8};
 //
@@ -1784,7 +1819,9 @@ __device__ constexpr uint32_t kValLen[9] = {48, 32, 32, 8, 8, 8, 8, 8, 8};
 // roots array.
 __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* __restrict__ rec, uint64_t n,
                                                                  uint4* __restrict__ roots, uint32_t gpw,
-                                                                 uint4* __restrict__ wins) {
+                                                                 uint4* __restrict__ wins,
+                                                                 const uint8_t* __restrict__ vals, uint64_t vbytes,
+                                                                 uint4* __restrict__ vwins) {
     constexpr uint32_t kRecLen = 160, kRw = kRecLen / 4, kNinstr = kRecLen / 16;
     __shared__ uint32_t buf[kLockThreads / 64][64 * kRw];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -1874,44 +1911,28 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     if (!wins || g_begin >= g_end) return;
     // the workgroup's roots are in L2 (written above; this CU never read those
     // lines, and its L1 was invalidated at dispatch): every wave's stores
-    // complete, then one window per lane
+    // complete, then one window per lane -- the registry's windows over the
+    // roots just written, then this workgroup's share of the optional second
+    // list's windows (`vals`, vbytes bytes of items dividing 128; the State's
+    // balances) on the lanes left over
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint64_t r0 = g_begin * kLockThreads, r1 = g_end * kLockThreads < n ? g_end * kLockThreads : n;
     const uint64_t w0 = r0 / 8, nw = (r1 - r0 + 7) / 8;
+    const uint64_t vw_total = (vbytes + 255) / 256, vpw = (vw_total + gridDim.x - 1) / gridDim.x;
+    const uint64_t v0 = (uint64_t)blockIdx.x * vpw;
+    const uint64_t nv = vals && v0 < vw_total ? (vw_total - v0 < vpw ? vw_total - v0 : vpw) : 0;
 #pragma unroll 1
-    for (uint64_t j = threadIdx.x; j < nw; j += kLockThreads) {
-        const uint64_t w = w0 + j;
+    for (uint64_t t = threadIdx.x; t < nw + nv; t += kLockThreads) {
+        const bool reg = t < nw;
+        const uint64_t w = reg ? w0 + t : v0 + (t - nw);
+        const uint8_t* base = reg ? reinterpret_cast<const uint8_t*>(roots) : vals;
+        const uint64_t total = reg ? 32 * n : vbytes;
         uint4 d0, d1;
-        if (8 * w + 8 <= n) {
-            hash_window256(roots + 16 * w, d0, d1);
-        } else {  // the ragged last window: r roots, one chunk + 0^128 when r <= 4 (hash.go:225-228)
-            const uint32_t r = (uint32_t)(n - 8 * w);
-            const uint32_t nw = 4 * r, len = 32 * r + (r <= 4 ? 128u : 0u);  // 160..256 B: two blocks
-            const uint2* p = reinterpret_cast<const uint2*>(roots + 16 * w);
-            State s;
-            zero(s);
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-#pragma unroll
-                for (int k = 0; k < 17; ++k) {
-                    const uint32_t q = 17 * b + k;
-                    uint2 v = q < nw ? p[q] : make_uint2(0, 0);
-                    if (q == len / 8) v.x ^= 1u;  // domain pad (len % 8 == 0)
-                    s.lo[k] ^= v.x;
-                    s.hi[k] ^= v.y;
-                }
-                if (b == 0) {
-                    keccak_f(s);
-                } else {
-                    s.hi[16] ^= 0x80000000u;
-                    keccak_f_digest(s);
-                }
-            }
-            digest(s, d0, d1);
-        }
-        wins[2 * w] = d0;
-        wins[2 * w + 1] = d1;
+        window256_or_ragged(base, total, w, d0, d1);
+        uint4* o = reg ? wins : vwins;
+        o[2 * w] = d0;
+        o[2 * w + 1] = d1;
     }
 }
 

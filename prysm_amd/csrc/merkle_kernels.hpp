@@ -53,7 +53,9 @@ template <int NB, int NRAW>
 __global__ void k_struct_reg(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
 // validator layout (kValOff/kValLen in merkle_kernels.hip), any n (a partial last group);
 // gpw > 0: contiguous groups per workgroup plus the level-1 windows of the roots' merkleHash
-__global__ void k_struct_lock(const uint8_t* rec, uint64_t n, uint4* roots, uint32_t gpw, uint4* wins);
+// (and of a second list of vbytes bytes at vals, when vals != nullptr)
+__global__ void k_struct_lock(const uint8_t* rec, uint64_t n, uint4* roots, uint32_t gpw, uint4* wins,
+                              const uint8_t* vals, uint64_t vbytes, uint4* vwins);
 #ifndef MK_STRUCT_LOCK
 #define MK_STRUCT_LOCK 1
 #endif

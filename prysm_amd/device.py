@@ -91,17 +91,23 @@ def struct_list_level1_ok(records: torch.Tensor, n: int, record_len: int, spec) 
 
 
 def struct_list_level1(records: torch.Tensor, n: int, record_len: int, spec, roots: torch.Tensor,
-                       nodes: torch.Tensor) -> torch.Tensor:
+                       nodes: torch.Tensor, values: torch.Tensor = None, nvalues: int = 0, value_len: int = 8,
+                       value_nodes: torch.Tensor = None) -> torch.Tensor:
     """The list root's first tree level in the struct-roots launch: the n
     struct roots into ``roots`` and the ceil(n/8) level-1 nodes of their
     merkleHash into ``nodes`` (finish with merkle_finish_nodes(nodes,
-    ceil(n/8), n))."""
+    ceil(n/8), n)); with ``values`` also the ceil(nvalues * value_len / 256)
+    level-1 nodes of a second list's merkleHash into ``value_nodes``."""
     from .registry import _fields
 
     if roots.numel() < 32 * n or nodes.numel() < 32 * -(-n // 8):
         raise ValueError("roots / nodes buffers too small")
+    if nvalues and (values is None or value_nodes is None or
+                    value_nodes.numel() < 32 * -(-nvalues * value_len // 256)):
+        raise ValueError("second list: values / value_nodes missing or too small")
     _lib.invoke("mk_dev_ssz_struct_list_level1", _p(records), n, record_len, _fields(spec), len(spec), _p(roots),
-                _p(nodes), _stream(records.device), device=_dev(records))
+                _p(nodes), _p(values) if nvalues else None, nvalues, value_len,
+                _p(value_nodes) if nvalues else None, _stream(records.device), device=_dev(records))
     return nodes
 
 

@@ -140,9 +140,10 @@ class DeviceStateHasher:
             at once beside it, on the CUs the struct kernel's 245-workgroup
             grid leaves free;
         "level1": the same kernel through mk_dev_ssz_struct_list_level1,
-            then the registry's latency-bound levels (merkle_finish_nodes)
-            and the balances tree side by side (measured equal to "list":
-            0.637-0.657 vs 0.645-0.661 ms, profiles/r04/c3_sched/);
+            which also hashes the balances tree's level-1 windows on the
+            lanes the registry's windows leave free; then the two trees'
+            latency-bound levels side by side (merkle_finish_nodes on two
+            streams);
         "two": round 3's schedule (struct roots alone, then the two trees
             side by side).
         Registries the fused kernel does not take (fewer than 2^18 records)
@@ -165,6 +166,9 @@ class DeviceStateHasher:
         self.c1 = -(-n // 8)  # level-1 nodes of the registry tree
         self.nodes = torch.empty(max(32, 32 * self.c1), dtype=torch.uint8, device=device)
         self.fin_ws = D.finish_workspace(self.c1, device) if schedule == "level1" else None
+        self.cb1 = -(-8 * n // 256)  # level-1 nodes of the balances tree
+        self.bnodes = torch.empty(max(32, 32 * self.cb1), dtype=torch.uint8, device=device)
+        self.bfin_ws = D.finish_workspace(self.cb1, device) if schedule == "level1" else None
         self.bal_ws = D.merkle_workspace(n, 8, device)
         self.pair = torch.empty(64, dtype=torch.uint8, device=device)  # reg_root || bal_root
         self.out = torch.empty(32, dtype=torch.uint8, device=device)
@@ -185,12 +189,14 @@ class DeviceStateHasher:
         if sched != "two" and not D.struct_list_level1_ok(records, n, 160, VALIDATOR_FIELDS):
             sched = "two"
         if sched == "level1":
-            D.struct_list_level1(records, n, 160, VALIDATOR_FIELDS, self.roots, self.nodes)
+            # one launch: struct roots + the level-1 windows of BOTH trees (the
+            # balances' on the lanes the registry's windows leave free)
+            D.struct_list_level1(records, n, 160, VALIDATOR_FIELDS, self.roots, self.nodes, values=balances,
+                                 nvalues=n, value_len=8, value_nodes=self.bnodes)
             self.ev_roots.record(cur)
             self.side.wait_event(self.ev_roots)
-            balances.record_stream(self.side)
             with torch.cuda.stream(self.side):
-                D.merkle_hash(balances, n, 8, out=self.pair[32:], ws=self.bal_ws)
+                D.merkle_finish_nodes(self.bnodes, self.cb1, n, out=self.pair[32:], ws=self.bfin_ws)
                 self.ev_bal.record(self.side)
             D.merkle_finish_nodes(self.nodes, self.c1, n, out=self.pair[:32], ws=self.fin_ws)
             cur.wait_event(self.ev_bal)

@@ -170,6 +170,20 @@ def test_struct_list_root_windows_vs_oracle(gpu, n):
     torch.cuda.synchronize()
     assert bytes(got2.cpu().numpy()) == want
     assert np.array_equal(roots_d.cpu().numpy().reshape(n, 32), roots.reshape(n, 32))
+    # with a second list's level-1 windows in the same launch (the State's
+    # balances: 8-B items; and 32-B items), ragged or not
+    for nv, vl in ((n, 8), (n + 3, 8), (1000, 32), (17, 8)):
+        vals = O.splitmix_bytes(nv * vl, SEED + 49 + nv)
+        dv = torch.from_numpy(vals.copy()).to(gpu)
+        cv = -(-nv * vl // 256)
+        vnodes = torch.empty(32 * cv, dtype=torch.uint8, device=gpu)
+        D.struct_list_level1(drec, n, 160, R.VALIDATOR_FIELDS, roots_d, nodes, values=dv, nvalues=nv, value_len=vl,
+                             value_nodes=vnodes)
+        gv = D.merkle_finish_nodes(vnodes, cv, nv)
+        gr = D.merkle_finish_nodes(nodes, c1, n)
+        torch.cuda.synchronize()
+        assert bytes(gr.cpu().numpy()) == want, (nv, vl)
+        assert bytes(gv.cpu().numpy()) == O.merkle_hash_flat(vals, nv, vl, nthreads=16), (nv, vl)
 
 
 def test_state_hasher_schedules_agree(gpu):
