@@ -309,8 +309,9 @@ uint64_t lock_grid_cap(hipStream_t st) {
 }
 
 int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t* d_ws, uint64_t ws_bytes,
-                hipStream_t st) {
+                hipStream_t st, uint8_t* pair_block = nullptr, uint32_t pair_slot = 0) {
     if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
+    if (p.small && pair_block) return fail(MK_EINVAL, "internal: pair finalize needs a k_wave3 plan");
     if (p.small) {
         hipLaunchKernelGGL(mk::k_final_small, dim3(1), dim3(64), 0, st, d_items, p.total, p.n, d_out32);
         HIPCHK(hipGetLastError());
@@ -319,12 +320,21 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
     if (ws_bytes < mk::plan_ws_bytes(p))
         return fail(MK_ENOMEM, "workspace too small: %llu < %llu", (unsigned long long)ws_bytes,
                     (unsigned long long)mk::plan_ws_bytes(p));
+    if (pair_block)  // checked before any pass is launched
+        for (const Pass& ps : p.passes)
+            if (ps.a.finalize && (!MK_WAVE3_SPREAD || !ps.wave || !ps.w3))
+                return fail(MK_EINVAL, "internal: pair finalize needs the spread-form k_wave3 final pass");
     uint8_t* slots[2] = {d_ws, d_ws + 32 * p.slot_nodes[0]};
     const bool prof = prof_on();
     for (const Pass& ps : p.passes) {
         ReduceArgs a = ps.a;
         a.items = ps.in_ws < 0 ? d_items : slots[ps.in_ws];
         a.out = ps.out_ws < 0 ? d_out32 : slots[ps.out_ws];
+        if (a.finalize && pair_block) {  // a two-field struct root (wave3_spread_final)
+            a.pair_block = pair_block;
+            a.pair_slot = pair_slot;
+            a.out = pair_block + 32 * pair_slot;
+        }
         ProfRec rec{};
         const bool rec_this = prof && ps.leaf;
         if (rec_this) {
@@ -474,10 +484,11 @@ int dev_merkle_hash(const void* d_items, uint64_t n, uint32_t item_len, void* d_
     return launch_plan(p, (const uint8_t*)d_items, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st);
 }
 
-int dev_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32, hipStream_t st) {
+int dev_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32, hipStream_t st,
+               void* d_pair_block = nullptr, uint32_t pair_slot = 0) {
     if (nroots == 0 || nroots > 2 * mk::kWave2Span)
         return fail(MK_EINVAL, "nroots %llu out of range (1..%u)", (unsigned long long)nroots, 2 * mk::kWave2Span);
-    if (!d_roots || !d_out32) return fail(MK_EINVAL, "null pointer");
+    if (!d_roots || (!d_out32 && !d_pair_block)) return fail(MK_EINVAL, "null pointer");
     // the reference level loop over the shard roots (odd -> 0^128) plus the
     // length mix-in is one finalizing node pass of the two-lane latency kernel
     ReduceArgs a{};
@@ -489,6 +500,11 @@ int dev_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_o
     a.n_items = n_total;
     a.levels = 64;
     a.finalize = 1;
+    if (d_pair_block) {
+        a.pair_block = (uint8_t*)d_pair_block;
+        a.pair_slot = pair_slot;
+        a.out = (uint8_t*)d_pair_block + 32 * pair_slot;
+    }
     launch_wave3<false>(mk::kWaveThreads, 1, a, st);
     HIPCHK(hipGetLastError());
     return MK_OK;
@@ -502,12 +518,14 @@ uint64_t finish_ws_bytes(uint64_t count) {
 }
 
 int dev_finish_nodes(const void* d_nodes, uint64_t count, uint64_t n_total, void* d_out32, void* d_ws,
-                     uint64_t ws_bytes, hipStream_t st) {
-    if (count <= 2 * mk::kWave2Span) return dev_finish(d_nodes, count, n_total, d_out32, st);
-    if (!d_nodes || !d_out32) return fail(MK_EINVAL, "null pointer");
+                     uint64_t ws_bytes, hipStream_t st, void* d_pair_block = nullptr, uint32_t pair_slot = 0) {
+    if (count <= 2 * mk::kWave2Span)
+        return dev_finish(d_nodes, count, n_total, d_out32, st, d_pair_block, pair_slot);
+    if (!d_nodes || (!d_out32 && !d_pair_block)) return fail(MK_EINVAL, "null pointer");
     Plan p;
     TRY(mk::make_plan(count, 32, false, 0, false, ((uintptr_t)d_nodes % 16) == 0, p, true, 0, n_total));
-    return launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st);
+    return launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st,
+                       (uint8_t*)d_pair_block, pair_slot);
 }
 
 // ---- TreeHash of a list of byte strings (makeSliceHasher + hashedEncoding) ---------------
@@ -1812,6 +1830,19 @@ int mk_dev_ssz_merkle_finish_nodes(mk_call* call, const void* d_nodes, uint64_t 
     Scope S(call);
     int rc = bind_stream((hipStream_t)stream);
     return S.done(rc ? rc : dev_finish_nodes(d_nodes, count, n_total, d_out32, d_ws, ws_bytes, (hipStream_t)stream));
+}
+
+int mk_dev_ssz_merkle_finish_nodes_pair(mk_call* call, const void* d_nodes, uint64_t count, uint64_t n_total,
+                                        void* d_pair_block, uint32_t slot, void* d_ws, uint64_t ws_bytes,
+                                        void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    if (!d_pair_block) return S.done(fail(MK_EINVAL, "null pointer"));
+    if (slot > 1) return S.done(fail(MK_EINVAL, "pair slot %u out of range (0..1)", slot));
+    if ((uintptr_t)d_pair_block % 16) return S.done(fail(MK_EINVAL, "pair block not 16-B aligned"));
+    return S.done(dev_finish_nodes(d_nodes, count, n_total, nullptr, d_ws, ws_bytes, (hipStream_t)stream,
+                                   d_pair_block, slot));
 }
 
 int mk_dev_ssz_merkle_finish(mk_call* call, const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32,

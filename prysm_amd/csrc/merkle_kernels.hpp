@@ -67,6 +67,9 @@ __global__ void k_struct_split(const uint8_t* rec, uint64_t n, StructSpec sp, ui
 constexpr uint64_t kStructSplitMaxN = MK_STRUCT_SPLIT_MAX_N;  // k_struct_split at or below (0: never)
 template <uint32_t NT, bool LEAF>
 __global__ void k_wave3(ReduceArgs a);
+#ifndef MK_WAVE3_SPREAD
+#define MK_WAVE3_SPREAD 1  // k_wave3's last levels one state per wave (the pair finalize needs it)
+#endif
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
 __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);
 __global__ void k_keccak64_lock(const uint4* in, uint64_t n, uint4* out);  // any n (a partial last group)

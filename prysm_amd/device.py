@@ -259,6 +259,22 @@ def finish_workspace(count: int, device) -> torch.Tensor:
                        device=device)
 
 
+def merkle_finish_nodes_pair(nodes: torch.Tensor, count: int, n_total: int, pair_block: torch.Tensor, slot: int,
+                             ws: torch.Tensor = None) -> None:
+    """merkle_finish_nodes for one list field of a two-field struct: the list
+    root goes to pair_block[32 slot:32 slot + 32]; whichever of the two
+    finishers (slot 0 and 1, any streams) completes second writes the struct
+    root Keccak(pair_block[0:64]) to pair_block[64:96].  ``pair_block``:
+    128 zeroed bytes before its first use (the finishers re-arm it)."""
+    dev = _dev(nodes)
+    if pair_block.numel() < 128:
+        raise ValueError("pair block of 128 bytes")
+    if ws is None:
+        ws = finish_workspace(count, nodes.device)
+    _lib.invoke("mk_dev_ssz_merkle_finish_nodes_pair", _p(nodes), count, n_total, _p(pair_block), slot, _p(ws),
+                ws.numel(), _stream(nodes.device), device=dev)
+
+
 def merkle_finish_nodes(nodes: torch.Tensor, count: int, n_total: int, out: torch.Tensor = None,
                         ws: torch.Tensor = None) -> torch.Tensor:
     """Reference level loop over one gathered tree level of `count` nodes +

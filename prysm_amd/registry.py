@@ -123,27 +123,26 @@ def state_root(registry: ValidatorRegistry, balances: np.ndarray) -> bytes:
 class DeviceStateHasher:
     """TreeHash of State{ValidatorRegistry, ValidatorBalances} from records and
     balances resident in HBM (BASELINE config 3, device-resident), with every
-    buffer allocated once.  Schedule on two streams: the struct kernel (5
-    permutations per validator, at the VALU issue ceiling) runs ALONE; the
-    balances tree then runs on a high-priority side stream beside the
-    registry tree.  Both trees are narrow and latency-bound (~20 levels of
-    one permutation latency each), so they fill each other's idle issue
-    slots; running the balances tree beside the struct kernel instead stole
-    ~90 us of the struct kernel's issue slots for a tree that needs ~10 us of
-    them (profiles/r03b: k_struct_reg 441 us alone, 533 us beside it)."""
+    buffer allocated once.  The struct kernel (5 permutations per validator,
+    at the VALU issue ceiling) also hashes the level-1 windows of both trees;
+    what is left after it is two narrow latency-bound trees (~17 levels of
+    one permutation latency each), run side by side on two streams so they
+    fill each other's idle issue slots."""
 
-    def __init__(self, n: int, device, schedule: str = "list"):
+    def __init__(self, n: int, device, schedule: str = "level1"):
         """``schedule``:
-        "list" (default): the registry root in one call
-            (mk_dev_ssz_struct_list_root: the struct kernel also hashes the
-            registry tree's level-1 windows) with the balances tree started
-            at once beside it, on the CUs the struct kernel's 245-workgroup
-            grid leaves free;
-        "level1": the same kernel through mk_dev_ssz_struct_list_level1,
-            which also hashes the balances tree's level-1 windows on the
-            lanes the registry's windows leave free; then the two trees'
-            latency-bound levels side by side (merkle_finish_nodes on two
-            streams);
+        "level1" (default): one launch for the struct roots and the level-1
+            windows of BOTH trees (mk_dev_ssz_struct_list_level1: the
+            balances' windows on the lanes the registry's leave free); then
+            the two trees' latency-bound levels side by side on two streams,
+            the second finisher to complete hashing the state root
+            (mk_dev_ssz_merkle_finish_nodes_pair): nothing waits on an event
+            between the struct kernel and the root;
+        "list": the registry root in one call (mk_dev_ssz_struct_list_root:
+            the struct kernel also hashes the registry tree's level-1 windows)
+            with the whole balances tree started at once beside it, on the CUs
+            the struct kernel's 245-workgroup grid leaves free, then
+            Keccak(reg_root || bal_root) after both;
         "two": round 3's schedule (struct roots alone, then the two trees
             side by side).
         Registries the fused kernel does not take (fewer than 2^18 records)
@@ -163,15 +162,19 @@ class DeviceStateHasher:
         self.reg_ws = D.merkle_workspace(n, 32, device)
         self.list_ws = torch.empty(L.mk_ssz_struct_list_workspace_bytes(n, f, len(VALIDATOR_FIELDS)) + 256,
                                    dtype=torch.uint8, device=device) if schedule == "list" else None
+        lv1 = schedule == "level1"
         self.c1 = -(-n // 8)  # level-1 nodes of the registry tree
         self.nodes = torch.empty(max(32, 32 * self.c1), dtype=torch.uint8, device=device)
-        self.fin_ws = D.finish_workspace(self.c1, device) if schedule == "level1" else None
+        self.fin_ws = D.finish_workspace(self.c1, device) if lv1 else None
         self.cb1 = -(-8 * n // 256)  # level-1 nodes of the balances tree
         self.bnodes = torch.empty(max(32, 32 * self.cb1), dtype=torch.uint8, device=device)
-        self.bfin_ws = D.finish_workspace(self.cb1, device) if schedule == "level1" else None
+        self.bfin_ws = D.finish_workspace(self.cb1, device) if lv1 else None
+        # reg_root || bal_root || state root || arrival counter (zero before first use)
+        self.pair_block = torch.zeros(128, dtype=torch.uint8, device=device) if lv1 else None
         self.bal_ws = D.merkle_workspace(n, 8, device)
         self.pair = torch.empty(64, dtype=torch.uint8, device=device)  # reg_root || bal_root
-        self.out = torch.empty(32, dtype=torch.uint8, device=device)
+        # the state root ("level1": the pair finisher writes it into the pair block)
+        self.out = self.pair_block[64:96] if lv1 else torch.empty(32, dtype=torch.uint8, device=device)
         self.side = torch.cuda.Stream(device=device, priority=-1)  # its own hardware queue
         self.ev_roots = torch.cuda.Event()
         self.ev_bal = torch.cuda.Event()
@@ -195,12 +198,13 @@ class DeviceStateHasher:
                                  nvalues=n, value_len=8, value_nodes=self.bnodes)
             self.ev_roots.record(cur)
             self.side.wait_event(self.ev_roots)
+            # the two trees' latency-bound levels side by side; whichever
+            # finisher completes second hashes Keccak(reg_root || bal_root)
             with torch.cuda.stream(self.side):
-                D.merkle_finish_nodes(self.bnodes, self.cb1, n, out=self.pair[32:], ws=self.bfin_ws)
+                D.merkle_finish_nodes_pair(self.bnodes, self.cb1, n, self.pair_block, 1, ws=self.bfin_ws)
                 self.ev_bal.record(self.side)
-            D.merkle_finish_nodes(self.nodes, self.c1, n, out=self.pair[:32], ws=self.fin_ws)
+            D.merkle_finish_nodes_pair(self.nodes, self.c1, n, self.pair_block, 0, ws=self.fin_ws)
             cur.wait_event(self.ev_bal)
-            D.hash_batch(self.pair, 1, 64, out=self.out)
             return self.out
         if sched == "list":
             self.ev_roots.record(cur)  # the inputs are ready

@@ -183,7 +183,36 @@ def test_struct_list_root_windows_vs_oracle(gpu, n):
         gr = D.merkle_finish_nodes(nodes, c1, n)
         torch.cuda.synchronize()
         assert bytes(gr.cpu().numpy()) == want, (nv, vl)
-        assert bytes(gv.cpu().numpy()) == O.merkle_hash_flat(vals, nv, vl, nthreads=16), (nv, vl)
+        want_v = O.merkle_hash_flat(vals, nv, vl, nthreads=16)
+        assert bytes(gv.cpu().numpy()) == want_v, (nv, vl)
+        # the pair finisher: each field's root into its slot, the second to
+        # complete hashes Keccak(slot 0 || slot 1) and re-arms the counter;
+        # both orders on one stream, then the two on two streams at once
+        pb = torch.zeros(128, dtype=torch.uint8, device=gpu)
+        want_s = O.keccak256(want + want_v)
+        for order in ((0, 1), (1, 0)):
+            pb[64:96].zero_()
+            for slot in order:  # cv may be 1: the one-node finisher
+                if slot == 0:
+                    D.merkle_finish_nodes_pair(nodes, c1, n, pb, 0)
+                else:
+                    D.merkle_finish_nodes_pair(vnodes, cv, nv, pb, 1)
+            torch.cuda.synchronize()
+            got_pb = bytes(pb.cpu().numpy())
+            assert got_pb[:32] == want and got_pb[32:64] == want_v, (nv, vl, order)
+            assert got_pb[64:96] == want_s, (nv, vl, order)
+            assert got_pb[96:] == bytes(32), (nv, vl, order)  # re-armed
+        pb[64:96].zero_()
+        side = torch.cuda.Stream(device=gpu)
+        ev = torch.cuda.Event()
+        ev.record()
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            D.merkle_finish_nodes_pair(vnodes, cv, nv, pb, 1)
+        D.merkle_finish_nodes_pair(nodes, c1, n, pb, 0)
+        torch.cuda.synchronize()
+        got_pb = bytes(pb.cpu().numpy())
+        assert got_pb[64:96] == want_s and got_pb[96:] == bytes(32), (nv, vl)
 
 
 def test_state_hasher_schedules_agree(gpu):

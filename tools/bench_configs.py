@@ -178,12 +178,12 @@ def run_config(args):
         bal = R.synthetic_balances(n, seed + 3)
         rec = torch.from_numpy(reg.records.view(np.uint8).reshape(-1).copy()).to(dev)
         dbal = torch.from_numpy(bal.view(np.uint8).copy()).to(dev)
-        # registry.DeviceStateHasher (schedule "list"): the registry root in one
-        # call (the struct kernel also hashes the registry tree's level-1
-        # windows), the balances tree beside it on a high-priority stream, then
-        # Keccak(reg_root || bal_root).  PRYSM_C3_SCHED=level1|two: the other
+        # registry.DeviceStateHasher (schedule "level1"): one launch for the
+        # struct roots and both trees' level-1 windows, then the two trees'
+        # top levels side by side, the second finisher hashing
+        # Keccak(reg_root || bal_root).  PRYSM_C3_SCHED=list|two: the other
         # schedules (A/B only)
-        hasher = R.DeviceStateHasher(n, dev, schedule=os.environ.get("PRYSM_C3_SCHED", "list"))
+        hasher = R.DeviceStateHasher(n, dev, schedule=os.environ.get("PRYSM_C3_SCHED", "level1"))
 
         def step():
             return hasher.submit(rec, dbal)

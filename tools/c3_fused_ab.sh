@@ -1,5 +1,5 @@
 #!/bin/bash
-# C3 A/B over registry.DeviceStateHasher's schedules (level1 = default, list, two = round 3), alternating processes
+# C3 A/B over registry.DeviceStateHasher schedules (level1 = default, list, two = round 3), alternating processes
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 O=gpurun_out/$1
