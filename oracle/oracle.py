@@ -11,6 +11,10 @@ Reference algorithms restated (file:line under the reference root):
   * ``merkle_hash``    shared/ssz/hash.go:194-239
   * ``deposit_trie``   shared/trieutil/deposit_trie.go:29-81
   * ``merkle_root``    shared/hashutil/merkleRoot.go:12-30
+  * ``DepositContract`` contracts/deposit-contract/depositContract.v.py:24-71
+    (the same trie kept by the ETH1 contract: the second implementation of
+    config 5's tree in the reference, with the deposit-data layout and the
+    per-log previous_deposit_root that powchain checks)
 Parity pins: hashutil/hash_test.go:13-31 KATs, ssz/hash_test.go:35-178
 vectors, ssz/example_and_test.go:105,144 (see tests/golden/).
 """
@@ -237,6 +241,46 @@ class DictTrie:
 
     def root(self) -> bytes:  # Root (:61-63)
         return self.m.get(1, bytes(32))
+
+
+class DepositContract:
+    """Restatement of the Vyper deposit contract's tree
+    (contracts/deposit-contract/depositContract.v.py): deposit_data =
+    to_bytes(amount) || to_bytes(timestamp) || deposit_input (:26-27, :43;
+    to_bytes = the low 8 bytes of the uint256, big-endian), leaf at heap index
+    count + 2^32 (:44, :49), every ancestor rehashed from its two children
+    with missing map keys reading as 0^32 (:50-52), root = node 1 (:31-32),
+    branch = the sibling at each level (:65-71).  deposit() returns the
+    Deposit event (:46): (previous_deposit_root, deposit_data, index bytes)."""
+
+    def __init__(self, depth: int = DEPOSIT_TREE_DEPTH):
+        self.depth, self.count, self.tree = depth, 0, {}
+
+    @staticmethod
+    def to_bytes(value: int) -> bytes:
+        return (value % (1 << 256)).to_bytes(32, "big")[24:]
+
+    def get_deposit_root(self) -> bytes:
+        return self.tree.get(1, bytes(32))
+
+    def deposit(self, amount_gwei: int, timestamp: int, deposit_input: bytes):
+        data = self.to_bytes(amount_gwei) + self.to_bytes(timestamp) + bytes(deposit_input)
+        index = self.count + (1 << self.depth)
+        event = (self.get_deposit_root(), data, self.to_bytes(index))
+        self.tree[index] = keccak256(data)
+        for _ in range(self.depth):
+            index //= 2
+            self.tree[index] = keccak256(self.tree.get(2 * index, bytes(32)) + self.tree.get(2 * index + 1, bytes(32)))
+        self.count += 1
+        return event
+
+    def get_branch(self, leaf: int):
+        index = leaf + (1 << self.depth)
+        out = []
+        for _ in range(self.depth):
+            out.append(self.tree.get(index ^ 1, bytes(32)))
+            index //= 2
+        return out
 
 
 def verify_merkle_branch(leaf: bytes, branch, depth: int, index: int, root: bytes,

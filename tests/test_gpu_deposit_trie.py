@@ -261,3 +261,34 @@ def test_save_logs_matches_reference_loop(gpu, start, k, bad):
     t.UpdateDepositTrie(extra)
     ref.update(extra)
     assert t.Root() == ref.root()
+
+
+@pytest.mark.parametrize("k,missed", [(1, None), (50, None), (50, 20), (300, 0)])
+def test_save_logs_of_deposit_contract_events(gpu, k, missed):
+    """The node side of the ETH1 contract: the Deposit events of the
+    contract restatement (depositContract.v.py:36-52; each carries the
+    contract's root before its deposit) fed to mk_deposit_trie_save_logs.
+    Every log is accepted and the trie's Root() and branches equal the
+    contract's get_deposit_root / get_branch.  With one log lost on the way
+    (`missed`), the ones after it carry roots the trie never had: they are
+    all skipped, and the trie stays at the root before the gap."""
+    import random
+
+    from oracle import oracle as O
+    from prysm_amd import trieutil as T
+
+    rng = random.Random(k * 31 + (missed or 0))
+    c = O.DepositContract()
+    events = [c.deposit(32 * 10**9, 1_540_000_000 + i, bytes(rng.getrandbits(8) for _ in range(264)))
+              for i in range(k)]
+    seen = [e for j, e in enumerate(events) if j != missed]
+    t = T.DepositTrie(32)
+    got = t.save_logs([e[1] for e in seen], [e[0] for e in seen])
+    if missed is None:
+        assert got == [True] * k
+        assert t.Root() == c.get_deposit_root()
+        for idx in sorted({0, k // 2, k - 1}):
+            assert t.GenerateMerkleBranch(idx) == c.get_branch(idx), idx
+    else:
+        assert got == [True] * missed + [False] * (k - 1 - missed)
+        assert t.Root() == events[missed][0]

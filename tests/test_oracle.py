@@ -144,6 +144,35 @@ def test_incremental_c_restatement_equals_dict_and_batch(n):
     assert O.deposit_trie_incremental_root(deps) == t.root() == O.deposit_trie_levels(deps)[0]
 
 
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 6, 33])
+def test_deposit_contract_equals_trieutil(n):
+    """The reference keeps config 5's tree twice: trieutil.DepositTrie
+    (deposit_trie.go:29-63) and the Vyper deposit contract
+    (depositContract.v.py:36-71).  The contract restatement's roots, branches
+    and per-deposit events against the dict restatement and the batch build
+    over the contract's own deposit-data layout (8-B big-endian amount and
+    timestamp, then the 264-B DepositInput of C5)."""
+    rng = np.random.default_rng(11 + n)
+    c, t = O.DepositContract(), _DictTrie()
+    datas = []
+    for i in range(n):
+        amount = 32 * 10**9 - int(rng.integers(0, 1000))
+        ts = 1_540_000_000 + i
+        ev = c.deposit(amount, ts, bytes(rng.integers(0, 256, 264, dtype=np.uint8)))
+        assert ev[0] == t.root()  # previous_deposit_root: the root before this deposit
+        assert ev[2] == (i + (1 << 32)).to_bytes(8, "big")
+        assert ev[1][:8] == amount.to_bytes(8, "big") and ev[1][8:16] == ts.to_bytes(8, "big")
+        assert len(ev[1]) == 280
+        t.update(ev[1])
+        datas.append(ev[1])
+        assert c.get_deposit_root() == t.root()
+    root, levels = O.deposit_trie_levels(datas)
+    assert c.get_deposit_root() == root == (t.root() if n else bytes(32))
+    for i in range(n):
+        assert c.get_branch(i) == t.branch(i)
+        assert O.verify_merkle_branch(O.keccak256(datas[i]), c.get_branch(i), 32, i, root)
+
+
 def test_restatement_fixtures_reproduce(res_vectors):
     for c in res_vectors["merkle_flat"][::17]:
         items = O.splitmix_bytes(c["n"] * c["item_len"], c["seed"])
