@@ -182,16 +182,19 @@ int mk_dev_ssz_merkle_finish_nodes(mk_call* call, const void* d_nodes, uint64_t 
 /* The same finisher for one field of a two-field struct whose fields are
  * both lists (hash.go:141-159; the State{registry, balances} of BASELINE
  * config 3): the list root goes to d_pair_block[32 slot, 32 slot + 32), and
- * whichever of the two finishers (slot 0 and slot 1, launched in any order on
- * any streams; neither waits for the other) completes second writes the
- * struct root Keccak(d_pair_block[0, 64)) to d_pair_block[64, 96) and
- * re-arms the arrival counter at d_pair_block[96, 100).  The block
- * (MK_PAIR_BLOCK_BYTES, 16-B aligned) must be zero before its first use; the
- * caller waits for both finishers before reading the struct root. */
+ * whichever of the two finishers of one pair (slot 0 and slot 1, the same
+ * `epoch`, launched in any order on any streams; neither waits for the other)
+ * completes second writes the struct root Keccak(d_pair_block[0, 64)) to
+ * d_pair_block[64, 96).  d_pair_block[96, 100) is the arrival word: zero
+ * before the block's first use, then owned by the finishers.  Each pair takes
+ * an epoch in 1 .. 2^30 - 1 different from the previous pair's on the block
+ * (a counter), so a pair left half-done by a failed call never completes with
+ * the next one.  The block is MK_PAIR_BLOCK_BYTES, 16-B aligned; the caller
+ * waits for both finishers before reading the struct root. */
 #define MK_PAIR_BLOCK_BYTES 128
 int mk_dev_ssz_merkle_finish_nodes_pair(mk_call* call, const void* d_nodes, uint64_t count, uint64_t n_total,
-                                        void* d_pair_block, uint32_t slot, void* d_ws, uint64_t ws_bytes,
-                                        void* stream);
+                                        void* d_pair_block, uint32_t slot, uint32_t epoch, void* d_ws,
+                                        uint64_t ws_bytes, void* stream);
 /* Finisher on one device: the reference level loop over the `nroots`
  * gathered shard roots (odd -> 0^128 pad), then Keccak(root || le64(n) || 0^24). */
 int mk_dev_ssz_merkle_finish(mk_call* call, const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32,

@@ -72,7 +72,7 @@ _SIGS = {
     "mk_dev_ssz_merkle_node_frontier": (_int, [_cp, _vp, _u64, _u32, _u32, _int, _vp, _vp, _vp, _u64, _vp]),
     "mk_ssz_merkle_finish_workspace_bytes": (_u64, [_u64]),
     "mk_dev_ssz_merkle_finish_nodes": (_int, [_cp, _vp, _u64, _u64, _vp, _vp, _u64, _vp]),
-    "mk_dev_ssz_merkle_finish_nodes_pair": (_int, [_cp, _vp, _u64, _u64, _vp, _u32, _vp, _u64, _vp]),
+    "mk_dev_ssz_merkle_finish_nodes_pair": (_int, [_cp, _vp, _u64, _u64, _vp, _u32, _u32, _vp, _u64, _vp]),
     "mk_ssz_merkle_hash_multi": (_int, [_cp, _vp, _u64, _u32, _int, _vp, _vp]),
     "mk_dev_ssz_merkle_hash_multi": (_int, [_cp, _vp, _u64, _u32, _int, _vp, _vp]),
     "mk_ssz_struct_msg_len": (_u64, [_vp, _u32]),

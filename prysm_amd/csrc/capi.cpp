@@ -309,7 +309,7 @@ uint64_t lock_grid_cap(hipStream_t st) {
 }
 
 int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t* d_ws, uint64_t ws_bytes,
-                hipStream_t st, uint8_t* pair_block = nullptr, uint32_t pair_slot = 0) {
+                hipStream_t st, uint8_t* pair_block = nullptr, uint32_t pair_slot = 0, uint32_t pair_epoch = 0) {
     if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
     if (p.small && pair_block) return fail(MK_EINVAL, "internal: pair finalize needs a k_wave3 plan");
     if (p.small) {
@@ -333,6 +333,7 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
         if (a.finalize && pair_block) {  // a two-field struct root (wave3_spread_final)
             a.pair_block = pair_block;
             a.pair_slot = pair_slot;
+            a.pair_epoch = pair_epoch;
             a.out = pair_block + 32 * pair_slot;
         }
         ProfRec rec{};
@@ -485,7 +486,7 @@ int dev_merkle_hash(const void* d_items, uint64_t n, uint32_t item_len, void* d_
 }
 
 int dev_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32, hipStream_t st,
-               void* d_pair_block = nullptr, uint32_t pair_slot = 0) {
+               void* d_pair_block = nullptr, uint32_t pair_slot = 0, uint32_t pair_epoch = 0) {
     if (nroots == 0 || nroots > 2 * mk::kWave2Span)
         return fail(MK_EINVAL, "nroots %llu out of range (1..%u)", (unsigned long long)nroots, 2 * mk::kWave2Span);
     if (!d_roots || (!d_out32 && !d_pair_block)) return fail(MK_EINVAL, "null pointer");
@@ -503,6 +504,7 @@ int dev_finish(const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_o
     if (d_pair_block) {
         a.pair_block = (uint8_t*)d_pair_block;
         a.pair_slot = pair_slot;
+        a.pair_epoch = pair_epoch;
         a.out = (uint8_t*)d_pair_block + 32 * pair_slot;
     }
     launch_wave3<false>(mk::kWaveThreads, 1, a, st);
@@ -518,14 +520,15 @@ uint64_t finish_ws_bytes(uint64_t count) {
 }
 
 int dev_finish_nodes(const void* d_nodes, uint64_t count, uint64_t n_total, void* d_out32, void* d_ws,
-                     uint64_t ws_bytes, hipStream_t st, void* d_pair_block = nullptr, uint32_t pair_slot = 0) {
+                     uint64_t ws_bytes, hipStream_t st, void* d_pair_block = nullptr, uint32_t pair_slot = 0,
+                     uint32_t pair_epoch = 0) {
     if (count <= 2 * mk::kWave2Span)
-        return dev_finish(d_nodes, count, n_total, d_out32, st, d_pair_block, pair_slot);
+        return dev_finish(d_nodes, count, n_total, d_out32, st, d_pair_block, pair_slot, pair_epoch);
     if (!d_nodes || (!d_out32 && !d_pair_block)) return fail(MK_EINVAL, "null pointer");
     Plan p;
     TRY(mk::make_plan(count, 32, false, 0, false, ((uintptr_t)d_nodes % 16) == 0, p, true, 0, n_total));
     return launch_plan(p, (const uint8_t*)d_nodes, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st,
-                       (uint8_t*)d_pair_block, pair_slot);
+                       (uint8_t*)d_pair_block, pair_slot, pair_epoch);
 }
 
 // ---- TreeHash of a list of byte strings (makeSliceHasher + hashedEncoding) ---------------
@@ -1833,16 +1836,17 @@ int mk_dev_ssz_merkle_finish_nodes(mk_call* call, const void* d_nodes, uint64_t 
 }
 
 int mk_dev_ssz_merkle_finish_nodes_pair(mk_call* call, const void* d_nodes, uint64_t count, uint64_t n_total,
-                                        void* d_pair_block, uint32_t slot, void* d_ws, uint64_t ws_bytes,
-                                        void* stream) {
+                                        void* d_pair_block, uint32_t slot, uint32_t epoch, void* d_ws,
+                                        uint64_t ws_bytes, void* stream) {
     Scope S(call);
     int rc = bind_stream((hipStream_t)stream);
     if (rc) return S.done(rc);
     if (!d_pair_block) return S.done(fail(MK_EINVAL, "null pointer"));
     if (slot > 1) return S.done(fail(MK_EINVAL, "pair slot %u out of range (0..1)", slot));
+    if (epoch == 0 || epoch >= (1u << 30)) return S.done(fail(MK_EINVAL, "pair epoch %u out of range (1..2^30-1)", epoch));
     if ((uintptr_t)d_pair_block % 16) return S.done(fail(MK_EINVAL, "pair block not 16-B aligned"));
     return S.done(dev_finish_nodes(d_nodes, count, n_total, nullptr, d_ws, ws_bytes, (hipStream_t)stream,
-                                   d_pair_block, slot));
+                                   d_pair_block, slot, epoch));
 }
 
 int mk_dev_ssz_merkle_finish(mk_call* call, const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32,

@@ -1144,7 +1144,10 @@ __device__ __forceinline__ void wave3_spread_levels(uint32_t* lds, uint64_t& c, 
 // balances} of BASELINE config 3): out is this field's slot of the pair
 // block, and the second of the two finishers to arrive -- they run as
 // separate launches on two streams, neither waits for the other -- hashes
-// K(slot 0 || slot 1) into pair[64..96) and re-arms the counter.
+// K(slot 0 || slot 1) into pair[64..96).  Arrival word pair[24] = epoch << 2 |
+// arrived-slot bits: a finisher of a newer epoch than the word's starts the
+// mask afresh, so a pair left half-done (a failed launch) cannot pair with the
+// next one.
 __device__ __forceinline__ void spread_store_digest(uint32_t e, uint32_t o, uint32_t L, uint32_t* out) {
     if (L < 4u) {
         out[2 * L] = ilv::spread16(e) | (ilv::spread16(o) << 1);
@@ -1152,7 +1155,7 @@ __device__ __forceinline__ void spread_store_digest(uint32_t e, uint32_t o, uint
     }
 }
 __device__ __forceinline__ void wave3_spread_final(const uint32_t* lds, uint64_t n_items, uint32_t* out,
-                                                   uint32_t* pair = nullptr) {
+                                                   uint32_t* pair = nullptr, uint32_t slot = 0, uint32_t epoch = 0) {
     const uint32_t L = threadIdx.x & 63u;
     const spread::Lane cst = spread::lane_consts(L);
     const uint32_t i = cst.i;
@@ -1170,11 +1173,22 @@ __device__ __forceinline__ void wave3_spread_final(const uint32_t* lds, uint64_t
     spread::keccak_f(e, o, cst);
     spread_store_digest(e, o, L, out);
     if (!pair) return;
-    __threadfence();  // this field's root is visible before the arrival count
-    uint32_t old = 0;
-    if (L == 0) old = atomicAdd(pair + 24, 1u);
-    old = __shfl(old, 0);
-    if (old != 1u) return;  // the other field's finisher is still running: it completes the pair
+    __threadfence();  // this field's root is visible before its arrival bit
+    uint32_t second = 0;
+    if (L == 0) {
+        uint32_t* word = pair + 24;
+        uint32_t old = atomicAdd(word, 0u);  // an atomic read of the arrival word
+        for (;;) {
+            const uint32_t nw = ((old >> 2) == epoch ? old : epoch << 2) | (1u << slot);
+            const uint32_t seen = atomicCAS(word, old, nw);
+            if (seen == old) {
+                second = (nw & 3u) == 3u;
+                break;
+            }
+            old = seen;
+        }
+    }
+    if (!__shfl(second, 0)) return;  // the other field's finisher is still running: it completes the pair
     __threadfence();
     const volatile uint32_t* both = pair;
     uint32_t e2 = 0u, o2 = 0u;
@@ -1188,7 +1202,6 @@ __device__ __forceinline__ void wave3_spread_final(const uint32_t* lds, uint64_t
     if (i == 16u) o2 ^= 0x80000000u;
     spread::keccak_f(e2, o2, cst);
     spread_store_digest(e2, o2, L, pair + 16);
-    if (L == 0) atomicExch(pair + 24, 0u);  // re-armed for the next pair
 }
 
 template <uint32_t NT, bool LEAF>
@@ -1268,7 +1281,9 @@ __global__ __launch_bounds__(NT) void k_wave3(ReduceArgs a) {
     if (MK_WAVE3_SPREAD) wave3_spread_levels<NT>(lds, c, m, left, done, a.pad_at_one);
     uint32_t* out = reinterpret_cast<uint32_t*>(a.out);
     if (MK_WAVE3_SPREAD && a.finalize) {
-        if (tid < 64) wave3_spread_final(lds, a.n_items, out, reinterpret_cast<uint32_t*>(a.pair_block));
+        if (tid < 64)
+            wave3_spread_final(lds, a.n_items, out, reinterpret_cast<uint32_t*>(a.pair_block), a.pair_slot,
+                               a.pair_epoch);
     } else if (a.finalize) {
         if (k == 0) {  // K(root || le64(n) || 0^24) on lanes 0/1
             ilv::Half s;

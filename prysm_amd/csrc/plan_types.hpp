@@ -41,9 +41,11 @@ struct ReduceArgs {
     uint32_t elem_len;     // LEAF, k_reduce_elem: `items` are n elements of elem_len bytes and the
                            // tree's 32-B items are their digests K(le32(elem_len) || element)
     uint8_t* pair_block;   // finalize (k_wave3), nullable: a two-field struct root -- the list root goes to
-                           // pair_block[32 pair_slot..), and the second of the two finishers to complete
-                           // writes K(pair_block[0..64)) to pair_block[64..96) (counter at [96..100))
+                           // pair_block[32 pair_slot..), and the second of the two finishers of epoch
+                           // pair_epoch to complete writes K(pair_block[0..64)) to pair_block[64..96)
+                           // (arrival word at [96..100))
     uint32_t pair_slot;
+    uint32_t pair_epoch;
 };
 
 // One list of a segmented (many-lists) merkleHash level: k_many_leaf /

@@ -260,18 +260,19 @@ def finish_workspace(count: int, device) -> torch.Tensor:
 
 
 def merkle_finish_nodes_pair(nodes: torch.Tensor, count: int, n_total: int, pair_block: torch.Tensor, slot: int,
-                             ws: torch.Tensor = None) -> None:
+                             epoch: int, ws: torch.Tensor = None) -> None:
     """merkle_finish_nodes for one list field of a two-field struct: the list
-    root goes to pair_block[32 slot:32 slot + 32]; whichever of the two
-    finishers (slot 0 and 1, any streams) completes second writes the struct
-    root Keccak(pair_block[0:64]) to pair_block[64:96].  ``pair_block``:
-    128 zeroed bytes before its first use (the finishers re-arm it)."""
+    root goes to pair_block[32 slot:32 slot + 32]; whichever of the pair's two
+    finishers (slot 0 and 1, the same ``epoch``, any streams) completes
+    second writes the struct root Keccak(pair_block[0:64]) to
+    pair_block[64:96].  ``pair_block``: 128 bytes, zeroed before its first
+    use; ``epoch``: 1 .. 2^30 - 1, a new one per pair."""
     dev = _dev(nodes)
     if pair_block.numel() < 128:
         raise ValueError("pair block of 128 bytes")
     if ws is None:
         ws = finish_workspace(count, nodes.device)
-    _lib.invoke("mk_dev_ssz_merkle_finish_nodes_pair", _p(nodes), count, n_total, _p(pair_block), slot, _p(ws),
+    _lib.invoke("mk_dev_ssz_merkle_finish_nodes_pair", _p(nodes), count, n_total, _p(pair_block), slot, epoch, _p(ws),
                 ws.numel(), _stream(nodes.device), device=dev)
 
 

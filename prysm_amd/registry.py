@@ -169,8 +169,9 @@ class DeviceStateHasher:
         self.cb1 = -(-8 * n // 256)  # level-1 nodes of the balances tree
         self.bnodes = torch.empty(max(32, 32 * self.cb1), dtype=torch.uint8, device=device)
         self.bfin_ws = D.finish_workspace(self.cb1, device) if lv1 else None
-        # reg_root || bal_root || state root || arrival counter (zero before first use)
+        # reg_root || bal_root || state root || arrival word (zero before first use)
         self.pair_block = torch.zeros(128, dtype=torch.uint8, device=device) if lv1 else None
+        self.epoch = 0  # one per submit (mk_dev_ssz_merkle_finish_nodes_pair)
         self.bal_ws = D.merkle_workspace(n, 8, device)
         self.pair = torch.empty(64, dtype=torch.uint8, device=device)  # reg_root || bal_root
         # the state root ("level1": the pair finisher writes it into the pair block)
@@ -200,10 +201,11 @@ class DeviceStateHasher:
             self.side.wait_event(self.ev_roots)
             # the two trees' latency-bound levels side by side; whichever
             # finisher completes second hashes Keccak(reg_root || bal_root)
+            self.epoch = self.epoch % ((1 << 30) - 1) + 1
             with torch.cuda.stream(self.side):
-                D.merkle_finish_nodes_pair(self.bnodes, self.cb1, n, self.pair_block, 1, ws=self.bfin_ws)
+                D.merkle_finish_nodes_pair(self.bnodes, self.cb1, n, self.pair_block, 1, self.epoch, ws=self.bfin_ws)
                 self.ev_bal.record(self.side)
-            D.merkle_finish_nodes_pair(self.nodes, self.c1, n, self.pair_block, 0, ws=self.fin_ws)
+            D.merkle_finish_nodes_pair(self.nodes, self.c1, n, self.pair_block, 0, self.epoch, ws=self.fin_ws)
             cur.wait_event(self.ev_bal)
             return self.out
         if sched == "list":

@@ -186,33 +186,45 @@ def test_struct_list_root_windows_vs_oracle(gpu, n):
         want_v = O.merkle_hash_flat(vals, nv, vl, nthreads=16)
         assert bytes(gv.cpu().numpy()) == want_v, (nv, vl)
         # the pair finisher: each field's root into its slot, the second to
-        # complete hashes Keccak(slot 0 || slot 1) and re-arms the counter;
-        # both orders on one stream, then the two on two streams at once
+        # complete hashes Keccak(slot 0 || slot 1); both orders on one stream,
+        # then the two on two streams at once, each pair with a new epoch
         pb = torch.zeros(128, dtype=torch.uint8, device=gpu)
         want_s = O.keccak256(want + want_v)
+        epoch = 0
         for order in ((0, 1), (1, 0)):
             pb[64:96].zero_()
+            epoch += 1
             for slot in order:  # cv may be 1: the one-node finisher
                 if slot == 0:
-                    D.merkle_finish_nodes_pair(nodes, c1, n, pb, 0)
+                    D.merkle_finish_nodes_pair(nodes, c1, n, pb, 0, epoch)
                 else:
-                    D.merkle_finish_nodes_pair(vnodes, cv, nv, pb, 1)
+                    D.merkle_finish_nodes_pair(vnodes, cv, nv, pb, 1, epoch)
             torch.cuda.synchronize()
             got_pb = bytes(pb.cpu().numpy())
             assert got_pb[:32] == want and got_pb[32:64] == want_v, (nv, vl, order)
             assert got_pb[64:96] == want_s, (nv, vl, order)
-            assert got_pb[96:] == bytes(32), (nv, vl, order)  # re-armed
+            assert int.from_bytes(got_pb[96:100], "little") == (epoch << 2) | 3, (nv, vl, order)
+        # a pair left half-done (only slot 0 ran) does not complete with the next
         pb[64:96].zero_()
+        D.merkle_finish_nodes_pair(nodes, c1, n, pb, 0, epoch + 1)
+        torch.cuda.synchronize()
+        assert bytes(pb[64:96].cpu().numpy()) == bytes(32)
+        D.merkle_finish_nodes_pair(nodes, c1, n, pb, 0, epoch + 2)
+        torch.cuda.synchronize()
+        assert bytes(pb[64:96].cpu().numpy()) == bytes(32), "slot 0 of a new epoch completed a stale pair"
         side = torch.cuda.Stream(device=gpu)
         ev = torch.cuda.Event()
         ev.record()
         side.wait_event(ev)
         with torch.cuda.stream(side):
-            D.merkle_finish_nodes_pair(vnodes, cv, nv, pb, 1)
-        D.merkle_finish_nodes_pair(nodes, c1, n, pb, 0)
+            D.merkle_finish_nodes_pair(vnodes, cv, nv, pb, 1, epoch + 2)
+        D.merkle_finish_nodes_pair(nodes, c1, n, pb, 0, epoch + 2)  # slot 0 twice in one epoch: idempotent
         torch.cuda.synchronize()
-        got_pb = bytes(pb.cpu().numpy())
-        assert got_pb[64:96] == want_s and got_pb[96:] == bytes(32), (nv, vl)
+        assert bytes(pb[64:96].cpu().numpy()) == want_s, (nv, vl)
+        with pytest.raises(Exception):
+            D.merkle_finish_nodes_pair(nodes, c1, n, pb, 2, epoch + 3)
+        with pytest.raises(Exception):
+            D.merkle_finish_nodes_pair(nodes, c1, n, pb, 0, 0)
 
 
 def test_state_hasher_schedules_agree(gpu):
