@@ -318,6 +318,25 @@ int mk_dev_deposit_trie_append(mk_call* call, void* d_levels, uint64_t capacity,
 int mk_dev_deposit_trie_build(mk_call* call, void* d_levels, uint64_t capacity, const void* d_data,
                               const uint64_t* d_offs, uint64_t n, uint32_t fixed_len, uint32_t d_to, uint32_t depth,
                               void* d_root32, void* stream);
+/* A stream of equal-size tries with each trie's wide top folded into the
+ * NEXT trie's front: levels 0..2 of the trie in d_levels (its leaves and the
+ * nodes over 2 and 4 of them) and, in the same launch, levels 3..7 of the
+ * previous trie in d_prev_levels (NULL for the first trie; the same n and
+ * capacity; its levels 0..2 from the previous call).  Then
+ * mk_dev_deposit_trie_pipe_top(d_prev_levels, ..) finishes the previous trie
+ * (on another stream, beside the next front), and
+ * mk_dev_deposit_trie_levels(d_levels, .., 2, depth) the last one.  Takes what mk_deposit_trie_pipe_ok accepts (280-B deposits, 16-B
+ * aligned, n a multiple of 4096 and at most 4096 x the CU count, depth >= 7);
+ * MK_EINVAL otherwise. */
+int mk_deposit_trie_pipe_ok(const void* d_data, uint64_t n, uint32_t deposit_len, uint32_t depth);
+/* Levels 8 .. depth and the root of a trie whose levels 0..7 are complete
+ * (a pipelined front's previous trie), in launches of at most one wave per
+ * SIMD, which run beside the next pipelined front instead of after it. */
+int mk_dev_deposit_trie_pipe_top(mk_call* call, void* d_levels, uint64_t capacity, uint64_t count, uint32_t depth,
+                                 void* d_root32, void* stream);
+int mk_dev_deposit_trie_build_pipe(mk_call* call, void* d_levels, void* d_prev_levels, uint64_t capacity,
+                                   const void* d_data, uint64_t n, uint32_t deposit_len, uint32_t depth,
+                                   void* stream);
 /* Levels d_from+1 .. d_to of the batch build of a `count`-deposit trie whose
  * level d_from is complete (the root to d_root32 when d_to == depth): lets a
  * caller hash the leaves and the wide levels of trie i+1 on one stream while

@@ -1069,8 +1069,12 @@ int launch_trie_spread(void* d_levels, uint64_t cap, uint32_t d, uint64_t lo, ui
 
 // Levels d_from+1 .. d_to of the batch build over `n` deposits, level d_from
 // complete; the root (level depth node 0) to d_root32 when d_to == depth.
+// nt_max / spread_max: the largest k_trie_top3 workgroup and k_trie_spread
+// wave count (256 / 4: at most one wave per SIMD, which fits beside a
+// resident k_trie_rec_lock<1024, 4, true> workgroup of 104 VGPRs).
 int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from, uint32_t d_to, uint32_t depth,
-                      void* d_root32, hipStream_t st) {
+                      void* d_root32, hipStream_t st, uint32_t nt_max = mk::kMidThreads,
+                      uint32_t spread_max = mk::kSpreadWavesMax) {
     // Wide levels: one launch per level (every lane busy); the narrow top
     // (<= 2^17 nodes) plus the zero-sibling tail: k_trie_top3 (bit-interleaved
     // lane pairs), log2(NT) levels per workgroup of NT inputs, the last
@@ -1087,7 +1091,7 @@ int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from,
     }
     bool root_done = false;
     while (d < d_to) {
-        if (MK_TRIE_SPREAD && c <= 2 * mk::kSpreadWavesMax) {  // the last <= 5 levels + zero-sibling tail
+        if (MK_TRIE_SPREAD && c <= 2 * spread_max) {  // the last <= 5 levels + zero-sibling tail
             void* root = d_to == depth ? d_root32 : nullptr;
             TRY(launch_trie_spread(d_levels, cap, d, 0, c, d_to, depth, root, st));
             root_done = root != nullptr;
@@ -1095,14 +1099,14 @@ int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from,
             break;
         }
         uint32_t nt = mk::kWaveThreads;
-        while (nt < mk::kMidThreads && ceil_div(c, nt) > kTrieTopWgs) nt *= 2;
-        while (nt < mk::kMidThreads && c <= mk::kMidThreads && c > nt) nt *= 2;  // the last <= 1024 nodes in one WG
+        while (nt < nt_max && ceil_div(c, nt) > kTrieTopWgs) nt *= 2;
+        while (nt < nt_max && c <= nt_max && c > nt) nt *= 2;  // the last <= nt_max nodes in one WG
         const uint64_t nwg = ceil_div(c, nt);
         uint32_t k = nwg == 1 ? d_to - d : std::min<uint32_t>(ilog2(nt), d_to - d);
         if (MK_TRIE_SPREAD && nwg == 1) {  // stop where k_trie_spread takes over
             uint64_t cc = c;
             uint32_t kk = 0;
-            while (kk < k && cc > 2 * mk::kSpreadWavesMax) {
+            while (kk < k && cc > 2 * spread_max) {
                 cc = (cc + 1) / 2;
                 ++kk;
             }
@@ -1170,8 +1174,8 @@ int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t*
     // persistent: every workgroup runs the same number of groups where possible
     const uint64_t cap_wg = std::min<uint64_t>(MK_TRIE_LOCK_GRID, lock_grid_cap(st));
     const uint64_t grid = ceil_div(ng, ceil_div(ng, cap_wg));
-    hipLaunchKernelGGL((mk::k_trie_rec_lock<NT, DPT>), dim3(grid), dim3(NT), 0, st, (const uint2*)d_data, ng, L[0],
-                       L[1], L[2], L[3]);
+    hipLaunchKernelGGL((mk::k_trie_rec_lock<NT, DPT, false>), dim3(grid), dim3(NT), 0, st, (const uint2*)d_data, ng,
+                       L[0], L[1], L[2], L[3], mk::TriePrev{});
     HIPCHK(hipGetLastError());
     const uint64_t done = ng * NT * DPT;
     if (done < n) {
@@ -1179,6 +1183,36 @@ int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t*
         TRY(trie_suffix_levels(d_levels, cap, n, done, nlv, st));
     }
     return trie_levels_range(d_levels, cap, n, nlv, d_to, depth, d_root32, st);
+}
+
+// A stream of tries with the previous trie's wide top in the front's
+// lock-step slots (k_trie_rec_lock<1024, 4, true>): 280-B deposits at a 16-B
+// aligned address, n a whole number of 4096-deposit groups, one group per
+// workgroup (n / 4096 <= the stream's CUs), depth >= 7.
+bool trie_pipe_ok(const void* d_data, uint64_t n, uint32_t fixed_len, uint32_t depth, hipStream_t st) {
+    constexpr uint64_t G = 1024 * 4;
+    return MK_TRIE_LOCK && fixed_len == 280 && ((uintptr_t)d_data % 16) == 0 && n >= G && n % G == 0 &&
+           n / G <= std::min<uint64_t>(MK_TRIE_LOCK_GRID, lock_grid_cap(st)) && depth >= 7;
+}
+
+// Levels 0..2 of the trie in d_levels and levels 3..7 of the previous one in
+// d_prev (NULL: none), one launch.
+int trie_front_pipe(void* d_levels, void* d_prev, uint64_t cap, const void* d_data, uint64_t n, uint32_t depth,
+                    hipStream_t st) {
+    if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
+    uint4* L[4];
+    for (uint32_t d = 0; d < 4; ++d) L[d] = trie_level(d_levels, cap, d);
+    mk::TriePrev prev{};
+    if (d_prev) {
+        prev.l2 = trie_level(d_prev, cap, 2);
+        for (uint32_t k = 0; k < 5; ++k) prev.l[k] = trie_level(d_prev, cap, 3 + k);
+        prev.live = 1;
+    }
+    const uint64_t ng = n / (1024 * 4);
+    hipLaunchKernelGGL((mk::k_trie_rec_lock<1024, 4, true>), dim3(ng), dim3(1024), 0, st, (const uint2*)d_data, ng,
+                       L[0], L[1], L[2], L[3], prev);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
 }
 
 int dev_trie_append(void* d_levels, uint64_t cap, uint64_t count, const void* d_data, const uint64_t* d_offs,
@@ -2104,6 +2138,38 @@ int mk_dev_deposit_trie_build(mk_call* call, void* d_levels, uint64_t capacity, 
         return S.done(fail(MK_EINVAL, "null pointer"));
     return S.done(trie_front(d_levels, capacity, d_data, d_offs, n, fixed_len, d_to, depth,
                              d_to == depth ? d_root32 : nullptr, (hipStream_t)stream));
+}
+
+int mk_deposit_trie_pipe_ok(const void* d_data, uint64_t n, uint32_t deposit_len, uint32_t depth) {
+    return trie_pipe_ok(d_data, n, deposit_len, depth, nullptr) ? 1 : 0;
+}
+
+int mk_dev_deposit_trie_build_pipe(mk_call* call, void* d_levels, void* d_prev_levels, uint64_t capacity,
+                                   const void* d_data, uint64_t n, uint32_t deposit_len, uint32_t depth,
+                                   void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    rc = check_trie(capacity, 0, n, depth);
+    if (rc) return S.done(rc);
+    if (!d_levels || !d_data) return S.done(fail(MK_EINVAL, "null pointer"));
+    if (d_prev_levels == d_levels) return S.done(fail(MK_EINVAL, "the previous trie's levels alias this trie's"));
+    if (!trie_pipe_ok(d_data, n, deposit_len, depth, (hipStream_t)stream))
+        return S.done(fail(MK_EINVAL, "pipelined front needs 280-B deposits, 16-B aligned, n a multiple of 4096 "
+                                      "with one group per CU, depth >= 7 (n = %llu)", (unsigned long long)n));
+    return S.done(trie_front_pipe(d_levels, d_prev_levels, capacity, d_data, n, depth, (hipStream_t)stream));
+}
+
+int mk_dev_deposit_trie_pipe_top(mk_call* call, void* d_levels, uint64_t capacity, uint64_t count, uint32_t depth,
+                                 void* d_root32, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    rc = check_trie(capacity, count, 0, depth);
+    if (rc) return S.done(rc);
+    if (!d_levels || !d_root32 || count == 0) return S.done(fail(MK_EINVAL, "null pointer or empty trie"));
+    if (depth < 7) return S.done(fail(MK_EINVAL, "depth %u < 7", depth));
+    return S.done(trie_levels_range(d_levels, capacity, count, 7, depth, depth, d_root32, (hipStream_t)stream, 256, 4));
 }
 
 int mk_dev_deposit_trie_levels(mk_call* call, void* d_levels, uint64_t capacity, uint64_t count, uint32_t d_from,

@@ -2219,10 +2219,23 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 #define MK_TRIE_DMA_ROUND 12
 #endif
 
-template <uint32_t NT, int DPT>
+// PIPE (a stream of tries, pipeline.TriePipeline): workgroup b also takes the
+// previous trie's subtree over its level-2 nodes [1024 b, 1024 b + 1024) up
+// to level 7: 512 + 256 + 128 + 64 + 32 node permutations.  Each wave does
+// ONE of them (level 3 on waves 0-7, 4 on 8-11, 5 on 12-13, 6 on 14, 7 on
+// 15, one node per lane) as an extra lock-step permutation inserted into its
+// own sequence, so every wave runs 16 permutations and the same barriers; a
+// level is inserted at least one whole permutation after the level it reads
+// was stored (slots 0, 3, 7, 10, 15: between deposits, where no state is
+// live), through L2 (same CU, lines it never read).  The 15 per-thread permutations of the front cost 15 slots alone;
+// the previous trie's wide top levels cost one more instead of a separate
+// latency-bound pass beside the front.
+template <uint32_t NT, int DPT, bool PIPE>
 __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict__ in, uint64_t ngroups,
                                                          uint4* __restrict__ L0, uint4* __restrict__ L1,
-                                                         uint4* __restrict__ L2, uint4* __restrict__ L3) {
+                                                         uint4* __restrict__ L2, uint4* __restrict__ L3,
+                                                         TriePrev prev) {
+    static_assert(!PIPE || (NT == 1024 && DPT == 4), "the previous-trie slots assume 16 waves x 4 deposits");
     constexpr uint32_t NW = 35;  // 8-B words per deposit
     constexpr int NLV = DPT == 8 ? 3 : DPT == 4 ? 2 : 1;
     static_assert(DPT == 2 || DPT == 4 || DPT == 8, "deposits per thread");
@@ -2257,6 +2270,39 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
             qp[1] = q1;
         }
     };
+    // the previous trie's level k node of this lane (waves of level k only)
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
+    auto prev_slot = [&](int k) {
+        const uint32_t w0 = 16u - (16u >> (k - 3)), per = 512u >> (k - 3);  // first wave, nodes per workgroup
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));  // computed here, not hoisted and kept live across the loop
+        const uint32_t j = 64u * (wv - w0) + ln;
+        const bool act = prev.live && j < per;
+        const uint32_t jg = blockIdx.x * per + j;  // < 2^19: 32-bit offsets from the uniform bases
+        const uint4* src = k == 3 ? prev.l2 : prev.l[k - 4];
+        asm volatile("" ::: "memory");
+        State s;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = act ? src[4 * jg + q] : make_uint4(0, 0, 0, 0);
+            s.lo[2 * q] = v.x;
+            s.hi[2 * q] = v.y;
+            s.lo[2 * q + 1] = v.z;
+            s.hi[2 * q + 1] = v.w;
+        }
+#pragma unroll
+        for (int w = 8; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
+        s.lo[8] = 1u;  // byte 64
+        s.hi[16] = 0x80000000u;
+        keccak_f_digest_lock(s);
+        if (act) {
+            uint4 d0, d1;
+            digest(s, d0, d1);
+            prev.l[k - 3][2 * jg] = d0;
+            prev.l[k - 3][2 * jg + 1] = d1;
+        }
+        asm volatile("" ::: "memory");
+    };
     uint64_t g = blockIdx.x;
     uint2 tnext = make_uint2(0, 0);
     if (g < ngroups) {
@@ -2270,6 +2316,11 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
         uint4 kl0[NLV], kl1[NLV];                   // the pending left node of each level
 #pragma unroll
         for (int i = 0; i < DPT; ++i) {
+            // the previous trie's slots sit between deposits (no state live)
+            if (PIPE && i == 0 && wv < 8) prev_slot(3);                // slot 0
+            if (PIPE && i == 1 && (wv >> 2) == 2) prev_slot(4);        // slot 3
+            if (PIPE && i == 2 && (wv == 12 || wv == 13)) prev_slot(5);  // slot 7
+            if (PIPE && i == 3 && wv == 14) prev_slot(6);              // slot 10
             State s;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 0 and the tail word landed
             flush();
@@ -2329,11 +2380,14 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                 dst = lv[l + 1] + 2 * ((r0 + i) >> (l + 1));
             }
         }
+        if (PIPE && wv == 15) prev_slot(7);  // slot 15
     }
     flush();
 }
-template __global__ void k_trie_rec_lock<MK_TRIE_LOCK_NT, MK_TRIE_LOCK_DPT>(const uint2*, uint64_t, uint4*, uint4*,
-                                                                           uint4*, uint4*);
+template __global__ void k_trie_rec_lock<MK_TRIE_LOCK_NT, MK_TRIE_LOCK_DPT, false>(const uint2*, uint64_t, uint4*,
+                                                                                  uint4*, uint4*, uint4*, TriePrev);
+template __global__ void k_trie_rec_lock<1024, 4, true>(const uint2*, uint64_t, uint4*, uint4*, uint4*, uint4*,
+                                                        TriePrev);
 
 // ----------------------------------------------------------------------------
 // Deposit trie level: node j = K(in[2j] || (2j+1 < cin ? in[2j+1] : 0^32)),

@@ -84,8 +84,17 @@ template <int NW>
 __global__ void k_keccak_rec(const uint2* in, uint64_t n, uint4* out);
 // Phase-locked deposit-trie front: leaves + levels 1..log2(DPT) of a trie of
 // 280-B deposits, ngroups * NT * DPT deposits (the host runs the rest).
-template <uint32_t NT, int DPT>
-__global__ void k_trie_rec_lock(const uint2* in, uint64_t ngroups, uint4* L0, uint4* L1, uint4* L2, uint4* L3);
+// PIPE: the same launch also builds levels 3..7 of the PREVIOUS trie of a
+// stream (one wave-wide permutation per wave, in the lock-step slots, see
+// the kernel); one group per workgroup.
+struct TriePrev {
+    const uint4* l2;  // the previous trie's level 2 (complete)
+    uint4* l[5];      // its levels 3..7 (written)
+    uint32_t live;    // 0: no previous trie (the slots hash zeros, store nothing)
+};
+template <uint32_t NT, int DPT, bool PIPE>
+__global__ void k_trie_rec_lock(const uint2* in, uint64_t ngroups, uint4* L0, uint4* L1, uint4* L2, uint4* L3,
+                                TriePrev prev);
 #ifndef MK_TRIE_LOCK
 #define MK_TRIE_LOCK 1
 #endif

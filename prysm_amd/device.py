@@ -358,6 +358,27 @@ def deposit_trie_build(levels: torch.Tensor, capacity: int, data: torch.Tensor, 
     return levels
 
 
+def deposit_trie_pipe_ok(data: torch.Tensor, n: int, deposit_len: int, depth: int) -> bool:
+    """Whether deposit_trie_build_pipe takes this stream shape."""
+    return bool(_lib.load().mk_deposit_trie_pipe_ok(_p(data), n, deposit_len, depth))
+
+
+def deposit_trie_build_pipe(levels: torch.Tensor, prev_levels, capacity: int, data: torch.Tensor, n: int,
+                            deposit_len: int, depth: int) -> None:
+    """Levels 0..2 of this trie and levels 3..7 of the previous trie of the
+    stream (``prev_levels``, None for the first) in one launch
+    (mk_dev_deposit_trie_build_pipe)."""
+    _lib.invoke("mk_dev_deposit_trie_build_pipe", _p(levels), None if prev_levels is None else _p(prev_levels),
+                capacity, _p(data), n, deposit_len, depth, _stream(levels.device), device=_dev(levels))
+
+
+def deposit_trie_pipe_top(levels: torch.Tensor, capacity: int, count: int, depth: int, root: torch.Tensor) -> None:
+    """Levels 8 .. depth and the root of a pipelined front's previous trie,
+    in launches that fit beside the next front (mk_dev_deposit_trie_pipe_top)."""
+    _lib.invoke("mk_dev_deposit_trie_pipe_top", _p(levels), capacity, count, depth, _p(root), _stream(levels.device),
+                device=_dev(levels))
+
+
 def deposit_trie_levels(levels: torch.Tensor, capacity: int, count: int, d_from: int, d_to: int, depth: int,
                         root: torch.Tensor = None) -> None:
     """Levels d_from+1 .. d_to of the batch build (level d_from complete);

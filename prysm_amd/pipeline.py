@@ -86,26 +86,41 @@ class MerklePipeline:
 class TriePipeline:
     """Batch builds of a stream of deposit tries (one trie per ``submit``,
     trieutil.DepositTrie semantics, deposit_trie.go:29-63) with each trie's
-    narrow top off the main stream.
+    narrow top off the critical path.
 
-    Per trie, on the caller's current stream: the leaf hashes
-    (Hash(deposit), one launch) and the wide levels, down to the first level
-    of at most 2^17 nodes (one launch per level, every lane busy).  On a
-    high-priority side stream, overlapping the next trie's leaves: the
-    latency-bound top (k_trie_top3 launches) plus the zero-sibling levels
-    up to ``depth`` and the root.  Level arrays and roots rotate over
-    ``slots`` sets (two by default: 2/3/4 sets and a wait every 2-3 submits
-    measured the same, profiles/r02r/ring_ab.jsonl): a submit waits for the
-    top of the trie ``slots`` submits back; a returned root stays valid for
-    the next ``slots - 1`` submits."""
+    ``front="pipe"`` (the default where mk_deposit_trie_pipe_ok takes the
+    shape: 280-B deposits, n a multiple of 4096 up to 4096 x the CU count):
+    trie i's leaves and levels 1-2 run in one phase-locked launch that also
+    builds levels 3-7 of trie i-1 in its lock-step slots
+    (mk_dev_deposit_trie_build_pipe); trie i-1's remaining top (levels 8 ..
+    depth and the root) then runs on a high-priority side stream beside trie
+    i+1's front.  A trie's root is therefore written one submit later: the
+    tensor ``submit`` returns is produced once the next ``submit`` or
+    ``flush()`` has been called (then synchronise, or wait on ``side``).
+    Level arrays and roots rotate over four sets; a returned root stays
+    valid for the next two submits after it is produced.
+
+    ``front="split"`` (other shapes): per trie, on the caller's current
+    stream, the leaf hashes and the wide levels down to the first level of at
+    most 2^17 nodes; on the side stream, overlapping the next trie's leaves,
+    the latency-bound top (k_trie_top3 launches), the zero-sibling levels up
+    to ``depth`` and the root.  ``slots`` sets (two by default: 2/3/4 sets
+    and a wait every 2-3 submits measured the same, profiles/r02r/
+    ring_ab.jsonl); a submit waits for the top of the trie ``slots`` submits
+    back; the returned root is written by the time the side stream has run
+    this submit's work, and stays valid for the next ``slots - 1`` submits."""
 
     TOP_MAX = 1 << 17  # capi.cpp kTrieTopMax: levels at or below this width run k_trie_top3
+    PIPE_TOP_FROM = 7  # the last level the pipelined front builds for the previous trie
 
     def __init__(self, n: int, deposit_len: int, depth: int, device, split: Optional[int] = None,
-                 slots: int = 2, wait_every: int = 1):
+                 slots: int = 2, wait_every: int = 1, front: str = "auto"):
         """``split``: the first level built on the side stream (default: the
         first level of at most TOP_MAX nodes); ``slots``, ``wait_every``:
-        parallel.SlotRing."""
+        parallel.SlotRing (split front); ``front``: "auto" (pipe where the
+        shape allows), "pipe" or "split"."""
+        if front not in ("auto", "pipe", "split"):
+            raise ValueError(f"unknown front {front!r}")
         self.n, self.dl, self.depth = n, deposit_len, depth
         self.device = torch.device(device)
         if split is None:
@@ -113,25 +128,84 @@ class TriePipeline:
             while split < depth and -(-n // (1 << split)) > self.TOP_MAX:
                 split += 1
         self.split = split
+        self.front = front
+        nsets = max(slots, 4) if front != "split" else slots
         nbytes = D.deposit_trie_levels_bytes(n, depth)
         self._ring = SlotRing(slots, wait_every)
-        self.levels = [torch.empty(nbytes, dtype=torch.uint8, device=self.device) for _ in range(slots)]
-        self.roots = [torch.empty(32, dtype=torch.uint8, device=self.device) for _ in range(slots)]
+        self.levels = [torch.empty(nbytes, dtype=torch.uint8, device=self.device) for _ in range(nsets)]
+        self.roots = [torch.empty(32, dtype=torch.uint8, device=self.device) for _ in range(nsets)]
         self.side = torch.cuda.Stream(device=self.device, priority=-1)  # its own hardware queue
+        self._i = 0
+        self._pending = None  # pipe: the set of the trie whose levels 3.. are not built yet
+        self._done = {}  # pipe: trie index -> event after its top
+
+    def _use_pipe(self, deposits: torch.Tensor) -> bool:
+        if self.front == "split":
+            return False
+        ok = D.deposit_trie_pipe_ok(deposits, self.n, self.dl, self.depth)
+        if self.front == "pipe" and not ok:
+            raise ValueError("pipelined front: 280-B deposits, n a multiple of 4096 within the CU count")
+        return ok
 
     def submit(self, deposits: torch.Tensor) -> torch.Tensor:
         """Enqueue the trie of n fixed-length deposits held in ``deposits``;
-        returns its (32,) root tensor, produced on ``self.side``."""
+        returns its (32,) root tensor, produced on ``self.side`` (pipe: once
+        the next submit or flush() has run)."""
         if deposits.numel() < self.n * self.dl:
             raise ValueError("deposit buffer shorter than n * deposit_len")
         cur = torch.cuda.current_stream(self.device)
-        slot = self._ring.acquire(cur)
-        lv, root = self.levels[slot], self.roots[slot]
-        D.deposit_trie_build(lv, self.n, deposits, self.n, self.dl, self.split, self.depth)
+        pipe = self._use_pipe(deposits)
+        if pipe != getattr(self, "_last_pipe", pipe):  # the two forms share the sets: drain on a switch
+            self.flush()
+            cur.wait_stream(self.side)
+        self._last_pipe = pipe
+        if not pipe:
+            slot = self._ring.acquire(cur)
+            lv, root = self.levels[slot], self.roots[slot]
+            D.deposit_trie_build(lv, self.n, deposits, self.n, self.dl, self.split, self.depth)
+            self.side.wait_stream(cur)
+            with torch.cuda.stream(self.side):
+                D.deposit_trie_levels(lv, self.n, self.n, self.split, self.depth, self.depth, root)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+            self._ring.release(ev)
+            return root
+        nsets = len(self.levels)
+        i = self._i
+        s = i % nsets
+        self._i += 1
+        # set s was last used by trie i - nsets, whose top (levels 8.. on the
+        # side stream) must be done.  One cross-stream wait every second
+        # submit (each costs ~10 us of command-processor time), on the top of
+        # trie i - nsets + 1: the side stream runs in order, so it covers the
+        # tries of this submit and the next.
+        if i % 2 == 0:
+            ev = self._done.get(i - nsets + 1)
+            if ev is not None:
+                cur.wait_event(ev)
+        self._done.pop(i - nsets - 1, None)
+        prev = self._pending
+        D.deposit_trie_build_pipe(self.levels[s], None if prev is None else self.levels[prev], self.n, deposits,
+                                  self.n, self.dl, self.depth)
+        if prev is not None:
+            self._top(i - 1, prev, self.PIPE_TOP_FROM, cur)
+        self._pending = s
+        return self.roots[s]
+
+    def _top(self, trie: int, s: int, d_from: int, cur) -> None:
         self.side.wait_stream(cur)
         with torch.cuda.stream(self.side):
-            D.deposit_trie_levels(lv, self.n, self.n, self.split, self.depth, self.depth, root)
+            if d_from == self.PIPE_TOP_FROM:  # beside the next front: one wave per SIMD at most
+                D.deposit_trie_pipe_top(self.levels[s], self.n, self.n, self.depth, self.roots[s])
+            else:
+                D.deposit_trie_levels(self.levels[s], self.n, self.n, d_from, self.depth, self.depth, self.roots[s])
             ev = torch.cuda.Event()
             ev.record(self.side)
-        self._ring.release(ev)
-        return root
+        self._done[trie] = ev
+
+    def flush(self) -> None:
+        """Finish the last pipelined trie (its levels 3 .. depth and root on
+        the side stream); a no-op when nothing is pending."""
+        if self._pending is not None:
+            self._top(self._i - 1, self._pending, 2, torch.cuda.current_stream(self.device))
+            self._pending = None

@@ -292,3 +292,59 @@ def test_save_logs_of_deposit_contract_events(gpu, k, missed):
     else:
         assert got == [True] * missed + [False] * (k - 1 - missed)
         assert t.Root() == events[missed][0]
+
+
+@pytest.mark.parametrize("n", [4096, 5 * 4096, 1 << 18])
+def test_trie_pipeline_pipelined_front(gpu, n):
+    """TriePipeline's "pipe" front: trie t's leaves + levels 1-2 in one
+    phase-locked launch that also builds levels 3-7 of trie t-1 in its
+    lock-step slots, trie t-1's top beside trie t+1's front, the last trie by
+    flush().  Every root and branches of three tries (the levels the slots
+    wrote among them) against the oracle's batch build; bad shapes refused."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import _lib
+    from prysm_amd import device as D
+    from prysm_amd.pipeline import TriePipeline
+
+    ln, depth = 280, 32
+    pipe = TriePipeline(n, ln, depth, gpu)
+    datas = []
+    for t in range(4):
+        d = torch.empty(n * ln, dtype=torch.uint8, device=gpu)
+        D.synth_fill(d, SEED + 950 + t)
+        datas.append(d)
+    assert D.deposit_trie_pipe_ok(datas[0], n, ln, depth)
+    got, handles = [], []
+    for t, d in enumerate(datas):
+        handles.append(pipe.submit(d))
+        if t:
+            torch.cuda.synchronize()
+            got.append(bytes(handles[t - 1].cpu().numpy()))
+    assert pipe._last_pipe
+    pipe.flush()
+    torch.cuda.synchronize()
+    got.append(bytes(handles[-1].cpu().numpy()))
+    wants = []
+    for t, d in enumerate(datas):
+        host = d.cpu().numpy()
+        root, levels = O.deposit_trie_levels([bytes(host[i * ln:(i + 1) * ln]) for i in range(n)])
+        assert got[t] == root, (t, n)
+        wants.append(levels)
+    # tries 1..3 still hold their levels (sets 1, 2, 0)
+    for t in (1, 2, 3):
+        lv = pipe.levels[t % len(pipe.levels)]
+        for idx in sorted({0, n // 3, n - 1}):
+            br = torch.empty(32 * depth, dtype=torch.uint8, device=gpu)
+            D.deposit_trie_branch(lv, n, n, depth, idx, br)
+            torch.cuda.synchronize()
+            want = b"".join(wants[t][d][(idx >> d) ^ 1] if ((idx >> d) ^ 1) < len(wants[t][d]) else bytes(32)
+                            for d in range(depth))
+            assert bytes(br.cpu().numpy()) == want, (t, idx)
+    lv = pipe.levels[0]
+    with pytest.raises(_lib.MerkleError):
+        D.deposit_trie_build_pipe(lv, None, n + 1, datas[0], n + 1, ln, depth)  # not whole groups
+    with pytest.raises(_lib.MerkleError):
+        D.deposit_trie_build_pipe(lv, lv, n, datas[0], n, ln, depth)  # aliasing sets
+    assert not D.deposit_trie_pipe_ok(datas[0], n, 200, depth)

@@ -290,16 +290,33 @@ def run_config(args):
                                                                P(root), st()), "c5")
         sec_one = _timeit(one, args.steps, args.warmup)  # one trie: leaves, levels, top, in order
         one_root = bytes(root.cpu().numpy())
-        # a stream of tries (TriePipeline): trie i's latency-bound top on a
-        # high-priority side stream overlaps trie i+1's leaves and wide levels
+        # a stream of tries (TriePipeline, front "pipe" at this shape): trie
+        # i's leaves and levels 1-2 in one phase-locked launch that also builds
+        # levels 3-7 of trie i-1; trie i-1's top (levels 8-32, root) on a
+        # high-priority side stream beside trie i+1's front.  The last trie's
+        # top (flush) runs inside the timed region.  PRYSM_C5_FRONT=split: the
+        # round-3 form (A/B).
         from prysm_amd.pipeline import TriePipeline
 
-        pipe = TriePipeline(n, dl, depth, dev)
+        pipe = TriePipeline(n, dl, depth, dev, front=os.environ.get("PRYSM_C5_FRONT", "auto"))
         got = pipe.submit(data)
+        pipe.flush()
         torch.cuda.synchronize()
         if bytes(got.cpu().numpy()) != one_root:
             raise SystemExit("c5: pipelined root differs from the one-call root")
-        sec = _timeit(lambda: pipe.submit(data), args.steps, args.warmup)
+        front = "pipe" if pipe._last_pipe else "split"
+        for _ in range(args.warmup):
+            pipe.submit(data)
+        pipe.flush()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            got = pipe.submit(data)
+        pipe.flush()
+        torch.cuda.synchronize()
+        sec = (time.perf_counter() - t0) / args.steps
+        if bytes(got.cpu().numpy()) != one_root:
+            raise SystemExit("c5: last pipelined root differs from the one-call root")
         perms = 3 * n + (n - 1) + (depth - 20)
         hashes = n + (n - 1) + (depth - 20)
         cpu = None
@@ -329,7 +346,8 @@ def run_config(args):
         _line("deposit trie build, 2^20 x 280-B deposits, depth 32", n / sec, "deposits/s", args, sec, perms, hashes,
               {"workload": "C5: trieutil deposit trie, 2^20 synthetic 280-B deposits (stream of tries, "
                            "each trie's top overlapping the next trie's leaves)", "n": n,
-               "root": one_root.hex(), "pipelined": True, "split_level": pipe.split,
+               "root": one_root.hex(), "pipelined": True, "front": front,
+               "split_level": pipe.split if front == "split" else TriePipeline.PIPE_TOP_FROM,
                "single_trie_ms": sec_one * 1e3}, cpu)
         return
 
