@@ -11,6 +11,7 @@
 #                           tools/kernel_coverage.py: kernels compiled but never launched
 #   pytest:PATH             one test file / node id
 #   bench:CFG               bench.py --config CFG (c1 c2 c3 c4 c4tree c5), JSON line kept
+#                           (c1/c2/c3/c5: --steps 100 --warmup 20)
 #   profile:CFG:KERNEL      rocprofv3 kernel-trace stats + separate PMC passes of CFG's
 #                           bench line (tools/profile.sh); KERNEL = substring of the
 #                           dominant kernel's name for the summary (empty: C4's leaf kernel)
@@ -49,7 +50,10 @@ for step in "$@"; do
         > $O/$name.log 2>&1 || { tail -30 $O/$name.log; exit 1; }
       tail -1 $O/$name.log ;;
     bench)
-      timeout -k 10 400 python bench.py --config $a > $O/bench_$a.json 2> $O/bench_$a.err || { tail -5 $O/bench_$a.err; exit 1; }
+      # sub-millisecond side configs: 100 timed steps, so the window (not the
+      # clock ramp after the idle sync, nor a pipeline's drain) sets the figure
+      case $a in c4|c4tree) K="";; *) K="--steps 100 --warmup 20";; esac
+      timeout -k 10 400 python bench.py --config $a $K > $O/bench_$a.json 2> $O/bench_$a.err || { tail -5 $O/bench_$a.err; exit 1; }
       cat $O/bench_$a.json ;;
     profile)
       export KERNEL="${b:-k_leaf_lock_sc}"  # empty: the C4 leaf kernel
