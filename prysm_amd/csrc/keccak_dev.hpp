@@ -97,31 +97,15 @@ __device__ __forceinline__ void rho_pi_all(const State& a, uint32_t (&blo)[25], 
     (rho_pi_one<Is>(a, blo, bhi), ...);
 }
 
-// MK_SCHED=1 fences the round's phases (sched_barrier) so the half-rate
-// alignbit work (theta D, rho) issues in long runs instead of being
-// interleaved with the full-rate bitop3 work (tools/isa_rates: a wave stream
-// alternating full- and half-rate ops issues at ~4.4 cycles per instruction,
-// segmented streams cost less).
-#ifndef MK_SCHED
-#define MK_SCHED 0
-#endif
-#if MK_SCHED
-#define MK_SB() __builtin_amdgcn_sched_barrier(0)
-#else
-#define MK_SB()
-#endif
-
-// MK_ASM_ROUND=1 (default): the round with its instruction order fixed, one
-// asm volatile statement per VALU op, phases in sequence (20 bitop3 | 10
-// alignbit | 50 bitop3 | 48 alignbit | 52 bitop3/xor): four full-/half-rate
-// class switches per round.  The compiler's own schedule interleaves the
-// classes and issues ~2 % slower (tools/asm_round_probe.hip, register-resident
-// 43.4 vs 42.7 T ops/s; leaf kernel 2^28: 10.35 -> 10.13 ms in one-process
-// A/B); interleaving rho and chi row by row is slower still (41.7-42.1 T).
-// Register allocation stays with the compiler.
-#ifndef MK_ASM_ROUND
-#define MK_ASM_ROUND 1
-#endif
+// The round with its instruction order fixed: one asm volatile statement per
+// VALU op, phases in sequence (20 bitop3 | 10 alignbit | 50 bitop3 | 48
+// alignbit | 52 bitop3/xor): four full-/half-rate class switches per round.
+// The compiler's own schedule of the same C++ round interleaves the classes
+// and issued ~2 % slower (tools/asm_round_probe.hip, register-resident 43.4 vs
+// 42.7 T ops/s; leaf kernel 2^28: 10.35 -> 10.13 ms in one-process A/B);
+// interleaving rho and chi row by row is slower still (41.7-42.1 T); fencing
+// the C++ round's phases with sched_barrier did not change it.  Register
+// allocation stays with the compiler.
 __device__ __forceinline__ uint32_t ax3(uint32_t a, uint32_t b, uint32_t c) {
     uint32_t r;
     asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -220,46 +204,7 @@ __device__ __forceinline__ void round_asm(State& s, uint32_t rclo, uint32_t rchi
     s.hi[0] = axs(s.hi[0], rchi);
 }
 
-__device__ __forceinline__ void round_fn(State& s, uint32_t rclo, uint32_t rchi) {
-#if MK_ASM_ROUND
-    round_asm(s, rclo, rchi);
-    return;
-#endif
-    uint32_t clo[5], chi_[5];
-#pragma unroll
-    for (int x = 0; x < 5; ++x) {
-        clo[x] = xor3(xor3(s.lo[x], s.lo[x + 5], s.lo[x + 10]), s.lo[x + 15], s.lo[x + 20]);
-        chi_[x] = xor3(xor3(s.hi[x], s.hi[x + 5], s.hi[x + 10]), s.hi[x + 15], s.hi[x + 20]);
-    }
-    MK_SB();
-    uint32_t rlo[5], rhi[5];  // rotl(C[x], 1)
-#pragma unroll
-    for (int x = 0; x < 5; ++x) rotl64<1>(clo[x], chi_[x], rlo[x], rhi[x]);
-    MK_SB();
-#pragma unroll
-    for (int i = 0; i < 25; ++i) {
-        const int x = i % 5;
-        s.lo[i] = xor3(s.lo[i], clo[(x + 4) % 5], rlo[(x + 1) % 5]);
-        s.hi[i] = xor3(s.hi[i], chi_[(x + 4) % 5], rhi[(x + 1) % 5]);
-    }
-    MK_SB();
-    uint32_t blo[25], bhi[25];
-    rho_pi_all(s, blo, bhi, std::make_integer_sequence<int, 25>{});
-    MK_SB();
-#pragma unroll
-    for (int y = 0; y < 5; ++y) {
-#pragma unroll
-        for (int x = 0; x < 5; ++x) {
-            const int i = x + 5 * y;
-            const int i1 = (x + 1) % 5 + 5 * y, i2 = (x + 2) % 5 + 5 * y;
-            s.lo[i] = chi3(blo[i], blo[i1], blo[i2]);
-            s.hi[i] = chi3(bhi[i], bhi[i1], bhi[i2]);
-        }
-    }
-    s.lo[0] ^= rclo;
-    s.hi[0] ^= rchi;
-    MK_SB();
-}
+__device__ __forceinline__ void round_fn(State& s, uint32_t rclo, uint32_t rchi) { round_asm(s, rclo, rchi); }
 
 #ifndef MK_ROUND_UNROLL
 #define MK_ROUND_UNROLL 2
@@ -315,12 +260,8 @@ __device__ __forceinline__ void last_round_digest(State& s, uint32_t rclo, uint3
     s.hi[0] ^= rchi;
 }
 
-#ifndef MK_DIGEST_ROUND
-#define MK_DIGEST_ROUND 1
-#endif
 // Final permutation of a hash: only digest(s) may read the state afterwards.
 __device__ __forceinline__ void keccak_f_digest(State& s) {
-#if MK_DIGEST_ROUND
 #pragma unroll kRoundUnroll
     for (int r = 0; r < 22; ++r) round_fn(s, kRcLo[r], kRcHi[r]);
     round_fn(s, kRcLo[22], kRcHi[22]);
@@ -331,9 +272,6 @@ __device__ __forceinline__ void keccak_f_digest(State& s) {
     // them (117 -> 159 VGPRs, 4 -> 3 waves/SIMD).
     asm volatile("" : "+v"(s.lo[0]), "+v"(s.hi[0]), "+v"(s.lo[1]), "+v"(s.hi[1]), "+v"(s.lo[2]), "+v"(s.hi[2]),
                  "+v"(s.lo[3]), "+v"(s.hi[3]));
-#else
-    keccak_f(s);
-#endif
 }
 
 // Phase-locked permutations (round_asm<true>): every wave of the workgroup
@@ -400,30 +338,13 @@ __device__ __forceinline__ void pad_const(State& s) {
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 // Loads of the streamed inputs (items, node levels, deposit records): plain,
-// L2-allocating loads.  Non-temporal loads (MK_LD_NT=1, rounds 1-2) let the
-// leaf kernel's lines leave L2 before all of a window's 16-B loads had hit
-// them: 10.09 GB fetched per 2^28 launch against 8.90 GB with plain loads
-// (8.59 GB algorithmic), and the leaf pass ran 1.3-2.5 % slower
-// (profiles/r02zc/ab.txt, three boxes).
-#ifndef MK_LD_NT
-#define MK_LD_NT 0
-#endif
-__device__ __forceinline__ uint4 ld_stream(const uint4* p) {
-#if MK_LD_NT
-    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ uint2 ld_stream(const uint2* p) {
-#if MK_LD_NT
-    const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
-    return make_uint2(v.x, v.y);
-#else
-    return *p;
-#endif
-}
+// L2-allocating loads.  Non-temporal loads (rounds 1-2) let the leaf kernel's
+// lines leave L2 before all of a window's 16-B loads had hit them: 10.09 GB
+// fetched per 2^28 launch against 8.90 GB with plain loads (8.59 GB
+// algorithmic), and the leaf pass ran 1.3-2.5 % slower (profiles/r02zc/ab.txt,
+// three boxes).
+__device__ __forceinline__ uint4 ld_stream(const uint4* p) { return *p; }
+__device__ __forceinline__ uint2 ld_stream(const uint2* p) { return *p; }
 
 // Squeeze the 32-byte digest (lanes 0..3, little-endian).
 __device__ __forceinline__ void digest(const State& s, uint4& d0, uint4& d1) {

@@ -2146,12 +2146,6 @@ __global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ 
 #ifndef MK_REC_WAVES
 #define MK_REC_WAVES 1
 #endif
-// MK_REC_SPLIT: a block's 17 loads in two groups (the second issued once the
-// first is absorbed), so at most 9 words wait in VGPRs beside the state and
-// the kernel fits MK_REC_WAVES waves per SIMD.
-#ifndef MK_REC_SPLIT
-#define MK_REC_SPLIT 0
-#endif
 template <int NW>
 __global__ __launch_bounds__(kRecThreads, MK_REC_WAVES) void k_keccak_rec(const uint2* __restrict__ in, uint64_t n,
                                                                           uint4* __restrict__ out) {
@@ -2166,7 +2160,6 @@ __global__ __launch_bounds__(kRecThreads, MK_REC_WAVES) void k_keccak_rec(const 
         for (int b = 0; b < NB; ++b) {
 #pragma unroll
             for (int w = 0; w < 17; ++w) {
-                if (MK_REC_SPLIT && w == 9) asm volatile("" ::: "memory");
                 const int idx = 17 * b + w;
                 if (idx < NW) {
                     const uint2 v = p[idx];

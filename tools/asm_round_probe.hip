@@ -22,7 +22,7 @@
         }                                                          \
     } while (0)
 
-// mk::round_asm lives in keccak_dev.hpp (MK_ASM_ROUND).
+// mk::round_asm lives in keccak_dev.hpp.
 
 // Alternative fixed orders.  Lane b[X + 5Y] (after pi) comes from a[x + 5X]
 // with x = 3 (Y - 3X) mod 5.

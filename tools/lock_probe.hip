@@ -9,7 +9,6 @@
 //   lockS: 1024-thread workgroups, 1 per CU, s_barrier every S rounds
 // with no memory traffic.  Output: T int32 ops/s at 4320 ops per permutation.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../prysm_amd/csrc lock_probe.hip -o lock_probe
-//        (add -DMK_SCHED=1 for the phase-fenced round)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -35,7 +34,12 @@ __global__ __launch_bounds__(NT) void k_perm(uint32_t* out, int iters) {
         s.hi[i] = g ^ (0x9E3779B9u * (i + 1));
     }
 #pragma unroll 1
-    for (int k = 0; k < iters; ++k) mk::keccak_f_s<SYNC>(s);
+    for (int k = 0; k < iters; ++k) {
+        if constexpr (SYNC != 0)
+            mk::keccak_f_lock(s);  // the phase-locked round (an s_barrier per round)
+        else
+            mk::keccak_f(s);
+    }
     uint32_t x = 0;
 #pragma unroll
     for (int i = 0; i < 25; ++i) x ^= s.lo[i] ^ s.hi[i];
@@ -60,8 +64,8 @@ static void run(const char* name, int blocks, int iters, uint32_t* out) {
         if (ms < best) best = ms;
     }
     const double perms = (double)blocks * NT * iters;
-    printf("{\"test\": \"%s\", \"sched\": %d, \"threads\": %d, \"blocks\": %d, \"ms\": %.3f, \"Tops\": %.2f}\n", name,
-           MK_SCHED, NT, blocks, best, perms * 4320 / (best / 1e3) / 1e12);
+    printf("{\"test\": \"%s\", \"threads\": %d, \"blocks\": %d, \"ms\": %.3f, \"Tops\": %.2f}\n", name, NT,
+           blocks, best, perms * 4320 / (best / 1e3) / 1e12);
 }
 
 int main() {
