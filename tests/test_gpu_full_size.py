@@ -187,6 +187,31 @@ def test_c5_full_2p20_deposits(gpu):
 
 
 @pytest.mark.gpu
+def test_c5_full_2p20_pipelined_stream(gpu):
+    """The C5 bench's stream form at full size: three 2^20-deposit tries
+    through TriePipeline's pipelined front (each trie's levels 3-7 built in
+    the next trie's lock-step slots, its top beside the front after that,
+    the last one by flush); every root = the golden 2^20 root."""
+    import torch
+
+    from prysm_amd import device as D
+    from prysm_amd.pipeline import TriePipeline
+
+    g = GOLD["c5"]
+    n, dl, depth = g["n"], g["deposit_len"], g["depth"]
+    data = torch.empty(n * dl, dtype=torch.uint8, device=gpu)
+    D.synth_fill(data, g["seed"])
+    pipe = TriePipeline(n, dl, depth, gpu, front="pipe")
+    roots = [pipe.submit(data) for _ in range(3)]
+    torch.cuda.synchronize()
+    got = [bytes(roots[0].cpu().numpy()).hex(), bytes(roots[1].cpu().numpy()).hex()]
+    pipe.flush()
+    torch.cuda.synchronize()
+    got.append(bytes(roots[2].cpu().numpy()).hex())
+    assert got == [g["root"]] * 3
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 8])
 def test_c5_sharded_subtrees_on_one_device(gpu, world):
     """SURVEY §8e's C5 split at full size on one device: every shard's
