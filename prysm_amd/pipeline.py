@@ -129,15 +129,22 @@ class TriePipeline:
                 split += 1
         self.split = split
         self.front = front
-        nsets = max(slots, 4) if front != "split" else slots
-        nbytes = D.deposit_trie_levels_bytes(n, depth)
+        self._nbytes = D.deposit_trie_levels_bytes(n, depth)
+        self._slots = slots
         self._ring = SlotRing(slots, wait_every)
-        self.levels = [torch.empty(nbytes, dtype=torch.uint8, device=self.device) for _ in range(nsets)]
-        self.roots = [torch.empty(32, dtype=torch.uint8, device=self.device) for _ in range(nsets)]
+        # the pipelined form's four sets (allocated unless front == "split")
+        # and the split form's `slots` sets (allocated on its first use): the
+        # two forms never hand out the same root tensor
+        self.levels, self.roots = self._sets(4) if front != "split" else ([], [])
+        self._split_sets = None
         self.side = torch.cuda.Stream(device=self.device, priority=-1)  # its own hardware queue
         self._i = 0
         self._pending = None  # pipe: the set of the trie whose levels 3.. are not built yet
         self._done = {}  # pipe: trie index -> event after its top
+
+    def _sets(self, k: int):
+        return ([torch.empty(self._nbytes, dtype=torch.uint8, device=self.device) for _ in range(k)],
+                [torch.empty(32, dtype=torch.uint8, device=self.device) for _ in range(k)])
 
     def _use_pipe(self, deposits: torch.Tensor) -> bool:
         if self.front == "split":
@@ -155,13 +162,14 @@ class TriePipeline:
             raise ValueError("deposit buffer shorter than n * deposit_len")
         cur = torch.cuda.current_stream(self.device)
         pipe = self._use_pipe(deposits)
-        if pipe != getattr(self, "_last_pipe", pipe):  # the two forms share the sets: drain on a switch
+        if pipe != getattr(self, "_last_pipe", pipe):  # finish the other form's pending trie first
             self.flush()
-            cur.wait_stream(self.side)
         self._last_pipe = pipe
         if not pipe:
+            if self._split_sets is None:
+                self._split_sets = self._sets(self._slots)
             slot = self._ring.acquire(cur)
-            lv, root = self.levels[slot], self.roots[slot]
+            lv, root = self._split_sets[0][slot], self._split_sets[1][slot]
             D.deposit_trie_build(lv, self.n, deposits, self.n, self.dl, self.split, self.depth)
             self.side.wait_stream(cur)
             with torch.cuda.stream(self.side):

@@ -348,3 +348,40 @@ def test_trie_pipeline_pipelined_front(gpu, n):
     with pytest.raises(_lib.MerkleError):
         D.deposit_trie_build_pipe(lv, lv, n, datas[0], n, ln, depth)  # aliasing sets
     assert not D.deposit_trie_pipe_ok(datas[0], n, 200, depth)
+
+
+def test_trie_pipeline_mixed_fronts_and_flush(gpu):
+    """TriePipeline over a stream whose buffers switch between the pipelined
+    front (16-B aligned) and the split front (an 8-B-offset view), with a
+    flush in the middle: every root against the oracle's batch build."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+    from prysm_amd.pipeline import TriePipeline
+
+    n, ln, depth = 4096, 280, 32
+    pipe = TriePipeline(n, ln, depth, gpu)
+    store = torch.empty(n * ln + 16, dtype=torch.uint8, device=gpu)
+    plan = ["pipe", "pipe", "split", "pipe", "flush", "pipe", "split", "split", "pipe", "pipe"]
+    handles, wants = [], []
+    for t, step in enumerate(plan):
+        if step == "flush":
+            pipe.flush()
+            continue
+        off = 0 if step == "pipe" else 8
+        d = store[off:off + n * ln]
+        D.synth_fill(store, SEED + 970 + t)
+        assert D.deposit_trie_pipe_ok(d, n, ln, depth) == (step == "pipe")
+        host = d.cpu().numpy()
+        wants.append(O.deposit_trie_levels([bytes(host[i * ln:(i + 1) * ln]) for i in range(n)])[0])
+        handles.append(pipe.submit(d))
+        assert pipe._last_pipe == (step == "pipe")
+        torch.cuda.synchronize()  # the next fill rewrites the shared buffer
+        if len(handles) > 1:
+            # a split root is final once its submit has run; a pipelined one
+            # once the next submit (or flush) has
+            assert bytes(handles[-2].cpu().numpy()) == wants[-2], (t, step)
+    pipe.flush()
+    torch.cuda.synchronize()
+    assert bytes(handles[-1].cpu().numpy()) == wants[-1]

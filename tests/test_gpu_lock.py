@@ -249,3 +249,60 @@ def test_state_hasher_schedules_agree(gpu):
         torch.cuda.synchronize()
         assert bytes(out.cpu().numpy()) == want, sched
 
+
+
+def _finish_ref(nodes: bytes, n_total: int) -> bytes:
+    """merkleHash's level loop over 32-B nodes and its length mix-in
+    (hash.go:225-237: an odd level appends the 128-B zero chunk)."""
+    from oracle import oracle as O
+
+    lv = [nodes[32 * i:32 * i + 32] for i in range(len(nodes) // 32)]
+    while len(lv) > 1:
+        if len(lv) % 2:
+            lv.append(bytes(128))
+        lv = [O.keccak256(lv[2 * i] + lv[2 * i + 1]) for i in range(len(lv) // 2)]
+    return O.keccak256(lv[0] + n_total.to_bytes(8, "little") + bytes(24))
+
+
+def test_pair_finisher_many_pairs_random_order(gpu):
+    """60 pairs through one pair block, the two finishers launched in a
+    random order on two streams each time (sometimes slot 0 first, sometimes
+    slot 1, sometimes concurrently), a new epoch per pair and one pair in five
+    left half-done first (a failed call's leftover): every struct root equals
+    Keccak(root0 || root1) of that pair's inputs."""
+    import random
+
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    rng = random.Random(77)
+    side = torch.cuda.Stream(device=gpu)
+    pb = torch.zeros(128, dtype=torch.uint8, device=gpu)
+    for e in range(1, 61):
+        c0, c1 = rng.choice([1, 7, 100, 3000]), rng.choice([1, 64, 65, 2048])
+        a = torch.from_numpy(O.splitmix_bytes(32 * c0, 9000 + e).copy()).to(gpu)
+        b = torch.from_numpy(O.splitmix_bytes(32 * c1, 9500 + e).copy()).to(gpu)
+        want0 = _finish_ref(bytes(a.cpu().numpy()), c0)
+        want1 = _finish_ref(bytes(b.cpu().numpy()), c1)
+        if e % 5 == 0:  # a stale half of an earlier epoch
+            D.merkle_finish_nodes_pair(a, c0, c0, pb, rng.randrange(2), 10_000 + e)
+        order = rng.randrange(3)
+        ev = torch.cuda.Event()
+        ev.record()
+        side.wait_event(ev)
+        if order == 0:
+            D.merkle_finish_nodes_pair(a, c0, c0, pb, 0, e)
+            D.merkle_finish_nodes_pair(b, c1, c1, pb, 1, e)
+        elif order == 1:
+            D.merkle_finish_nodes_pair(b, c1, c1, pb, 1, e)
+            D.merkle_finish_nodes_pair(a, c0, c0, pb, 0, e)
+        else:
+            with torch.cuda.stream(side):
+                D.merkle_finish_nodes_pair(b, c1, c1, pb, 1, e)
+            D.merkle_finish_nodes_pair(a, c0, c0, pb, 0, e)
+        torch.cuda.synchronize()
+        got = bytes(pb.cpu().numpy())
+        assert got[:32] == want0 and got[32:64] == want1, e
+        assert got[64:96] == O.keccak256(want0 + want1), (e, order)
