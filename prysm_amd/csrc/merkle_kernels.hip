@@ -1818,35 +1818,32 @@ template __global__ void k_struct_reg<3, 6>(const uint8_t*, uint64_t, StructSpec
 // hashes its r bytes, plus 0^128 when they fill one chunk only (hash.go:225-228).
 __device__ __forceinline__ void window256_or_ragged(const uint8_t* __restrict__ base, uint64_t total, uint64_t w,
                                                     uint4& d0, uint4& d1) {
-    // one 8-B word per Keccak lane straight into the state, block by block:
-    // no staging registers beside the state (the struct kernel's window
-    // phase then needs no more VGPRs than its record loop)
-    const uint64_t rem = total - 256 * w;
-    const uint32_t r = rem < 256 ? (uint32_t)rem : 256u;           // 8..256 bytes
-    const uint32_t nwd = r / 8, pad = (r + (r <= 128 ? 128u : 0u)) / 8;  // the pad word (len % 8 == 0)
+    if (256 * w + 256 <= total) {
+        hash_window256(reinterpret_cast<const uint4*>(base) + 16 * w, d0, d1);
+        return;
+    }
+    const uint32_t r = (uint32_t)(total - 256 * w);                // 8..248 bytes
+    const uint32_t nwd = r / 8, len = r + (r <= 128 ? 128u : 0u);  // 136..256 B: two blocks
     const uint2* p = reinterpret_cast<const uint2*>(base + 256 * w);
     State s;
+    zero(s);
 #pragma unroll
-    for (int k = 0; k < 17; ++k) {
-        uint2 v = (uint32_t)k < nwd ? p[k] : make_uint2(0, 0);
-        if ((uint32_t)k == pad) v.x ^= 1u;
-        s.lo[k] = v.x;
-        s.hi[k] = v.y;
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int k = 0; k < 17; ++k) {
+            const uint32_t q = 17 * b + k;
+            uint2 v = q < nwd ? p[q] : make_uint2(0, 0);
+            if (q == len / 8) v.x ^= 1u;  // domain pad (len % 8 == 0)
+            s.lo[k] ^= v.x;
+            s.hi[k] ^= v.y;
+        }
+        if (b == 0) {
+            keccak_f(s);
+        } else {
+            s.hi[16] ^= 0x80000000u;
+            keccak_f_digest(s);
+        }
     }
-#pragma unroll
-    for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
-    keccak_f(s);
-    asm volatile("" ::: "memory");  // block 2's loads stay after the permutation
-#pragma unroll
-    for (int k = 0; k < 17; ++k) {
-        const uint32_t q = 17 + k;
-        uint2 v = q < nwd ? p[q] : make_uint2(0, 0);
-        if (q == pad) v.x ^= 1u;
-        s.lo[k] ^= v.x;
-        s.hi[k] ^= v.y;
-    }
-    s.hi[16] ^= 0x80000000u;
-    keccak_f_digest(s);
     digest(s, d0, d1);
 }
 
