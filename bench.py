@@ -63,20 +63,55 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def tree_work(n: int, item_len: int):
+    """(permutations, hashes) of merkleHash over n items of item_len bytes
+    (shared/ssz/hash.go:194-239): every message of m bytes
+    costs m // 136 + 1 permutations; the algorithmic op count of the whole
+    tree is perms x 4320 - hashes x 122."""
+    def p(m):
+        return m // 136 + 1
+
+    cb = (128 // item_len) * item_len if item_len < 128 else item_len
+    total = n * item_len
+    full, rem = divmod(total, cb)
+    count = full + (1 if rem else 0)
+    if count <= 1:  # a single (or empty: 0^128) chunk is the root's input
+        return p((rem or cb if n else 128) + 32), 1
+    pairs = count // 2
+    if count % 2:  # the last chunk alone, padded with 0^128
+        perms = pairs * p(2 * cb) + p((rem or cb) + 128)
+    else:
+        perms = (pairs - 1) * p(2 * cb) + p(cb + (rem or cb))
+    hashes = count = (count + 1) // 2
+    while count > 1:  # 64-B node pairs; an odd node + 0^128 is 160 B
+        perms += count // 2 + (2 if count % 2 else 0)
+        count = (count + 1) // 2
+        hashes += count
+    return perms + 1, hashes + 1  # the length mix-in K(root || le64(n) || 0^24)
+
+
 def cpu_baseline(item_len: int, log2n_sample: int, threads: int = 1):
     """The oracle (a C port of hash.go:194-239; 1 thread = the reference's
     single-goroutine shape, more threads split the tree by subtrees) on a
-    bounded sample of the same workload."""
+    bounded sample of the same workload, with the unrolled permutation
+    (oracle/keccak_fast.c: the 25-locals, rounds-unrolled shape of the
+    x/crypto keccakF1600 the reference runs, WORKSPACE:542-546)."""
     from oracle import oracle as O
 
     n = 1 << log2n_sample
     items = O.splitmix_bytes(n * item_len, SEED)
-    t0 = time.perf_counter()
-    O.merkle_hash_flat(items, n, item_len, nthreads=threads)
-    dt = time.perf_counter() - t0
+    perms, _ = tree_work(n, item_len)
+    with O.fast_permutation():
+        t0 = time.perf_counter()
+        O.merkle_hash_flat(items, n, item_len, nthreads=threads)
+        dt = time.perf_counter() - t0
+    ns = dt / perms * 1e9 * threads
     return {"value": n / dt, "unit": "leaves/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "ns_per_perm": ns,
             "sample": f"oracle/merkle_ref.c or_merkle_hash, 2^{log2n_sample} x {item_len}-B items "
-                      f"(same SplitMix64 stream), {threads} thread{'s' if threads > 1 else ''}, {dt:.1f} s"}
+                      f"(same SplitMix64 stream, {perms} perms), unrolled permutation (oracle/keccak_fast.c), "
+                      f"{threads} thread{'s' if threads > 1 else ''}, {dt:.1f} s, {ns:.0f} ns per permutation"
+                      f"{' per thread' if threads > 1 else ''}"}
 
 
 def leaf_kernel():
@@ -217,8 +252,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--log2n", type=int, default=28)
     ap.add_argument("--item-len", type=int, default=32)
-    ap.add_argument("--cpu-sample-log2n", type=int, default=26)
+    ap.add_argument("--cpu-sample-log2n", type=int, default=27)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-side-configs", action="store_true",
+                    help="N = 1: skip the C2/C3/C5/C1 side configs after the C4 line's own measurements")
+    ap.add_argument("--side-steps", type=int, default=200)
+    ap.add_argument("--side-warmup", type=int, default=40)
+    ap.add_argument("--no-single-gpu", action="store_true",
+                    help="N > 1: skip rank 0's single-GPU run of the whole tree (parallel_efficiency)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend (nccl = RCCL over xGMI; gloo only to rehearse N ranks on one GPU)")
     ap.add_argument("--share-device", action="store_true",
@@ -464,16 +505,27 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
         single_tree_ms = e0.elapsed_time(e1) / runs
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
-    per_rank = None
+    per_rank = per_rank_leaf_frac = None
+    nl = max(leaf_launches, 1)
     if world > 1:
-        # every rank's step time and leaf-kernel launch average, for the record
-        mine = torch.tensor([elapsed / args.steps * 1e3, leaf_ms / max(leaf_launches, 1)], dtype=torch.float64,
-                            device=t.device)
-        allr = torch.empty(world * 2, dtype=torch.float64, device=t.device)
-        dist.all_gather_into_tensor(allr, mine)
-        per_rank = [[round(x, 4) for x in allr[2 * r:2 * r + 2].tolist()] for r in range(world)]
+        # every rank's step time, leaf-kernel launch average and the ops of
+        # its average leaf launch, for the record
+        mine = torch.tensor([elapsed / args.steps * 1e3, leaf_ms / nl,
+                             leaf_perms / nl * INT_OPS_PER_PERM - leaf_hashes / nl * INT_OPS_SAVED_PER_HASH],
+                            dtype=torch.float64, device=t.device)
+        allr = torch.empty(world * 3, dtype=torch.float64, device=t.device).view(world, 3)
+        dist.all_gather_into_tensor(allr.view(-1), mine)
+        rows = allr.tolist()
+        per_rank = [[round(r[0], 4), round(r[1], 4)] for r in rows]
+        per_rank_leaf_frac = [round(r[2] / (r[1] / 1e3) / PEAK_INT_OPS, 4) if r[1] > 0 else None for r in rows]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = t.item()
+    # N > 1: the same whole tree on rank 0's GPU alone (MerklePipeline, the
+    # N = 1 bench's step, same steps/warmup), after the timed region, so the
+    # line carries its own strong-scaling efficiency t_1 / (N t_N)
+    single_gpu_ms = None
+    if world > 1 and rank == 0 and not args.no_single_gpu:
+        single_gpu_ms = single_gpu_step_ms(args, dev, n, item_len)
 
     if rank == 0:
         value = n * args.steps / t_max
@@ -483,7 +535,13 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
         ops_per_launch = perms_per_launch * INT_OPS_PER_PERM - hashes_per_launch * INT_OPS_SAVED_PER_HASH
         achieved = ops_per_launch / avg_leaf_s if avg_leaf_s > 0 else 0.0
         kname, kdesc = leaf_kernel()
-        traffic, clk, pmc_src = load_pmc(kname) if world == 1 and args.log2n == 28 else (None, None, None)
+        traffic, clk, pmc_src = load_pmc(kname) if args.log2n == 28 else (None, None, None)
+        if traffic is not None and world > 1:  # the committed PMC is of a whole 2^28 leaf launch
+            traffic *= local_n / n
+            pmc_src += f", scaled by this rank's {local_n}/{n} of the leaves"
+        step_s = t_max / args.steps
+        tree_perms, tree_hashes = tree_work(n, item_len)
+        tree_ops = tree_perms * INT_OPS_PER_PERM - tree_hashes * INT_OPS_SAVED_PER_HASH
         out = {
             "metric": "tree-hash leaves/sec @2^28 chunks (ssz.merkleHash, 32-B leaves)",
             "value": value,
@@ -511,7 +569,14 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
                        # finish] (parallel.PhaseTimer; pipelined: nodes/gather/finish overlap the
                        # next leaf pass, so their sum exceeds ms_per_step)
                        "phases_ms": phases["phases_ms"] if phases else None,
-                       "per_rank_phases_ms": phases["per_rank_phases_ms"] if phases else None},
+                       "per_rank_phases_ms": phases["per_rank_phases_ms"] if phases else None,
+                       # every rank's leaf-kernel fraction of one GPU's peak (its own launches)
+                       "per_rank_leaf_frac": per_rank_leaf_frac,
+                       # N > 1: the whole tree on rank 0's GPU alone, same steps, after the timed
+                       # region; parallel_efficiency = single_gpu_ms / (N x ms_per_step)
+                       "single_gpu_ms": single_gpu_ms,
+                       "parallel_efficiency": (single_gpu_ms / (world * step_s * 1e3)
+                                               if single_gpu_ms else None)},
             "roofline": {
                 "bound": "valu-int",
                 "kernel": kdesc,
@@ -532,6 +597,9 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
                 "hashes_per_launch": hashes_per_launch,
                 "avg_launch_ms": avg_leaf_s * 1e3,
                 "hbm_GBps_algorithmic": (local_n * item_len) / avg_leaf_s / 1e9 if avg_leaf_s > 0 else None,
+                # the whole step: the tree's algorithmic ops (tree_work) / (step time x N GPUs x peak)
+                "tree_perms": tree_perms,
+                "step_frac_aggregate": tree_ops / (step_s * world * PEAK_INT_OPS),
             },
         }
         if world == 1 and not args.no_cpu_baseline:
@@ -540,6 +608,20 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
             # also the restatement on the host's share of cores (16 on the GPU box)
             nt = min(16, len(os.sched_getaffinity(0)))
             out["cpu_baseline_threads"] = cpu_baseline(item_len, args.cpu_sample_log2n, threads=nt)
+        if world == 1 and not args.no_side_configs:
+            # every other BASELINE config, device-resident, >= 100 steps each,
+            # roots against tests/golden/full_size_roots.json (tools/bench_configs.py)
+            from tools.bench_configs import side_configs
+
+            del items, ws
+            pipe = None
+            torch.cuda.empty_cache()
+            log("side configs ...")
+            out["side_configs"] = side_configs(dev, steps=args.side_steps, warmup=args.side_warmup,
+                                               cpu=not args.no_cpu_baseline)
+            if not all(e.get("root_matches_golden") for e in out["side_configs"].values()):
+                log("ERROR: a side config's root differs from its golden (or it failed)")
+                status = 1
         print(json.dumps(out), flush=True)
     if world > 1:
         st = torch.tensor([status], dtype=torch.int32, device=dev if args.backend == "nccl" else "cpu")
@@ -547,6 +629,35 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
         status = int(st.item())
         dist.destroy_process_group()
     return status
+
+
+def single_gpu_step_ms(args, dev, n: int, item_len: int) -> float:
+    """ms per step of the whole n-item tree on this GPU alone: the N = 1
+    bench's pipelined step (pipeline.MerklePipeline), args.warmup untimed
+    and args.steps timed steps, wall clock bracketed by synchronize()."""
+    import torch
+
+    from prysm_amd import device as D
+    from prysm_amd.pipeline import MerklePipeline
+
+    log(f"rank 0: the whole 2^{args.log2n} tree on one GPU (parallel_efficiency) ...")
+    items = torch.empty(n * item_len, dtype=torch.uint8, device=dev)
+    D.synth_fill(items, SEED)
+    pipe = MerklePipeline(n, item_len, dev)
+    for _ in range(args.warmup):
+        pipe.submit(items)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r = pipe.submit(items)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    want = golden_root(args.log2n, item_len)
+    if want is not None and bytes(r.cpu().numpy()).hex() != want:
+        raise RuntimeError("single-GPU root differs from the golden root")
+    del items, pipe
+    torch.cuda.empty_cache()
+    return ms
 
 
 def run_c5_ranks(args, world: int, rank: int, local: int) -> int:

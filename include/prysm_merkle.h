@@ -187,10 +187,13 @@ int mk_dev_ssz_merkle_finish_nodes(mk_call* call, const void* d_nodes, uint64_t 
  * completes second writes the struct root Keccak(d_pair_block[0, 64)) to
  * d_pair_block[64, 96).  d_pair_block[96, 100) is the arrival word: zero
  * before the block's first use, then owned by the finishers.  Each pair takes
- * an epoch in 1 .. 2^30 - 1 different from the previous pair's on the block
- * (a counter), so a pair left half-done by a failed call never completes with
- * the next one.  The block is MK_PAIR_BLOCK_BYTES, 16-B aligned; the caller
- * waits for both finishers before reading the struct root. */
+ * the next epoch of a counter over 1 .. 2^30 - 1 (wrapping; "newer" = ahead by
+ * less than 2^29), so a pair left half-done by a failed call never completes
+ * with the next one, and a late finisher of an older epoch is ignored.  The
+ * first finisher of an epoch zeroes d_pair_block[64, 96), so a pair that
+ * never completes reads back as zeros, not as the previous pair's root.  The
+ * block is MK_PAIR_BLOCK_BYTES, 16-B aligned; the caller waits for both
+ * finishers before reading the struct root. */
 #define MK_PAIR_BLOCK_BYTES 128
 int mk_dev_ssz_merkle_finish_nodes_pair(mk_call* call, const void* d_nodes, uint64_t count, uint64_t n_total,
                                         void* d_pair_block, uint32_t slot, uint32_t epoch, void* d_ws,
@@ -325,10 +328,12 @@ int mk_dev_deposit_trie_build(mk_call* call, void* d_levels, uint64_t capacity, 
  * capacity; its levels 0..2 from the previous call).  Then
  * mk_dev_deposit_trie_pipe_top(d_prev_levels, ..) finishes the previous trie
  * (on another stream, beside the next front), and
- * mk_dev_deposit_trie_levels(d_levels, .., 2, depth) the last one.  Takes what mk_deposit_trie_pipe_ok accepts (280-B deposits, 16-B
- * aligned, n a multiple of 4096 and at most 4096 x the CU count, depth >= 7);
- * MK_EINVAL otherwise. */
-int mk_deposit_trie_pipe_ok(const void* d_data, uint64_t n, uint32_t deposit_len, uint32_t depth);
+ * mk_dev_deposit_trie_levels(d_levels, .., 2, depth) the last one.  Takes what
+ * mk_deposit_trie_pipe_ok accepts on the same stream (280-B deposits, 16-B
+ * aligned, n a multiple of 4096 and at most 4096 x the CUs the stream may
+ * use, depth >= 7); MK_EINVAL otherwise.  pipe_ok returns 1 or 0 (0 also
+ * when the stream cannot be bound). */
+int mk_deposit_trie_pipe_ok(const void* d_data, uint64_t n, uint32_t deposit_len, uint32_t depth, void* stream);
 /* Levels 8 .. depth and the root of a trie whose levels 0..7 are complete
  * (a pipelined front's previous trie), in launches of at most one wave per
  * SIMD, which run beside the next pipelined front instead of after it. */

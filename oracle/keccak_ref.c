@@ -60,9 +60,25 @@ void or_keccak_f1600(uint64_t A[25]) {
 }
 
 static inline uint64_t load_le64(const uint8_t* p) {
+#if defined(__BYTE_ORDER__) && __BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__
+    uint64_t v;
+    memcpy(&v, p, 8);
+#else
     uint64_t v = 0;
     for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+#endif
     return v;
+}
+
+/* The permutation every sponge below runs: the loop form above (default) or
+ * the unrolled x/crypto-shaped one (keccak_fast.c) for the CPU baselines.
+ * Process-wide; set it before starting a computation, not during one. */
+static void (*g_perm)(uint64_t A[25]) = or_keccak_f1600;
+
+int or_set_fast_permutation(int on) {
+    int was = g_perm == or_keccak_f1600_unrolled;
+    g_perm = on ? or_keccak_f1600_unrolled : or_keccak_f1600;
+    return was;
 }
 
 /* Sponge over a message with a selectable domain pad byte (0x01 legacy
@@ -74,7 +90,7 @@ void or_sponge(const uint8_t* in, uint64_t len, uint8_t pad, uint32_t rate,
     uint8_t block[200];
     while (len >= rate) {
         for (uint32_t i = 0; i < rate / 8; ++i) A[i] ^= load_le64(in + 8 * i);
-        or_keccak_f1600(A);
+        g_perm(A);
         in += rate;
         len -= rate;
     }
@@ -83,7 +99,7 @@ void or_sponge(const uint8_t* in, uint64_t len, uint8_t pad, uint32_t rate,
     block[len] ^= pad;
     block[rate - 1] ^= 0x80;
     for (uint32_t i = 0; i < rate / 8; ++i) A[i] ^= load_le64(block + 8 * i);
-    or_keccak_f1600(A);
+    g_perm(A);
     for (uint32_t i = 0; i < out_len; ++i) out[i] = (uint8_t)(A[i / 8] >> (8 * (i % 8)));
 }
 

@@ -4,6 +4,8 @@
 #include <stdint.h>
 
 void or_keccak_f1600(uint64_t A[25]);
+void or_keccak_f1600_unrolled(uint64_t A[25]);
+int or_set_fast_permutation(int on);
 void or_sponge(const uint8_t* in, uint64_t len, uint8_t pad, uint32_t rate, uint8_t* out,
                uint32_t out_len);
 void or_keccak256(const uint8_t* in, uint64_t len, uint8_t out[32]);

@@ -46,6 +46,10 @@ def lib():
         L = ctypes.CDLL(LIB_PATH)
         u8p = ctypes.c_void_p
         L.or_keccak256.argtypes = [u8p, ctypes.c_uint64, u8p]
+        L.or_keccak_f1600.argtypes = [u8p]
+        L.or_keccak_f1600_unrolled.argtypes = [u8p]
+        L.or_set_fast_permutation.argtypes = [ctypes.c_int]
+        L.or_set_fast_permutation.restype = ctypes.c_int
         L.or_sha3_256.argtypes = [u8p, ctypes.c_uint64, u8p]
         L.or_keccak256_batch.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, u8p, ctypes.c_int]
         L.or_keccak256_var.argtypes = [u8p, u8p, ctypes.c_uint64, u8p]
@@ -71,6 +75,27 @@ def lib():
             getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib
+
+
+def keccak_f(state: np.ndarray, unrolled: bool = False) -> np.ndarray:
+    """One Keccak-f[1600] of a (25,) uint64 state (a copy): the loop form or
+    the unrolled x/crypto-shaped form (keccak_fast.c)."""
+    a = np.ascontiguousarray(state, dtype=np.uint64).copy()
+    (lib().or_keccak_f1600_unrolled if unrolled else lib().or_keccak_f1600)(a.ctypes.data)
+    return a
+
+
+class fast_permutation:
+    """``with fast_permutation():`` every oracle sponge in this process runs
+    the unrolled permutation (the CPU baseline's); restored on exit."""
+
+    def __enter__(self):
+        self._was = lib().or_set_fast_permutation(1)
+        return self
+
+    def __exit__(self, *exc):
+        lib().or_set_fast_permutation(self._was)
+        return False
 
 
 def _buf(b: bytes):

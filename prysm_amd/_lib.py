@@ -90,7 +90,7 @@ _SIGS = {
     "mk_deposit_trie_build": (_int, [_cp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "mk_dev_deposit_trie_append": (_int, [_cp, _vp, _u64, _u64, _vp, _vp, _u64, _u32, _u32, _vp, _vp]),
     "mk_dev_deposit_trie_branch": (_int, [_cp, _vp, _u64, _u64, _u32, _u64, _vp, _vp]),
-    "mk_deposit_trie_pipe_ok": (_int, [_vp, _u64, _u32, _u32]),
+    "mk_deposit_trie_pipe_ok": (_int, [_vp, _u64, _u32, _u32, _vp]),
     "mk_dev_deposit_trie_build_pipe": (_int, [_cp, _vp, _vp, _u64, _vp, _u64, _u32, _u32, _vp]),
     "mk_dev_deposit_trie_pipe_top": (_int, [_cp, _vp, _u64, _u64, _u32, _vp, _vp]),
     "mk_dev_deposit_trie_levels": (_int, [_cp, _vp, _u64, _u64, _u32, _u32, _u32, _vp, _vp]),

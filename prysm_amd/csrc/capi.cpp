@@ -2140,8 +2140,12 @@ int mk_dev_deposit_trie_build(mk_call* call, void* d_levels, uint64_t capacity, 
                              d_to == depth ? d_root32 : nullptr, (hipStream_t)stream));
 }
 
-int mk_deposit_trie_pipe_ok(const void* d_data, uint64_t n, uint32_t deposit_len, uint32_t depth) {
-    return trie_pipe_ok(d_data, n, deposit_len, depth, nullptr) ? 1 : 0;
+int mk_deposit_trie_pipe_ok(const void* d_data, uint64_t n, uint32_t deposit_len, uint32_t depth, void* stream) {
+    // the same check mk_dev_deposit_trie_build_pipe makes, on the caller's
+    // stream (its CU mask bounds the persistent grid), on its device
+    Scope S(nullptr);
+    if (bind_stream((hipStream_t)stream)) return S.done(0);
+    return S.done(trie_pipe_ok(d_data, n, deposit_len, depth, (hipStream_t)stream) ? 1 : 0);
 }
 
 int mk_dev_deposit_trie_build_pipe(mk_call* call, void* d_levels, void* d_prev_levels, uint64_t capacity,

@@ -1145,9 +1145,13 @@ __device__ __forceinline__ void wave3_spread_levels(uint32_t* lds, uint64_t& c, 
 // block, and the second of the two finishers to arrive -- they run as
 // separate launches on two streams, neither waits for the other -- hashes
 // K(slot 0 || slot 1) into pair[64..96).  Arrival word pair[24] = epoch << 2 |
-// arrived-slot bits: a finisher of a newer epoch than the word's starts the
-// mask afresh, so a pair left half-done (a failed launch) cannot pair with the
-// next one.
+// arrived-slot bits (epochs are 30-bit and wrap; "newer" = ahead by less than
+// 2^29): a finisher of a newer epoch than the word's starts the mask afresh,
+// so a pair left half-done (a failed launch) cannot pair with the next one; a
+// finisher of an OLDER epoch (a late one) is ignored, so it cannot clear the
+// current pair's bits.  The first finisher of an epoch zeroes pair[64..96)
+// before it sets its bit, so a pair that never completes reads back as
+// zeros, never as the previous epoch's root.
 __device__ __forceinline__ void spread_store_digest(uint32_t e, uint32_t o, uint32_t L, uint32_t* out) {
     if (L < 4u) {
         out[2 * L] = ilv::spread16(e) | (ilv::spread16(o) << 1);
@@ -1179,7 +1183,13 @@ __device__ __forceinline__ void wave3_spread_final(const uint32_t* lds, uint64_t
         uint32_t* word = pair + 24;
         uint32_t old = atomicAdd(word, 0u);  // an atomic read of the arrival word
         for (;;) {
-            const uint32_t nw = ((old >> 2) == epoch ? old : epoch << 2) | (1u << slot);
+            const uint32_t ahead = (epoch - (old >> 2)) & 0x3FFFFFFFu;
+            if (ahead >= (1u << 29)) break;  // an older epoch than the word's: a late finisher, ignored
+            if (ahead != 0u || (old & 3u) == 0u) {  // first of this epoch (so far): clear the pair root
+                for (uint32_t w = 16; w < 24; ++w) pair[w] = 0u;
+                __threadfence();
+            }
+            const uint32_t nw = (ahead == 0u ? old : epoch << 2) | (1u << slot);
             const uint32_t seen = atomicCAS(word, old, nw);
             if (seen == old) {
                 second = (nw & 3u) == 3u;

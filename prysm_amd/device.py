@@ -360,7 +360,7 @@ def deposit_trie_build(levels: torch.Tensor, capacity: int, data: torch.Tensor, 
 
 def deposit_trie_pipe_ok(data: torch.Tensor, n: int, deposit_len: int, depth: int) -> bool:
     """Whether deposit_trie_build_pipe takes this stream shape."""
-    return bool(_lib.load().mk_deposit_trie_pipe_ok(_p(data), n, deposit_len, depth))
+    return bool(_lib.load().mk_deposit_trie_pipe_ok(_p(data), n, deposit_len, depth, _stream(data.device)))
 
 
 def deposit_trie_build_pipe(levels: torch.Tensor, prev_levels, capacity: int, data: torch.Tensor, n: int,

@@ -88,19 +88,7 @@ class TriePipeline:
     trieutil.DepositTrie semantics, deposit_trie.go:29-63) with each trie's
     narrow top off the critical path.
 
-    ``front="pipe"`` (the default where mk_deposit_trie_pipe_ok takes the
-    shape: 280-B deposits, n a multiple of 4096 up to 4096 x the CU count):
-    trie i's leaves and levels 1-2 run in one phase-locked launch that also
-    builds levels 3-7 of trie i-1 in its lock-step slots
-    (mk_dev_deposit_trie_build_pipe); trie i-1's remaining top (levels 8 ..
-    depth and the root) then runs on a high-priority side stream beside trie
-    i+1's front.  A trie's root is therefore written one submit later: the
-    tensor ``submit`` returns is produced once the next ``submit`` or
-    ``flush()`` has been called (then synchronise, or wait on ``side``).
-    Level arrays and roots rotate over four sets; a returned root stays
-    valid for the next two submits after it is produced.
-
-    ``front="split"`` (other shapes): per trie, on the caller's current
+    ``front="split"`` (the default): per trie, on the caller's current
     stream, the leaf hashes and the wide levels down to the first level of at
     most 2^17 nodes; on the side stream, overlapping the next trie's leaves,
     the latency-bound top (k_trie_top3 launches), the zero-sibling levels up
@@ -108,17 +96,35 @@ class TriePipeline:
     and a wait every 2-3 submits measured the same, profiles/r02r/
     ring_ab.jsonl); a submit waits for the top of the trie ``slots`` submits
     back; the returned root is written by the time the side stream has run
-    this submit's work, and stays valid for the next ``slots - 1`` submits."""
+    this submit's work, and stays valid for the next ``slots - 1`` submits.
+
+    ``front="pipe"`` (opt-in; the C5 bench's form): trie i's leaves and
+    levels 1-2 run in one phase-locked launch that also builds levels 3-7 of
+    trie i-1 in its lock-step slots (mk_dev_deposit_trie_build_pipe); trie
+    i-1's remaining top (levels 8 .. depth and the root) then runs on a
+    high-priority side stream beside trie i+1's front.  **A trie's root is
+    therefore written one submit later**: the tensor ``submit`` returns is
+    produced once the next ``submit`` or ``flush()`` has been called (then
+    synchronise, or wait on ``side``).  Level arrays and roots rotate over
+    four sets; a returned root stays valid for the next two submits after it
+    is produced.  Takes what mk_deposit_trie_pipe_ok accepts on the current
+    stream (280-B deposits, 16-B aligned, n a multiple of 4096 within the
+    stream's CUs); ValueError otherwise.  Submits may come from different
+    streams: each front waits for the previous one, whose levels it reads.
+
+    ``front="auto"``: "pipe" where the shape allows it, "split" otherwise
+    (so the root's timing depends on the shape: only for callers that always
+    flush() before reading roots)."""
 
     TOP_MAX = 1 << 17  # capi.cpp kTrieTopMax: levels at or below this width run k_trie_top3
     PIPE_TOP_FROM = 7  # the last level the pipelined front builds for the previous trie
 
     def __init__(self, n: int, deposit_len: int, depth: int, device, split: Optional[int] = None,
-                 slots: int = 2, wait_every: int = 1, front: str = "auto"):
+                 slots: int = 2, wait_every: int = 1, front: str = "split"):
         """``split``: the first level built on the side stream (default: the
         first level of at most TOP_MAX nodes); ``slots``, ``wait_every``:
-        parallel.SlotRing (split front); ``front``: "auto" (pipe where the
-        shape allows), "pipe" or "split"."""
+        parallel.SlotRing (split front); ``front``: "split" (default), "pipe"
+        or "auto" (pipe where the shape allows)."""
         if front not in ("auto", "pipe", "split"):
             raise ValueError(f"unknown front {front!r}")
         self.n, self.dl, self.depth = n, deposit_len, depth
@@ -141,6 +147,7 @@ class TriePipeline:
         self._i = 0
         self._pending = None  # pipe: the set of the trie whose levels 3.. are not built yet
         self._done = {}  # pipe: trie index -> event after its top
+        self._front_ev = None  # pipe: (stream, event) after the last front
 
     def _sets(self, k: int):
         return ([torch.empty(self._nbytes, dtype=torch.uint8, device=self.device) for _ in range(k)],
@@ -193,10 +200,15 @@ class TriePipeline:
                 cur.wait_event(ev)
         self._done.pop(i - nsets - 1, None)
         prev = self._pending
+        if prev is not None and self._front_ev is not None and self._front_ev[0] != cur:
+            cur.wait_event(self._front_ev[1])  # the previous front (levels 0-2 read here) ran elsewhere
         D.deposit_trie_build_pipe(self.levels[s], None if prev is None else self.levels[prev], self.n, deposits,
                                   self.n, self.dl, self.depth)
         if prev is not None:
             self._top(i - 1, prev, self.PIPE_TOP_FROM, cur)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._front_ev = (cur, ev)
         self._pending = s
         return self.roots[s]
 
@@ -215,5 +227,8 @@ class TriePipeline:
         """Finish the last pipelined trie (its levels 3 .. depth and root on
         the side stream); a no-op when nothing is pending."""
         if self._pending is not None:
-            self._top(self._i - 1, self._pending, 2, torch.cuda.current_stream(self.device))
+            cur = torch.cuda.current_stream(self.device)
+            if self._front_ev is not None and self._front_ev[0] != cur:
+                cur.wait_event(self._front_ev[1])
+            self._top(self._i - 1, self._pending, 2, cur)
             self._pending = None

@@ -175,6 +175,7 @@ class DeviceStateHasher:
         self.bal_ws = D.merkle_workspace(n, 8, device)
         self.pair = torch.empty(64, dtype=torch.uint8, device=device)  # reg_root || bal_root
         # the state root ("level1": the pair finisher writes it into the pair block)
+        # (every schedule writes its root here, so a fallback returns the same tensor)
         self.out = self.pair_block[64:96] if lv1 else torch.empty(32, dtype=torch.uint8, device=device)
         self.side = torch.cuda.Stream(device=device, priority=-1)  # its own hardware queue
         self.ev_roots = torch.cuda.Event()
@@ -192,6 +193,16 @@ class DeviceStateHasher:
         sched = self.schedule
         if sched != "two" and not D.struct_list_level1_ok(records, n, 160, VALIDATOR_FIELDS):
             sched = "two"
+        # the level-1 front also takes the balances' windows: 16-B aligned, more
+        # than one chunk (mk_dev_ssz_struct_list_level1); otherwise the one-call
+        # list root with the balances tree beside it
+        if sched == "level1" and (balances.data_ptr() % 16 or n * 8 <= 128):
+            sched = "list"
+            if self.list_ws is None:
+                L = _lib.load()
+                self.list_ws = torch.empty(
+                    L.mk_ssz_struct_list_workspace_bytes(n, _fields(VALIDATOR_FIELDS), len(VALIDATOR_FIELDS)) + 256,
+                    dtype=torch.uint8, device=self.dev)
         if sched == "level1":
             # one launch: struct roots + the level-1 windows of BOTH trees (the
             # balances' on the lanes the registry's windows leave free)

@@ -7,7 +7,8 @@ restatement_vectors.json; the oracle is pinned by reference_vectors.json).
   c1: TreeHash([]*ValidatorRecord) of 16,384 synthetic validators (C struct
       roots + merkleHash, cross-checked against the reflective ssz_ref walk)
   c2: hashutil.Hash of 2^24 x 64-B SplitMix64 messages -> Keccak-256 of the
-      concatenated 2^24 digests (a checksum of checksums)
+      concatenated 2^24 digests and merkleHash of the digests as 32-B items
+      (checksums of checksums)
   c3: TreeHash of State{1,000,000 synthetic validators, balances}
   c4: merkleHash of 2^28 x 32-B SplitMix64 items (the headline tree)
   c4tree: TreeHash([][32]byte) of 2^28 SplitMix64 elements (the C4 secondary:
@@ -104,7 +105,10 @@ def main(only=None):
         n = 1 << 24
         msgs = O.splitmix_bytes(n * 64, SEED + 2)
         dig = O.keccak256_batch(msgs, 64, nthreads=nt)
-        out["c2"] = {"n": n, "msg_len": 64, "seed": SEED + 2, "digest_of_digests": O.keccak256(dig.tobytes()).hex()}
+        # two checksums of the 2^24 digests: Keccak of their concatenation, and
+        # merkleHash of them as 32-B items (what bench.py checks on the device)
+        out["c2"] = {"n": n, "msg_len": 64, "seed": SEED + 2, "digest_of_digests": O.keccak256(dig.tobytes()).hex(),
+                     "merkle_of_digests": O.merkle_hash_flat(dig.reshape(-1), n, 32, nthreads=nt).hex()}
         del msgs, dig
 
     if want("c3"):

@@ -309,7 +309,7 @@ def test_trie_pipeline_pipelined_front(gpu, n):
     from prysm_amd.pipeline import TriePipeline
 
     ln, depth = 280, 32
-    pipe = TriePipeline(n, ln, depth, gpu)
+    pipe = TriePipeline(n, ln, depth, gpu, front="pipe")
     datas = []
     for t in range(4):
         d = torch.empty(n * ln, dtype=torch.uint8, device=gpu)
@@ -361,7 +361,7 @@ def test_trie_pipeline_mixed_fronts_and_flush(gpu):
     from prysm_amd.pipeline import TriePipeline
 
     n, ln, depth = 4096, 280, 32
-    pipe = TriePipeline(n, ln, depth, gpu)
+    pipe = TriePipeline(n, ln, depth, gpu, front="auto")
     store = torch.empty(n * ln + 16, dtype=torch.uint8, device=gpu)
     plan = ["pipe", "pipe", "split", "pipe", "flush", "pipe", "split", "split", "pipe", "pipe"]
     handles, wants = [], []
@@ -385,3 +385,59 @@ def test_trie_pipeline_mixed_fronts_and_flush(gpu):
     pipe.flush()
     torch.cuda.synchronize()
     assert bytes(handles[-1].cpu().numpy()) == wants[-1]
+
+
+def test_trie_pipeline_default_root_ready_after_submit(gpu):
+    """The default front is "split" at every shape, including the shapes the
+    pipelined front takes (whole 4096-deposit groups): a root read after
+    submit + synchronize is that trie's root (the pipelined form's deferred
+    root is opt-in)."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+    from prysm_amd.pipeline import TriePipeline
+
+    n, ln, depth = 8192, 280, 32
+    pipe = TriePipeline(n, ln, depth, gpu)
+    d = torch.empty(n * ln, dtype=torch.uint8, device=gpu)
+    for t in range(3):
+        D.synth_fill(d, SEED + 990 + t)
+        assert D.deposit_trie_pipe_ok(d, n, ln, depth)
+        r = pipe.submit(d)
+        torch.cuda.synchronize()
+        host = d.cpu().numpy()
+        assert bytes(r.cpu().numpy()) == O.deposit_trie_levels([bytes(host[i * ln:(i + 1) * ln])
+                                                                 for i in range(n)])[0], t
+    assert not pipe._last_pipe
+
+
+def test_trie_pipeline_pipe_submits_from_two_streams(gpu):
+    """Pipelined fronts submitted alternately from two streams (each front
+    reads the previous trie's levels 0-2, which the other stream wrote): the
+    pipeline orders them, every root equals the oracle's."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+    from prysm_amd.pipeline import TriePipeline
+
+    n, ln, depth = 2 * 4096, 280, 32
+    pipe = TriePipeline(n, ln, depth, gpu, front="pipe")
+    streams = [torch.cuda.Stream(device=gpu), torch.cuda.Stream(device=gpu)]
+    datas, handles = [], []
+    for t in range(5):
+        d = torch.empty(n * ln, dtype=torch.uint8, device=gpu)
+        D.synth_fill(d, SEED + 995 + t)
+        datas.append(d)
+    torch.cuda.synchronize()
+    for t, d in enumerate(datas):
+        with torch.cuda.stream(streams[t % 2]):
+            handles.append(pipe.submit(d))
+    with torch.cuda.stream(streams[1]):
+        pipe.flush()
+    torch.cuda.synchronize()
+    for t, d in enumerate(datas):
+        host = d.cpu().numpy()
+        want = O.deposit_trie_levels([bytes(host[i * ln:(i + 1) * ln]) for i in range(n)])[0]
+        assert bytes(handles[t].cpu().numpy()) == want, t

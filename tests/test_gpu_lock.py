@@ -250,6 +250,30 @@ def test_state_hasher_schedules_agree(gpu):
         assert bytes(out.cpu().numpy()) == want, sched
 
 
+def test_state_hasher_misaligned_balances_fall_back(gpu):
+    """"level1" needs the balances 16-B aligned (mk_dev_ssz_struct_list_level1);
+    an 8-B-offset view falls back to the one-call list schedule (same root
+    tensor) instead of raising MK_EINVAL, and aligned balances take level1
+    again on the next submit."""
+    import torch
+
+    from prysm_amd import registry as R
+
+    n = (1 << 18) + 3
+    reg = R.synthetic_registry(n, SEED + 49)
+    bal = R.synthetic_balances(n, SEED + 49)
+    want = R.state_root(reg, bal)
+    rec = torch.from_numpy(reg.records.view(np.uint8).reshape(-1).copy()).to(gpu)
+    store = torch.empty(n * 8 + 16, dtype=torch.uint8, device=gpu)
+    h = R.DeviceStateHasher(n, gpu)
+    for off in (8, 0, 8):
+        store[off:off + n * 8].copy_(torch.from_numpy(bal.view(np.uint8).copy()))
+        out = h.submit(rec, store[off:off + n * 8])
+        torch.cuda.synchronize()
+        assert out.data_ptr() == h.out.data_ptr()
+        assert bytes(out.cpu().numpy()) == want, off
+
+
 
 def _finish_ref(nodes: bytes, n_total: int) -> bytes:
     """merkleHash's level loop over 32-B nodes and its length mix-in
@@ -267,8 +291,11 @@ def _finish_ref(nodes: bytes, n_total: int) -> bytes:
 def test_pair_finisher_many_pairs_random_order(gpu):
     """60 pairs through one pair block, the two finishers launched in a
     random order on two streams each time (sometimes slot 0 first, sometimes
-    slot 1, sometimes concurrently), a new epoch per pair and one pair in five
-    left half-done first (a failed call's leftover): every struct root equals
+    slot 1, sometimes concurrently), a new epoch per pair; one pair in five
+    is preceded by a half-done pair of the epoch before it (a failed call's
+    leftover: the block's root reads back as zeros, not the previous pair's),
+    and one in seven is followed by a late finisher of an older epoch (it is
+    ignored: the arrival word and the root stay).  Every struct root equals
     Keccak(root0 || root1) of that pair's inputs."""
     import random
 
@@ -281,28 +308,55 @@ def test_pair_finisher_many_pairs_random_order(gpu):
     side = torch.cuda.Stream(device=gpu)
     pb = torch.zeros(128, dtype=torch.uint8, device=gpu)
     for e in range(1, 61):
+        ep = 2 * e
         c0, c1 = rng.choice([1, 7, 100, 3000]), rng.choice([1, 64, 65, 2048])
         a = torch.from_numpy(O.splitmix_bytes(32 * c0, 9000 + e).copy()).to(gpu)
         b = torch.from_numpy(O.splitmix_bytes(32 * c1, 9500 + e).copy()).to(gpu)
         want0 = _finish_ref(bytes(a.cpu().numpy()), c0)
         want1 = _finish_ref(bytes(b.cpu().numpy()), c1)
-        if e % 5 == 0:  # a stale half of an earlier epoch
-            D.merkle_finish_nodes_pair(a, c0, c0, pb, rng.randrange(2), 10_000 + e)
+        if e % 5 == 0:  # a stale half of the epoch before this pair's
+            D.merkle_finish_nodes_pair(a, c0, c0, pb, rng.randrange(2), ep - 1)
+            torch.cuda.synchronize()
+            assert bytes(pb[64:96].cpu().numpy()) == bytes(32), e  # never a plausible old root
         order = rng.randrange(3)
         ev = torch.cuda.Event()
         ev.record()
         side.wait_event(ev)
         if order == 0:
-            D.merkle_finish_nodes_pair(a, c0, c0, pb, 0, e)
-            D.merkle_finish_nodes_pair(b, c1, c1, pb, 1, e)
+            D.merkle_finish_nodes_pair(a, c0, c0, pb, 0, ep)
+            D.merkle_finish_nodes_pair(b, c1, c1, pb, 1, ep)
         elif order == 1:
-            D.merkle_finish_nodes_pair(b, c1, c1, pb, 1, e)
-            D.merkle_finish_nodes_pair(a, c0, c0, pb, 0, e)
+            D.merkle_finish_nodes_pair(b, c1, c1, pb, 1, ep)
+            D.merkle_finish_nodes_pair(a, c0, c0, pb, 0, ep)
         else:
             with torch.cuda.stream(side):
-                D.merkle_finish_nodes_pair(b, c1, c1, pb, 1, e)
-            D.merkle_finish_nodes_pair(a, c0, c0, pb, 0, e)
+                D.merkle_finish_nodes_pair(b, c1, c1, pb, 1, ep)
+            D.merkle_finish_nodes_pair(a, c0, c0, pb, 0, ep)
         torch.cuda.synchronize()
+        if e % 7 == 0:  # a late finisher of an older epoch: ignored
+            D.merkle_finish_nodes_pair(b, c1, c1, pb, rng.randrange(2), ep - 3)
+            torch.cuda.synchronize()
         got = bytes(pb.cpu().numpy())
         assert got[:32] == want0 and got[32:64] == want1, e
         assert got[64:96] == O.keccak256(want0 + want1), (e, order)
+        assert int.from_bytes(got[96:100], "little") == (ep << 2) | 3, e
+
+
+def test_pair_finisher_epoch_wraps(gpu):
+    """Epochs are 30-bit counters: after 2^30 - 1 comes 1, which is newer
+    (the state hasher's epoch % (2^30 - 1) + 1); the pair still completes."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+
+    pb = torch.zeros(128, dtype=torch.uint8, device=gpu)
+    a = torch.from_numpy(O.splitmix_bytes(32 * 5, 31).copy()).to(gpu)
+    b = torch.from_numpy(O.splitmix_bytes(32 * 9, 32).copy()).to(gpu)
+    want = O.keccak256(_finish_ref(bytes(a.cpu().numpy()), 5) + _finish_ref(bytes(b.cpu().numpy()), 9))
+    for ep in ((1 << 30) - 1, 1, 2):
+        D.merkle_finish_nodes_pair(a, 5, 5, pb, 0, ep)
+        D.merkle_finish_nodes_pair(b, 9, 9, pb, 1, ep)
+        torch.cuda.synchronize()
+        assert bytes(pb[64:96].cpu().numpy()) == want, ep
+        assert int.from_bytes(bytes(pb[96:100].cpu().numpy()), "little") == (ep << 2) | 3, ep

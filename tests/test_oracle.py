@@ -7,6 +7,7 @@ the example structs; the deposit-trie batch build against a literal
 dict-based restatement of UpdateDepositTrie (deposit_trie.go:29-40).
 """
 import hashlib
+import json
 import os
 import struct
 
@@ -29,6 +30,29 @@ def test_permutation_vs_fips_sha3(n):
     assert O.sha3_256(msg) == hashlib.sha3_256(msg).digest()
     assert O.py_keccak256(msg, pad=0x06) == hashlib.sha3_256(msg).digest()
     assert O.py_keccak256(msg) == O.keccak256(msg)
+
+
+def test_unrolled_permutation_equals_loop_form():
+    """The CPU baseline's permutation (keccak_fast.c, the x/crypto shape)
+    is the same function as the restatement's loop form: random states,
+    every sponge through it (KATs, FIPS SHA3-256) and a merkleHash."""
+    rng = np.random.default_rng(5)
+    for _ in range(256):
+        s = rng.integers(0, 2**63, 25, dtype=np.uint64) * np.uint64(3)
+        assert np.array_equal(O.keccak_f(s), O.keccak_f(s, unrolled=True))
+    items = O.splitmix_bytes(1000 * 32, 11)
+    want = O.merkle_hash_flat(items, 1000, 32)
+    kats = [(bytes.fromhex(k["in"]), k["out"]) for k in
+            json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                        "reference_vectors.json")))["keccak256_kats"]]
+    with O.fast_permutation():
+        for n in (0, 1, 135, 136, 137, 500):
+            msg = bytes(rng.integers(0, 256, n, dtype=np.uint8))
+            assert O.sha3_256(msg) == hashlib.sha3_256(msg).digest()
+        for m, out in kats:
+            assert O.keccak256(m).hex() == out
+        assert O.merkle_hash_flat(items, 1000, 32) == want
+    assert O.lib().or_set_fast_permutation(0) == 0  # restored on exit
 
 
 def _pyval(t, v):

@@ -28,7 +28,7 @@ else:
     n = 1 << 20
     data = torch.empty(n * 280, dtype=torch.uint8, device=dev)
     D.synth_fill(data, 0x5EED000000000005)
-    pipe = TriePipeline(n, 280, 32, dev)
+    pipe = TriePipeline(n, 280, 32, dev, front="pipe")
     step = lambda: pipe.submit(data)  # noqa: E731
 step()
 torch.cuda.synchronize()
