@@ -863,9 +863,11 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
     }
     if (kStructReg && layout && nb == 3 && nraw == 6) {
         if (MK_STRUCT_LOCK && vec16 && validator_layout(sp) && n >= (1u << 18))  // phase-locked, partial last group
-            hipLaunchKernelGGL(mk::k_struct_lock, dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), lock_grid_cap(st))),
+            hipLaunchKernelGGL(mk::k_struct_lock<false>,
+                               dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), lock_grid_cap(st))),
                                dim3(mk::kLockThreads), 0, st, (const uint8_t*)d_rec, n, (uint4*)d_roots, 0u,
-                               (uint4*)nullptr, (const uint8_t*)nullptr, (uint64_t)0, (uint4*)nullptr);
+                               (uint4*)nullptr, (const uint8_t*)nullptr, (uint64_t)0, (uint4*)nullptr,
+                               mk::StructPrev{});
         else
             hipLaunchKernelGGL((mk::k_struct_reg<3, 6>), dim3(ceil_div(n, mk::kStructThreads)),
                                dim3(mk::kStructThreads), 0, st, (const uint8_t*)d_rec, n, sp, vec16 ? 1u : 0u,
@@ -938,15 +940,23 @@ bool struct_win_ok(const void* d_rec, uint64_t n, const mk::StructSpec& sp) {
 
 // d_vals (nullable): a second list of vbytes bytes whose level-1 windows the
 // kernel hashes on its leftover lanes (item length dividing 128, 16-B aligned)
+uint32_t struct_gpw(uint64_t n, hipStream_t st) {  // contiguous groups per workgroup
+    return (uint32_t)ceil_div(ceil_div(n, mk::kLockThreads), lock_grid_cap(st));
+}
 int dev_struct_level1(const void* d_rec, uint64_t n, void* d_roots, void* d_wins, hipStream_t st,
-                      const void* d_vals = nullptr, uint64_t vbytes = 0, void* d_vwins = nullptr) {
+                      const void* d_vals = nullptr, uint64_t vbytes = 0, void* d_vwins = nullptr,
+                      const mk::StructPrev* prev = nullptr) {
     if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
     const uint64_t ngroups = ceil_div(n, mk::kLockThreads);
-    const uint64_t cap = lock_grid_cap(st);
-    const uint32_t gpw = (uint32_t)ceil_div(ngroups, cap);  // contiguous groups per workgroup
-    hipLaunchKernelGGL(mk::k_struct_lock, dim3(ceil_div(ngroups, gpw)), dim3(mk::kLockThreads), 0, st,
-                       (const uint8_t*)d_rec, n, (uint4*)d_roots, gpw, (uint4*)d_wins,
-                       (const uint8_t*)(vbytes ? d_vals : nullptr), vbytes, (uint4*)d_vwins);
+    const uint32_t gpw = struct_gpw(n, st);
+    if (prev)
+        hipLaunchKernelGGL(mk::k_struct_lock<true>, dim3(ceil_div(ngroups, gpw)), dim3(mk::kLockThreads), 0, st,
+                           (const uint8_t*)d_rec, n, (uint4*)d_roots, gpw, (uint4*)d_wins,
+                           (const uint8_t*)(vbytes ? d_vals : nullptr), vbytes, (uint4*)d_vwins, *prev);
+    else
+        hipLaunchKernelGGL(mk::k_struct_lock<false>, dim3(ceil_div(ngroups, gpw)), dim3(mk::kLockThreads), 0, st,
+                           (const uint8_t*)d_rec, n, (uint4*)d_roots, gpw, (uint4*)d_wins,
+                           (const uint8_t*)(vbytes ? d_vals : nullptr), vbytes, (uint4*)d_vwins, mk::StructPrev{});
     HIPCHK(hipGetLastError());
     return MK_OK;
 }
@@ -1971,6 +1981,104 @@ int mk_dev_ssz_struct_list_level1(mk_call* call, const void* d_records, uint64_t
     }
     return S.done(dev_struct_level1(d_records, n, d_roots, d_nodes, (hipStream_t)stream, d_values,
                                     nvalues * (uint64_t)value_len, d_value_nodes));
+}
+
+// ---- a stream of states (registry.StatePipeline) ----------------------------
+// The registry tree's level-1 nodes of workgroup b of the pipelined launch,
+// [512 b, 512 b + 512), form a complete subtree whose levels 2..10 the NEXT
+// launch builds (k_struct_lock<true>); d_levels holds level k (2..10) of
+// subtree b at node offset 511 nfull - (1024 >> (k - 2)) nfull + (512 >>
+// (k - 1)) b, i.e. the levels back to back, level 10 last with room for the
+// ragged last subtree's node after the nfull complete ones.
+constexpr uint64_t kPipeSub = 512;  // level-1 nodes per workgroup (4 groups x 1024 records / 8)
+uint64_t pipe_nfull(uint64_t n) { return ceil_div(n, 8) / kPipeSub; }
+uint64_t pipe_level_off(uint64_t nfull, uint32_t k) {  // nodes before level k
+    uint64_t off = 0;
+    for (uint32_t j = 2; j < k; ++j) off += (kPipeSub >> (j - 1)) * nfull;
+    return off;
+}
+bool struct_pipe_ok(const void* d_rec, uint64_t n, const mk::StructSpec& sp, hipStream_t st) {
+    return struct_win_ok(d_rec, n, sp) && struct_gpw(n, st) == 4 && pipe_nfull(n) >= 1;
+}
+
+int mk_ssz_struct_pipe_ok(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
+                          uint32_t nfields, void* stream) {
+    Scope S(nullptr);
+    mk::StructSpec sp;
+    if (make_spec(fields, nfields, record_len, sp) != MK_OK || bind_stream((hipStream_t)stream)) return S.done(0);
+    return S.done(struct_pipe_ok(d_records, n, sp, (hipStream_t)stream) ? 1 : 0);
+}
+
+uint64_t mk_ssz_struct_pipe_levels_bytes(uint64_t n) {
+    return 32 * (pipe_level_off(pipe_nfull(n), 11) + 1);
+}
+
+uint64_t mk_ssz_struct_pipe_top_workspace_bytes(uint64_t n) {
+    Scope S(nullptr, false);
+    const uint64_t nfull = pipe_nfull(n), rag = ceil_div(n, 8) - kPipeSub * nfull;
+    uint64_t ws = std::max<uint64_t>(256, finish_ws_bytes(nfull + 1));
+    Plan p;
+    if (rag && mk::make_plan(rag, 32, true, 9, true, true, p, true, 0) == MK_OK)
+        ws = std::max<uint64_t>(ws, mk::plan_ws_bytes(p));
+    return ws;
+}
+
+int mk_dev_ssz_struct_list_level1_pipe(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
+                                       const mk_field* fields, uint32_t nfields, void* d_roots, void* d_nodes,
+                                       const void* d_values, uint64_t nvalues, uint32_t value_len,
+                                       void* d_value_nodes, const void* d_prev_nodes, void* d_prev_levels,
+                                       void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    mk::StructSpec sp;
+    rc = make_spec(fields, nfields, record_len, sp);
+    if (rc) return S.done(rc);
+    if (!d_records || !d_roots || !d_nodes || (d_prev_nodes && !d_prev_levels))
+        return S.done(fail(MK_EINVAL, "null pointer"));
+    if (!struct_pipe_ok(d_records, n, sp, (hipStream_t)stream))
+        return S.done(fail(MK_EINVAL, "pipelined struct launch needs ValidatorRecords at a 16-B aligned address, "
+                                      "4 groups of 1024 per workgroup (n = %llu)", (unsigned long long)n));
+    if (d_prev_nodes == d_nodes) return S.done(fail(MK_EINVAL, "the previous state's nodes alias this state's"));
+    if (nvalues) {
+        if (!d_values || !d_value_nodes) return S.done(fail(MK_EINVAL, "null pointer"));
+        if (value_len % 8 || value_len == 0 || 128 % value_len || ((uintptr_t)d_values % 16))
+            return S.done(fail(MK_EINVAL, "second list: items of 8, 16, 32, 64 or 128 B at a 16-B aligned address"));
+        if (nvalues * value_len <= 128)
+            return S.done(fail(MK_EINVAL, "second list of one chunk has no level-1 window"));
+    }
+    mk::StructPrev prev{};
+    prev.nfull = (uint32_t)pipe_nfull(n);
+    prev.live = d_prev_nodes ? 1u : 0u;
+    prev.l1 = (const uint4*)d_prev_nodes;
+    for (uint32_t k = 2; k <= 10; ++k)
+        prev.lv[k - 2] = d_prev_levels ? (uint4*)d_prev_levels + 2 * pipe_level_off(prev.nfull, k) : nullptr;
+    return S.done(dev_struct_level1(d_records, n, d_roots, d_nodes, (hipStream_t)stream, d_values,
+                                    nvalues * (uint64_t)value_len, d_value_nodes, &prev));
+}
+
+int mk_dev_ssz_struct_pipe_top(mk_call* call, const void* d_nodes, uint64_t n, void* d_levels, void* d_pair_block,
+                               uint32_t slot, uint32_t epoch, void* d_ws, uint64_t ws_bytes, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    if (!d_nodes || !d_levels || !d_pair_block) return S.done(fail(MK_EINVAL, "null pointer"));
+    if (slot > 1) return S.done(fail(MK_EINVAL, "pair slot %u out of range (0..1)", slot));
+    if (epoch == 0 || epoch >= (1u << 30)) return S.done(fail(MK_EINVAL, "pair epoch %u out of range (1..2^30-1)", epoch));
+    if ((uintptr_t)d_pair_block % 16) return S.done(fail(MK_EINVAL, "pair block not 16-B aligned"));
+    const uint64_t nfull = pipe_nfull(n), c1 = ceil_div(n, 8), rag = c1 - kPipeSub * nfull;
+    if (nfull == 0) return S.done(fail(MK_EINVAL, "no complete subtree (n = %llu)", (unsigned long long)n));
+    uint8_t* top = (uint8_t*)d_levels + 32 * pipe_level_off(nfull, 10);  // level 10: nfull (+1) nodes
+    if (rag) {  // the ragged last subtree from level 1 to level 10, the odd rule at every level (pad_at_one)
+        Plan p;
+        rc = mk::make_plan(rag, 32, true, 9, true, ((uintptr_t)d_nodes % 16) == 0, p, true, 0);
+        if (rc) return S.done(rc);
+        rc = launch_plan(p, (const uint8_t*)d_nodes + 32 * kPipeSub * nfull, top + 32 * nfull, (uint8_t*)d_ws,
+                         ws_bytes, (hipStream_t)stream);
+        if (rc) return S.done(rc);
+    }
+    return S.done(dev_finish_nodes(top, nfull + (rag ? 1 : 0), n, nullptr, d_ws, ws_bytes, (hipStream_t)stream,
+                                   d_pair_block, slot, epoch));
 }
 
 int mk_dev_ssz_struct_roots(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,

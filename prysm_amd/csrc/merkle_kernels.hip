@@ -1868,15 +1868,68 @@ __device__ constexpr uint32_t kValLen[9] = {48, 32, 32, 8, 8, 8, 8, 8, 8};
 // 0..(gpw*2 - 1), free-running (the other waves have left), into `wins`.  That
 // replaces the merkleHash leaf pass, a latency-bound pass over the whole
 // roots array.
+//
+// PREV (gpw == 4, a stream of states, registry.StatePipeline): the launch
+// also builds levels 2..10 of the PREVIOUS state's registry tree from that
+// state's level-1 windows (its own launch wrote them): workgroup b < nfull
+// takes the subtree over windows [512 b, 512 b + 512) -- 256 + 128 + ... + 1
+// node permutations -- and writes its level-10 node, so what is left of that
+// tree is a 245-node top.  Each wave does ONE of them as an extra lock-step
+// permutation (level 2 on waves 0-3, 3 on 4-5, then levels 4..10 on waves
+// 6..12, one node per lane; waves 13-15 a discarded one), so every wave runs
+// 21 permutations and the same barriers.  Level k sits before the field
+// permutation at position 2 (k - 2) of the 16 (4 groups x f0, f1, f2, s1);
+// level 10 at position 15 (before the last struct message): the writer
+// waits for its store in the middle of the field permutation that follows,
+// so the reader of the next level, a position or two on, loads after the
+// barriers of that wait (through L2: this CU never read those lines, and its
+// L1 was invalidated at dispatch).
+template <bool PREV>
 __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* __restrict__ rec, uint64_t n,
                                                                  uint4* __restrict__ roots, uint32_t gpw,
                                                                  uint4* __restrict__ wins,
                                                                  const uint8_t* __restrict__ vals, uint64_t vbytes,
-                                                                 uint4* __restrict__ vwins) {
+                                                                 uint4* __restrict__ vwins, StructPrev prev) {
     constexpr uint32_t kRecLen = 160, kRw = kRecLen / 4, kNinstr = kRecLen / 16;
     __shared__ uint32_t buf[kLockThreads / 64][64 * kRw];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t* Bw = buf[wave];
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
+    // the previous state's level this wave builds (2..10; 11 = a discarded
+    // permutation on waves 13-15) and its slot position
+    const uint32_t my_level = wv < 4 ? 2u : wv < 6 ? 3u : wv < 13 ? wv - 2u : 11u;
+    auto prev_slot = [&](uint32_t k) {
+        const uint32_t w0 = k == 2 ? 0u : k == 3 ? 4u : k + 2u;  // first wave of level k
+        const uint32_t per = k <= 10 ? 512u >> (k - 1) : 0u;     // level-k nodes per subtree
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));  // computed here, not hoisted and kept live across the loop
+        const uint32_t j = 64u * (wv - w0) + ln;
+        const bool act = prev.live && blockIdx.x < prev.nfull && j < per;
+        const uint4* src = k == 2 ? prev.l1 + 2 * (512u * blockIdx.x) : prev.lv[k <= 10 ? k - 3 : 0] + 4 * (per * blockIdx.x);
+        asm volatile("" ::: "memory");
+        State s;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = act ? src[4 * j + q] : make_uint4(0, 0, 0, 0);
+            s.lo[2 * q] = v.x;
+            s.hi[2 * q] = v.y;
+            s.lo[2 * q + 1] = v.z;
+            s.hi[2 * q + 1] = v.w;
+        }
+#pragma unroll
+        for (int w = 8; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
+        s.lo[8] = 1u;  // byte 64
+        s.hi[16] = 0x80000000u;
+        keccak_f_digest_lock(s);
+        if (act) {
+            uint4 d0, d1;
+            digest(s, d0, d1);
+            uint4* dst = prev.lv[k - 2] + 2 * (per * blockIdx.x + j);
+            dst[0] = d0;
+            dst[1] = d1;
+        }
+        asm volatile("" ::: "memory");
+    };
     // the last group may be partial: its lanes past n copy the last record
     // (every wave still runs the same permutations and barriers) and store nothing
     const uint64_t ngroups = (n + kLockThreads - 1) / kLockThreads;
@@ -1900,6 +1953,9 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;  // the previous group's root, stored after the next wait
     uint64_t qi = 0;
     bool pend = false;
+    // the previous state's slots run in workgroups of exactly gpw == 4 groups
+    // (uniform over the workgroup: all its waves run the same permutations)
+    const bool slots = PREV && gpw == 4 && g_end - g_begin == 4;
 #pragma unroll 1
     for (; g < g_end; g += g_step) {
         uint32_t* R = Bw + lane * kRw;
@@ -1908,8 +1964,12 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
             roots[2 * qi] = q0;
             roots[2 * qi + 1] = q1;
         }
+        const uint32_t pos0 = 4u * (uint32_t)(g - g_begin);  // slot position of field 0 of this group
 #pragma unroll
         for (int f = 0; f < 3; ++f) {  // Keccak(le32(len) || bytes), one block
+            // this wave's slot of the previous state's tree (f = 0, 2 only: positions 2 (k - 2))
+            const bool slot_here = slots && (f == 0 || f == 2) && my_level <= 10 && 2u * (my_level - 2u) == pos0 + f;
+            if (slot_here) prev_slot(my_level);
             const uint32_t len = kValLen[f], off = kValOff[f] / 4, nd = len / 4 + 1;
             State s;
 #pragma unroll
@@ -1924,11 +1984,23 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
 #pragma unroll
             for (int k = 9; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
             s.hi[16] = 0x80000000u;
-            keccak_f_digest_lock(s);
+            if constexpr (PREV) {
+                // the slot's node store completes mid-permutation, before the
+                // next level's reader (two positions on) can pass a barrier
+                keccak_f_digest_lock<12>(s, [&] {
+                    if (slot_here) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                });
+            } else {
+                keccak_f_digest_lock(s);
+            }
             // the digest replaces the field's own bytes (absorbed above)
             R[off + 0] = s.lo[0]; R[off + 1] = s.hi[0]; R[off + 2] = s.lo[1]; R[off + 3] = s.hi[1];
             R[off + 4] = s.lo[2]; R[off + 5] = s.hi[2]; R[off + 6] = s.lo[3]; R[off + 7] = s.hi[3];
         }
+        // level 10 (wave 12; waves 13-15 discard theirs) before the last
+        // group's struct message: it reads level 9, whose writer waited in the
+        // field-2 permutation just before; nothing in this launch reads it
+        if (slots && my_level >= 10 && pos0 == 12u) prev_slot(my_level);
         // struct message (hash.go:141-159): the digests of fields 0..2, then
         // the six uint64 raw: 36 dwords = block 1 (34) + 2 dwords of block 2
         State s;
@@ -1987,6 +2059,10 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     }
 }
 
+template __global__ void k_struct_lock<false>(const uint8_t*, uint64_t, uint4*, uint32_t, uint4*, const uint8_t*,
+                                              uint64_t, uint4*, StructPrev);
+template __global__ void k_struct_lock<true>(const uint8_t*, uint64_t, uint4*, uint32_t, uint4*, const uint8_t*,
+                                             uint64_t, uint4*, StructPrev);
 template __global__ void k_struct_reg<2, 0>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
 
 // The same layouts for SMALL registries (the 16,384-validator C1 shape),

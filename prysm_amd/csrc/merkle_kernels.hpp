@@ -54,8 +54,19 @@ __global__ void k_struct_reg(const uint8_t* rec, uint64_t n, StructSpec sp, uint
 // validator layout (kValOff/kValLen in merkle_kernels.hip), any n (a partial last group);
 // gpw > 0: contiguous groups per workgroup plus the level-1 windows of the roots' merkleHash
 // (and of a second list of vbytes bytes at vals, when vals != nullptr)
+// PREV (a stream of states, gpw == 4): the same launch also builds levels
+// 2..10 of the PREVIOUS state's registry tree over its level-1 windows, one
+// extra lock-step permutation per wave (see the kernel); workgroups b <
+// nfull each take the complete 512-window subtree [512 b, 512 b + 512).
+struct StructPrev {
+    const uint4* l1;   // the previous state's level-1 windows (complete)
+    uint4* lv[9];      // its levels 2..10: level k node j of subtree b at lv[k - 2][(512 >> (k - 1)) b + j]
+    uint32_t nfull;    // subtrees (workgroups) with all 512 windows
+    uint32_t live;     // 0: no previous state (the slots hash zeros, store nothing)
+};
+template <bool PREV>
 __global__ void k_struct_lock(const uint8_t* rec, uint64_t n, uint4* roots, uint32_t gpw, uint4* wins,
-                              const uint8_t* vals, uint64_t vbytes, uint4* vwins);
+                              const uint8_t* vals, uint64_t vbytes, uint4* vwins, StructPrev prev);
 #ifndef MK_STRUCT_LOCK
 #define MK_STRUCT_LOCK 1
 #endif

@@ -166,10 +166,15 @@ def measure_c2(dev, steps, warmup):
 def measure_c3(dev, steps, warmup):
     """TreeHash of State{registry, balances} at 10^6 validators, records and
     balances generated in HBM (registry.synthetic_*_device: the same bytes as
-    the host generators the golden was made from).  registry.DeviceStateHasher
-    (schedule "level1" unless PRYSM_C3_SCHED says otherwise)."""
+    the host generators the golden was made from).  The step: a stream of
+    states through registry.StatePipeline (each state's registry levels 2..10
+    in the next state's struct launch, its tops beside that launch; the last
+    state's top inside the timed region).  Beside it, one state alone through
+    registry.DeviceStateHasher ("level1"; PRYSM_C3_SCHED: another schedule).
+    PRYSM_C3_STREAM=0: time the one-state form as the step."""
     import torch
 
+    from prysm_amd import device as D
     from prysm_amd import registry as R
 
     g = golden("c3")
@@ -178,20 +183,44 @@ def measure_c3(dev, steps, warmup):
     dbal = R.synthetic_balances_device(n, g["seed"], dev)
     hasher = R.DeviceStateHasher(n, dev, schedule=os.environ.get("PRYSM_C3_SCHED", "level1"))
     out = hasher.out
-    sec = _timeit(lambda: hasher.submit(rec, dbal), steps, warmup)
-    got = bytes(out.cpu().numpy()).hex()
-    ok = got == g["state_root"]
+    sec_one = _timeit(lambda: hasher.submit(rec, dbal), steps, warmup)
+    one = bytes(out.cpu().numpy()).hex()
+    stream = os.environ.get("PRYSM_C3_STREAM", "1") == "1" and D.struct_pipe_ok(rec, n, 160, R.VALIDATOR_FIELDS)
+    got = one
+    sec = sec_one
+    if stream:
+        p = R.StatePipeline(n, dev)
+        for _ in range(warmup):
+            p.submit(rec, dbal)
+        p.flush()
+        p.wait()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            h = p.submit(rec, dbal)
+        p.flush()
+        p.wait()
+        torch.cuda.synchronize()
+        sec = (time.perf_counter() - t0) / steps
+        got = bytes(h.cpu().numpy()).hex()
+    ok = got == g["state_root"] and one == g["state_root"]
     # perms: 3 field hashes + 2 struct blocks per validator, registry + balances merkle, final
     perms = 5 * n + (n / 4 / 2) * 2 + n / 8 + (n / 16 / 2) * 2 + n / 32 + 1
     hashes = 4 * n + n / 8 + n / 8 + n / 32 + n / 32 + 1
     del rec, dbal
     return {"metric": "TreeHash of a 1M-validator State (registry + balances)", "unit": "validators/s",
             "value": n / sec, "sec": sec, "perms": perms, "hashes": hashes,
-            "dominant_kernel": "k_struct_lock (phase-locked, 5 perms per record + both trees' level-1 windows)",
+            "dominant_kernel": ("k_struct_lock<true> (phase-locked, 5 perms per record + both trees' level-1 windows "
+                                "+ the previous state's registry levels 2-10 in one extra slot per wave)" if stream
+                                else "k_struct_lock<false> (phase-locked, 5 perms per record + both trees' level-1 "
+                                     "windows)"),
             "root": got, "root_matches_golden": ok,
             "config": {"workload": "C3: synthetic State{[]*ValidatorRecord, []uint64}, 1,000,000 validators, "
-                                   "device-resident", "n": n, "root": got, "root_matches_golden": ok,
-                       "schedule": hasher.schedule}}
+                                   "device-resident" + (", a stream of states (registry.StatePipeline)" if stream
+                                                        else ""),
+                       "n": n, "root": got, "root_matches_golden": ok, "stream": stream,
+                       "schedule": hasher.schedule, "single_state_ms": sec_one * 1e3,
+                       "single_state_frac": _ops(perms, hashes) / sec_one / PEAK_INT_OPS}}
 
 
 def measure_c5(dev, steps, warmup):
@@ -266,8 +295,9 @@ def side_entry(r):
          "frac": ops / r["sec"] / PEAK_INT_OPS, "achieved_Tops": ops / r["sec"] / 1e12,
          "perms_per_step": r["perms"], "dominant_kernel": r["dominant_kernel"], "root": r["root"],
          "root_matches_golden": r["root_matches_golden"]}
-    for k in ("single_trie_ms", "single_trie_frac", "device_resident_ms", "device_resident_frac", "schedule",
-              "front", "reference_incremental_perms", "hbm_GBps_algorithmic"):
+    for k in ("single_trie_ms", "single_trie_frac", "single_state_ms", "single_state_frac", "stream",
+              "device_resident_ms", "device_resident_frac", "schedule", "front", "reference_incremental_perms",
+              "hbm_GBps_algorithmic"):
         if k in r["config"]:
             e[k] = r["config"][k]
     return e
