@@ -33,7 +33,7 @@ def test_bench_world2_line_is_self_sufficient():
     cfg, roof = out["config"], out["roofline"]
     assert out["n_gpus"] == 2 and cfg["world_size"] == 2
     assert 0 < roof["step_frac_aggregate"] < 1
-    assert roof["tree_perms"] == 3 * (1 << 20)  # 2^22 items: 2^20 windows x 2 + 2^20 - 1 nodes + 1
+    assert roof["tree_perms"] == 3 << 19  # 2^22 items: 2^19 windows x 2 + 2^19 - 1 nodes + 1
     assert len(cfg["per_rank_leaf_frac"]) == 2 and all(0 < f < 1 for f in cfg["per_rank_leaf_frac"])
     assert cfg["single_gpu_ms"] > 0
     assert 0 < cfg["parallel_efficiency"] <= 1.2
