@@ -27,25 +27,9 @@ using mk::kReduceThreads;
 
 namespace {
 
-#ifndef MK_SIDE_PRIO
 #define MK_SIDE_PRIO 1
-#endif
 constexpr bool kSidePrio = MK_SIDE_PRIO != 0;  // library side/copy streams at high priority
-#ifndef MK_REC_KERNEL
-#define MK_REC_KERNEL 1
-#endif
-constexpr bool kRecKernel = MK_REC_KERNEL != 0;  // k_keccak_rec<35> for 280-B deposit leaves
-#ifndef MK_STRUCT_FUSED
-#define MK_STRUCT_FUSED 1
-#endif
-constexpr bool kStructFused = MK_STRUCT_FUSED != 0;  // k_struct_fused instead of fields + message kernels
-#ifndef MK_STRUCT_REG
-#define MK_STRUCT_REG 1
-#endif
-constexpr bool kStructReg = MK_STRUCT_REG != 0;  // k_struct_reg<NB, NRAW> for bytes-then-u64 layouts
-#ifndef MK_TRIE_TOP_MAX_LOG2
 #define MK_TRIE_TOP_MAX_LOG2 17
-#endif
 constexpr uint64_t kTrieTopMax = 1ull << MK_TRIE_TOP_MAX_LOG2;  // trie levels at or below: k_trie_top3
 constexpr uint64_t kTrieTopWgs = 256;
 constexpr uint64_t kAppendMaxRange = 1020;  // k_trie_append<1024>: one parent per lane pair
@@ -437,7 +421,7 @@ int dev_hash_batch(const void* d_in, uint64_t n, uint32_t msg_len, void* d_out, 
                                dim3(mk::kLockThreads), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
         else
             hipLaunchKernelGGL(mk::k_keccak64, dim3(grid), dim3(256), 0, st, (const uint4*)d_in, n, (uint4*)d_out);
-    } else if (kRecKernel && msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0) {
+    } else if (msg_len == 280 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0) {
         hipLaunchKernelGGL((mk::k_keccak_rec<35>), dim3(std::min<uint64_t>(ceil_div(n, mk::kRecThreads), mk::kRecGridMax)),
                            dim3(mk::kRecThreads), 0, st, (const uint2*)d_in, n, (uint4*)d_out);
     } else if (msg_len % 8 == 0 && msg_len > 0 && ((uintptr_t)d_in % 8) == 0 && ((uintptr_t)d_out % 16) == 0) {
@@ -546,12 +530,8 @@ struct ElemPlan {
     uint64_t nwin = 0;
 };
 
-#ifndef MK_ELEM_LOCK
 #define MK_ELEM_LOCK 1
-#endif
-#ifndef MK_ELEM_LOCK_MIN_LOG2
 #define MK_ELEM_LOCK_MIN_LOG2 23  // elements (2^20 windows: 1024 groups)
-#endif
 
 int make_elem_plan(uint64_t n, uint32_t elem_len, bool aligned16, ElemPlan& e) {
     e = ElemPlan();
@@ -828,7 +808,7 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
                         hipStream_t st) {
     if (n == 0) return MK_OK;
     // fused path: dword-granular single-block fields, dword-aligned message
-    bool fused = kStructFused && sp.msg_len % 4 == 0 && sp.msg_len <= mk::kStructFusedMaxMsg &&
+    bool fused = sp.msg_len % 4 == 0 && sp.msg_len <= mk::kStructFusedMaxMsg &&
                  ((uintptr_t)d_rec % 4) == 0;
     bool vec16 = ((uintptr_t)d_rec % 16) == 0 && sp.rec_len % 16 == 0;
     for (uint32_t f = 0; f < sp.nfields; ++f) {
@@ -849,19 +829,19 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
         if (sp.kind[f] != MK_FIELD_RAW || sp.len[f] != 8) layout = false;
     const uint32_t nraw = sp.nfields - nb;
     const bool split = n <= mk::kStructSplitMaxN;  // latency-bound: 4 lanes per record
-    if (kStructReg && layout && split && nb == 3 && nraw == 6) {
+    if (layout && split && nb == 3 && nraw == 6) {
         hipLaunchKernelGGL((mk::k_struct_split<3, 6>), dim3(ceil_div(n, 64)), dim3(256), 0, st, (const uint8_t*)d_rec,
                            n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);
         HIPCHK(hipGetLastError());
         return MK_OK;
     }
-    if (kStructReg && layout && split && nb == 2 && nraw == 0) {
+    if (layout && split && nb == 2 && nraw == 0) {
         hipLaunchKernelGGL((mk::k_struct_split<2, 0>), dim3(ceil_div(n, 64)), dim3(256), 0, st, (const uint8_t*)d_rec,
                            n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);
         HIPCHK(hipGetLastError());
         return MK_OK;
     }
-    if (kStructReg && layout && nb == 3 && nraw == 6) {
+    if (layout && nb == 3 && nraw == 6) {
         if (MK_STRUCT_LOCK && vec16 && validator_layout(sp) && n >= (1u << 18))  // phase-locked, partial last group
             hipLaunchKernelGGL(mk::k_struct_lock<false>,
                                dim3(std::min<uint64_t>(ceil_div(n, mk::kLockThreads), lock_grid_cap(st))),
@@ -875,7 +855,7 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
         HIPCHK(hipGetLastError());
         return MK_OK;
     }
-    if (kStructReg && layout && nb == 2 && nraw == 0) {
+    if (layout && nb == 2 && nraw == 0) {
         hipLaunchKernelGGL((mk::k_struct_reg<2, 0>), dim3(ceil_div(n, mk::kStructThreads)), dim3(mk::kStructThreads),
                            0, st, (const uint8_t*)d_rec, n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);
         HIPCHK(hipGetLastError());
@@ -913,9 +893,7 @@ uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 #ifndef MK_H2D_CHUNKS
 #define MK_H2D_CHUNKS 8
 #endif
-#ifndef MK_H2D_MIN_CHUNK
 #define MK_H2D_MIN_CHUNK 65536
-#endif
 constexpr uint64_t kH2dChunks = MK_H2D_CHUNKS;
 constexpr uint64_t kH2dMinChunk = MK_H2D_MIN_CHUNK;
 
@@ -926,11 +904,9 @@ constexpr uint64_t kH2dMinChunk = MK_H2D_MIN_CHUNK;
 // finish from the windows (dev_finish_nodes: the same odd rule at every
 // level, hash.go:225-237).  false: not this layout / size (caller takes the
 // two-launch path).
-#ifndef MK_STRUCT_WIN
 #define MK_STRUCT_WIN 1
-#endif
 bool struct_win_ok(const void* d_rec, uint64_t n, const mk::StructSpec& sp) {
-    if (!MK_STRUCT_WIN || !MK_STRUCT_LOCK || !kStructReg || n < (1u << 18)) return false;
+    if (!MK_STRUCT_WIN || !MK_STRUCT_LOCK || n < (1u << 18)) return false;
     if (((uintptr_t)d_rec % 16) != 0 || sp.rec_len % 16 != 0 || !validator_layout(sp)) return false;
     for (uint32_t f = 0; f < sp.nfields; ++f)
         if (sp.kind[f] == MK_FIELD_BYTES && (sp.off[f] % 16 || sp.off[f] + ((sp.len[f] + 15) & ~15u) > sp.rec_len))

@@ -123,9 +123,7 @@ __device__ __forceinline__ void hash_final(uint4 r0, uint4 r1, uint64_t n, uint4
 // (first_level_generic, k_spread_leaf neighbours): the whole window is in
 // registers before the first permutation, so each 128-B line is fetched once.
 // The throughput leaf pass uses hash_window256_split below instead.
-#ifndef MK_MIN_WAVES
 #define MK_MIN_WAVES 1
-#endif
 
 __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint4& d0, uint4& d1) {
     State s;
@@ -158,8 +156,8 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
     digest(s, d0, d1);
 }
 
-// The throughput leaf pass's window (MK_LEAF_SPLIT, merkle_kernels.hpp; the
-// only form since round 3).  Block 1 (bytes 0..135) is loaded straight into
+// The throughput leaf pass's window (k_reduce<LEAF, FAST>; the only form
+// since round 3).  Block 1 (bytes 0..135) is loaded straight into
 // the state registers, block 2 only after the first permutation, in two
 // halves, so at most 16 data VGPRs are live beside the state; the thread's
 // held digests live in its own LDS level slots (k_reduce), so the kernel
@@ -172,9 +170,7 @@ __device__ __forceinline__ void hash_window256(const uint4* __restrict__ w, uint
 // 5 waves: 94 VGPRs and no spill, 0.8-1.7 % faster than 6 waves (80 VGPRs,
 // 15 dwords in scratch) and 7 waves (54 spilled) slower still
 // (profiles/r02zi, r02zj).
-#ifndef MK_LEAF_SPLIT_WAVES
 #define MK_LEAF_SPLIT_WAVES 5
-#endif
 __device__ __forceinline__ void hash_window256_split(const uint4* __restrict__ w, uint4& d0, uint4& d1) {
     State s;
     uint4 v[9];
@@ -359,11 +355,11 @@ __device__ __forceinline__ void reduce_levels_out(const ReduceArgs& a, uint4* ld
 // Non-final passes write 512 >> (levels-2) nodes per workgroup; the final
 // pass (one workgroup) reduces to the root and applies the length mix-in.
 template <bool LEAF, bool FAST, int NI>
-__global__ __launch_bounds__(kReduceThreads, (MK_LEAF_SPLIT && LEAF && FAST) ? MK_LEAF_SPLIT_WAVES : MK_MIN_WAVES) void
+__global__ __launch_bounds__(kReduceThreads, (LEAF && FAST) ? MK_LEAF_SPLIT_WAVES : MK_MIN_WAVES) void
 k_reduce(ReduceArgs a) {
     constexpr uint64_t kSpan1 = 2 * NI * kReduceThreads;  // first-level nodes per workgroup
     constexpr uint64_t kSpan2 = kSpan1 / 2;
-    constexpr bool kSplit = MK_LEAF_SPLIT && LEAF && FAST;
+    constexpr bool kSplit = LEAF && FAST;  // the split window form (hash_window256_split)
     __shared__ uint4 lds[2 * kSpan2];
     const uint32_t tid = threadIdx.x;
     const uint64_t wg = a.wg_base + blockIdx.x;
@@ -395,22 +391,16 @@ k_reduce(ReduceArgs a) {
             lds[2 * q + 1] = d1;
         }
     } else if constexpr (FAST) {
-        // Full workgroup of full windows / complete node pairs (host-checked):
-        // no bounds checks, no odd padding, one keccak_f copy per call site.
+        // Full workgroup of complete node pairs (host-checked): no bounds
+        // checks, no odd padding, one keccak_f copy per call site.
 #pragma unroll 1
         for (int i = 0; i < NI; ++i) {
             const uint32_t q = i * kReduceThreads + tid;
             const uint64_t j0 = lo1 + 2 * (uint64_t)q;
             uint4 l0, l1, r0, r1, d0, d1;
-            if constexpr (LEAF) {
-                const uint4* w = reinterpret_cast<const uint4*>(a.items) + j0 * 16;
-                hash_window256(w, l0, l1);
-                hash_window256(w + 16, r0, r1);
-            } else {
-                const uint4* in = reinterpret_cast<const uint4*>(a.items) + j0 * 4;
-                hash_pair(ld_node(in), ld_node(in + 1), ld_node(in + 2), ld_node(in + 3), false, l0, l1);
-                hash_pair(ld_node(in + 4), ld_node(in + 5), ld_node(in + 6), ld_node(in + 7), false, r0, r1);
-            }
+            const uint4* in = reinterpret_cast<const uint4*>(a.items) + j0 * 4;
+            hash_pair(ld_node(in), ld_node(in + 1), ld_node(in + 2), ld_node(in + 3), false, l0, l1);
+            hash_pair(ld_node(in + 4), ld_node(in + 5), ld_node(in + 6), ld_node(in + 7), false, r0, r1);
             hash_pair(l0, l1, r0, r1, false, d0, d1);
             lds[2 * q] = d0;
             lds[2 * q + 1] = d1;
@@ -786,9 +776,7 @@ __device__ __noinline__ void elem_window_generic(const ReduceArgs& a, uint64_t j
     digest(s, o0, o1);
 }
 
-#ifndef MK_ELEM_WAVES
 #define MK_ELEM_WAVES 4
-#endif
 // The leaf pass of the element-digest tree (a.n_items elements, a.nchunks =
 // ceil(n / 4) chunks, a.c1 windows), one window pair per thread (NI = 1:
 // 512 windows = 4096 elements per workgroup; LDS 8 KB of levels + 32 KB of
@@ -1402,9 +1390,7 @@ __global__ void k_final_small(const uint8_t* __restrict__ items, uint64_t total,
 // Batched hashutil.Hash: n messages of 64 B (one permutation each).
 // 6 waves/SIMD (73 VGPRs, no spill): 2^24 messages 1.804 -> 1.749 ms against
 // the unconstrained 82 VGPRs / 5 waves (8 waves spills and halves the rate)
-#ifndef MK_K64_WAVES
 #define MK_K64_WAVES 6
-#endif
 __global__ __launch_bounds__(256, MK_K64_WAVES) void k_keccak64(const uint4* __restrict__ in, uint64_t n,
                                                                uint4* __restrict__ out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1730,9 +1716,7 @@ __global__ __launch_bounds__(kStructThreads) void k_struct_fused(const uint8_t* 
 // message in k_struct_fused), the NRAW scalars are re-read from the record
 // at absorb time, and the absorb loop is unrolled over compile-time message
 // dwords.  No barrier: a thread only touches its own LDS column.
-#ifndef MK_STRUCT_REG_WAVES
 #define MK_STRUCT_REG_WAVES 6
-#endif
 template <int NB, int NRAW>
 __global__ __launch_bounds__(kStructThreads, MK_STRUCT_REG_WAVES) void k_struct_reg(const uint8_t* __restrict__ rec,
                                                                                   uint64_t n, StructSpec sp,
@@ -2229,9 +2213,7 @@ __global__ __launch_bounds__(256) void k_keccak_words(const uint2* __restrict__ 
 // 0.582 ms, profiles/r02d/ab_rec_prefetch.log): the other resident waves
 // hide the load as well.  At 5 waves/SIMD (96 VGPRs, 4 dwords spilled) the
 // stream of 2^20-deposit tries got 3 % slower (profiles/r02m/rejected/).
-#ifndef MK_REC_WAVES
 #define MK_REC_WAVES 1
-#endif
 template <int NW>
 __global__ __launch_bounds__(kRecThreads, MK_REC_WAVES) void k_keccak_rec(const uint2* __restrict__ in, uint64_t n,
                                                                           uint4* __restrict__ out) {
@@ -2471,9 +2453,7 @@ template __global__ void k_trie_rec_lock<1024, 4, true>(const uint2*, uint64_t, 
 // ----------------------------------------------------------------------------
 // Deposit trie level: node j = K(in[2j] || (2j+1 < cin ? in[2j+1] : 0^32)),
 // the map-miss-reads-zero rule of deposit_trie.go:35-37.
-#ifndef MK_TRIE_LEVEL_WAVES
 #define MK_TRIE_LEVEL_WAVES 1
-#endif
 __global__ __launch_bounds__(256, MK_TRIE_LEVEL_WAVES) void k_trie_level(const uint4* __restrict__ in, uint64_t cin,
                                                                         uint4* __restrict__ out) {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

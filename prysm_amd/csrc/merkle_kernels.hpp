@@ -8,9 +8,7 @@
 namespace mk {
 
 constexpr uint32_t kMaxStructFields = 32;
-#ifndef MK_STRUCT_THREADS
 #define MK_STRUCT_THREADS 256
-#endif
 constexpr uint32_t kStructThreads = MK_STRUCT_THREADS;  // k_struct_fused: one record per thread
 constexpr uint32_t kStructFusedMaxMsg = 160;          // LDS: kStructThreads * msg_len bytes
 constexpr uint32_t kStructFusedMaxField = 64;         // bytes fields held in 16 registers
@@ -22,11 +20,6 @@ struct StructSpec {                 // flat fixed-layout record (hash.go:141-159
     uint32_t nfields, rec_len, msg_len;
 };
 
-// The free-running leaf kernel's split window form (merkle_kernels.hip).
-#ifndef MK_LEAF_SPLIT
-#define MK_LEAF_SPLIT 1
-#endif
-constexpr bool kLeafSplit = MK_LEAF_SPLIT != 0;
 template <bool LEAF, bool FAST, int NI>
 __global__ void k_reduce(ReduceArgs a);
 // Phase-locked leaf pass (merkle_kernels.hip): 4096 full windows per
@@ -67,26 +60,18 @@ struct StructPrev {
 template <bool PREV>
 __global__ void k_struct_lock(const uint8_t* rec, uint64_t n, uint4* roots, uint32_t gpw, uint4* wins,
                               const uint8_t* vals, uint64_t vbytes, uint4* vwins, StructPrev prev);
-#ifndef MK_STRUCT_LOCK
 #define MK_STRUCT_LOCK 1
-#endif
 template <int NB, int NRAW>
 __global__ void k_struct_split(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots);
-#ifndef MK_STRUCT_SPLIT_MAX_N
 #define MK_STRUCT_SPLIT_MAX_N 32768
-#endif
 constexpr uint64_t kStructSplitMaxN = MK_STRUCT_SPLIT_MAX_N;  // k_struct_split at or below (0: never)
 template <uint32_t NT, bool LEAF>
 __global__ void k_wave3(ReduceArgs a);
-#ifndef MK_WAVE3_SPREAD
 #define MK_WAVE3_SPREAD 1  // k_wave3's last levels one state per wave (the pair finalize needs it)
-#endif
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
 __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);
 __global__ void k_keccak64_lock(const uint4* in, uint64_t n, uint4* out);  // any n (a partial last group)
-#ifndef MK_K64_LOCK
 #define MK_K64_LOCK 1
-#endif
 __global__ void k_keccak_fixed(const uint8_t* in, uint64_t n, uint32_t msg_len, uint4* out);
 __global__ void k_keccak_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint4* out);
 __global__ void k_trie_level(const uint4* in, uint64_t cin, uint4* out);
@@ -106,9 +91,7 @@ struct TriePrev {
 template <uint32_t NT, int DPT, bool PIPE>
 __global__ void k_trie_rec_lock(const uint2* in, uint64_t ngroups, uint4* L0, uint4* L1, uint4* L2, uint4* L3,
                                 TriePrev prev);
-#ifndef MK_TRIE_LOCK
 #define MK_TRIE_LOCK 1
-#endif
 #ifndef MK_TRIE_LOCK_NT
 #define MK_TRIE_LOCK_NT 1024  // threads per workgroup (one workgroup per CU)
 #endif
@@ -118,17 +101,11 @@ __global__ void k_trie_rec_lock(const uint2* in, uint64_t ngroups, uint4* L0, ui
 #ifndef MK_TRIE_LOCK_GRID
 #define MK_TRIE_LOCK_GRID 256  // persistent grid cap
 #endif
-#ifndef MK_TRIE_LOCK_MIN
 #define MK_TRIE_LOCK_MIN (1u << 18)  // deposits: at least one group per CU
-#endif
 
-#ifndef MK_REC_THREADS
 #define MK_REC_THREADS 256
-#endif
 constexpr uint32_t kRecThreads = MK_REC_THREADS;  // k_keccak_rec workgroup size
-#ifndef MK_REC_GRID
 #define MK_REC_GRID 4096
-#endif
 constexpr uint32_t kRecGridMax = MK_REC_GRID;  // k_keccak_rec grid cap (A/B at 2^20: 512..4096 WGs, 4096 best)
 template <uint32_t NT>
 __global__ void k_trie_top3(const uint32_t* in, uint64_t cin, uint32_t* lv_out, uint32_t levels, uint64_t capn);
@@ -138,12 +115,8 @@ __global__ void k_verify_branches(const uint4* leaves, const uint4* branches, co
 template <uint32_t NT>
 __global__ void k_trie_append(uint32_t* levels, uint64_t cap, uint32_t d0, uint64_t lo, uint64_t c, uint32_t d_end,
                               uint32_t depth, uint32_t* root_out);
-#ifndef MK_TRIE_SPREAD
 #define MK_TRIE_SPREAD 1
-#endif
-#ifndef MK_SPREAD_WAVES_MAX
 #define MK_SPREAD_WAVES_MAX 16
-#endif
 constexpr uint32_t kSpreadWavesMax = MK_SPREAD_WAVES_MAX;  // k_trie_spread: one state per wave (<= 4 per SIMD)
 __global__ void k_spread_leaf(ReduceArgs a, uint32_t w8);
 // new deposits k_trie_spread hashes into level 0 first (k == 0: none)

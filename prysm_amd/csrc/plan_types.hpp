@@ -15,9 +15,7 @@ constexpr uint32_t kWave2Span = kWaveThreads / 2;    // lane pairs per wave: 32 
 constexpr uint32_t kMidThreads = 1024;               // largest k_wave3: 16 waves, 512 lane pairs, 10 levels
 // Wide leaf passes of full windows run the phase-locked k_leaf_lock_sc
 // (merkle_kernels.hip, planner.cpp) instead of k_reduce's fused form.
-#ifndef MK_LEAF_LOCK
 #define MK_LEAF_LOCK 1
-#endif
 #ifndef MK_LOCK_BARS
 #define MK_LOCK_BARS 2  // s_barriers per locked Keccak round (keccak_dev.hpp round_asm)
 #endif

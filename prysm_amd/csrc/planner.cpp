@@ -39,46 +39,22 @@ mk_call* swap_call(mk_call* c) {
 // ---- configuration (compile-time knobs; A/B variants via the Makefile) ----------
 // latency passes: k_wave3 (bit-interleaved lane pairs, one state per wave at
 // the top; round 4 removed the lo/hi-halves k_wave2 it replaced in round 1)
-#ifndef MK_NODE_WAVE_MAX_LOG2
 #define MK_NODE_WAVE_MAX_LOG2 17
-#endif
 // node passes switch to the latency form at or below this width: the first
 // level is throughput-bound either way, but the throughput kernel spends ~9
 // serial permutations on its 5 levels where the wave pass spends 6
 constexpr uint64_t kNodeWaveMaxC1 = 1ull << MK_NODE_WAVE_MAX_LOG2;
-#ifndef MK_NODE_WAVE_WGS
 #define MK_NODE_WAVE_WGS 256
-#endif
 constexpr uint64_t kNodeWaveWgs = MK_NODE_WAVE_WGS;
-#ifndef MK_LEAF_WAVE_MAX_LOG2
 #define MK_LEAF_WAVE_MAX_LOG2 17
-#endif
 constexpr uint64_t kLeafWaveMaxC1 = 1ull << MK_LEAF_WAVE_MAX_LOG2;  // leaf passes at or below: latency form
-#ifndef MK_REDUCE_NI2_MIN_LOG2
 #define MK_REDUCE_NI2_MIN_LOG2 18
-#endif
 constexpr uint64_t kReduceNi2MinC1 = 1ull << MK_REDUCE_NI2_MIN_LOG2;  // leaf passes narrower than this use NI = 1
-#ifndef MK_TOP_ONE_WG
-#define MK_TOP_ONE_WG 1
-#endif
-constexpr bool kTopOneWg = MK_TOP_ONE_WG != 0;
-// The one-workgroup top pass takes the full 1024 threads even when fewer
-// pairs need them: k_wave3 switches to one state per wave once a level has
-// at most NT/64 parents, so 16 waves run the last 4 levels and the mix-in in
-// the spread form instead of 2 (256 threads) or 1.
-#ifndef MK_TOP_WG1024
-#define MK_TOP_WG1024 1
-#endif
-constexpr bool kTopWg1024 = MK_TOP_WG1024 != 0;
 // Largest k_wave3 workgroup the planner picks (64..1024 threads).
-#ifndef MK_W3_MAX_NT
 #define MK_W3_MAX_NT 1024
-#endif
 constexpr uint32_t kW3MaxNt = MK_W3_MAX_NT < kMidThreads ? MK_W3_MAX_NT : kMidThreads;
 // leaf passes of at most this many windows: k_spread_leaf (0: never)
-#ifndef MK_SPREAD_LEAF_MAX_LOG2
 #define MK_SPREAD_LEAF_MAX_LOG2 12
-#endif
 constexpr uint64_t kSpreadLeafMaxC1 = MK_SPREAD_LEAF_MAX_LOG2 < 0 ? 0 : 1ull << MK_SPREAD_LEAF_MAX_LOG2;
 constexpr uint64_t kSpreadSpan = 16;  // windows per k_spread_leaf workgroup
 // Phase-locked leaf pass (k_leaf_lock_sc, merkle_kernels.hip): wide leaf passes
@@ -86,12 +62,8 @@ constexpr uint64_t kSpreadSpan = 16;  // windows per k_spread_leaf workgroup
 // 4 windows) in 1024-thread workgroups whose Keccak rounds hold an s_barrier;
 // the next (node) pass takes the levels the leaf pass used to fuse in LDS.
 constexpr bool kLeafLock = MK_LEAF_LOCK != 0;  // plan_types.hpp
-#ifndef MK_LOCK_SUBTREE_PERSIST
 #define MK_LOCK_SUBTREE_PERSIST 0
-#endif
-#ifndef MK_LEAF_LOCK_MIN_LOG2
 #define MK_LEAF_LOCK_MIN_LOG2 20
-#endif
 constexpr uint64_t kLeafLockMinC1 = 1ull << MK_LEAF_LOCK_MIN_LOG2;  // windows (first-level nodes)
 constexpr uint32_t kLockLevels = 3;
 constexpr uint64_t kLockSpans = 4;  // k_reduce spans (1024 windows) per k_leaf_lock_sc workgroup
@@ -186,9 +158,12 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         uint32_t nt = w3 ? kWaveThreads : kReduceThreads;
         if (w3) {
             while (nt < kW3MaxNt && ceil_div(c1, nt / 2) > kNodeWaveWgs) nt *= 2;
-            if (kTopOneWg)  // the last <= 512 pairs in one workgroup: one launch to the root
-                while (nt < kW3MaxNt && c1 <= kW3MaxNt / 2 && c1 > nt / 2) nt *= 2;
-            if (kTopWg1024 && c1 <= kW3MaxNt / 2) nt = kW3MaxNt;
+            // the last <= 512 pairs in one workgroup of the full 1024 threads
+            // even when fewer pairs need them: k_wave3 switches to one state
+            // per wave once a level has at most NT/64 parents, so 16 waves run
+            // the last 4 levels and the mix-in in the spread form (one launch
+            // to the root)
+            if (c1 <= kW3MaxNt / 2) nt = kW3MaxNt;
         }
         // throughput pass: 2 window pairs per thread on wide passes, 1 on mid-size
         // leaf passes so they still spread over the CUs
