@@ -1136,8 +1136,8 @@ __device__ __forceinline__ void wave3_spread_levels(uint32_t* lds, uint64_t& c, 
 // arrived-slot bits (epochs are 30-bit and wrap; "newer" = ahead by less than
 // 2^29): a finisher of a newer epoch than the word's starts the mask afresh,
 // so a pair left half-done (a failed launch) cannot pair with the next one; a
-// finisher of an OLDER epoch (a late one) is ignored, so it cannot clear the
-// current pair's bits.  The first finisher of an epoch zeroes pair[64..96)
+// finisher of an OLDER epoch (a late one) is ignored -- it writes neither its
+// slot nor the arrival word -- so it cannot clear the current pair's bits.  The first finisher of an epoch zeroes pair[64..96)
 // before it sets its bit, so a pair that never completes reads back as
 // zeros, never as the previous epoch's root.
 __device__ __forceinline__ void spread_store_digest(uint32_t e, uint32_t o, uint32_t L, uint32_t* out) {
@@ -1163,6 +1163,11 @@ __device__ __forceinline__ void wave3_spread_final(const uint32_t* lds, uint64_t
     }
     if (i == 16u) o ^= 0x80000000u;
     spread::keccak_f(e, o, cst);
+    if (pair) {  // a late finisher of an older epoch than the word's leaves the block alone
+        uint32_t stale = 0;
+        if (L == 0) stale = ((epoch - (atomicAdd(pair + 24, 0u) >> 2)) & 0x3FFFFFFFu) >= (1u << 29);
+        if (__shfl(stale, 0)) return;
+    }
     spread_store_digest(e, o, L, out);
     if (!pair) return;
     __threadfence();  // this field's root is visible before its arrival bit
@@ -2303,7 +2308,6 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
     __shared__ uint4 buf[NT / 64][9 * 64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint4* Bw = buf[wave];
-    const uint2* Bw2 = reinterpret_cast<const uint2*>(Bw);
     uint4* const lv[4] = {L0, L1, L2, L3};
     auto first = [&](uint64_t g) { return (g * NT + 64 * wave) * DPT; };  // lane 0's first deposit
     auto dma = [&](uint64_t g, int i, int b) {
@@ -2320,7 +2324,6 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                                              MK_TRIE_LOCK_AUX);
         }
     };
-    auto tail = [&](uint64_t g, int i) { return in[(first(g) + DPT * lane + i) * NW + 34]; };
     // a node is stored after the next slot's first wait, so no wait covers a
     // store issued just before it (stores count in vmcnt)
     uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
@@ -2364,12 +2367,45 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
         }
         asm volatile("" ::: "memory");
     };
+    // Absorb lane m's staged block (17 8-B words) into s (XOR; SET: assign)
+    // from its 9 16-B units, read as rows at the odd stride 9 (conflict-free
+    // ds_read_b128: a b64 read of 8 B from each lane's own 16-B unit needs two
+    // LDS cycles per 32 lanes whatever the layout).  The block starts `o8`
+    // words (0 or 1, wave-uniform) into unit 0, so word w is half (w + o8) & 1
+    // of unit (w + o8) / 2: one select per dword, every state index static
+    // (the slot loop stays rolled).  Units are consumed one at a time (a
+    // compiler fence between) so few data VGPRs are live beside the state.
+    // Returns word 17 (the word after the block when o8 = 0).
+    auto absorb = [&](State& st, uint32_t o8, auto setc) {
+        constexpr bool SET = decltype(setc)::value;
+        const bool sh = o8 != 0;
+        uint4 prev = Bw[9 * lane];
+        uint2 w17 = make_uint2(0, 0);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            // words 2k and 2k + 1: unshifted (x, y) (z, w) of unit k; shifted
+            // (z, w) of unit k and (x, y) of unit k + 1
+            const uint4 cur = k + 1 < 9 ? Bw[9 * lane + k + 1] : make_uint4(0, 0, 0, 0);
+            const uint32_t a0 = sh ? prev.z : prev.x, a1 = sh ? prev.w : prev.y;
+            const uint32_t b0 = sh ? cur.x : prev.z, b1 = sh ? cur.y : prev.w;
+            const int wa = 2 * k, wb = 2 * k + 1;
+            st.lo[wa] = SET ? a0 : st.lo[wa] ^ a0;
+            st.hi[wa] = SET ? a1 : st.hi[wa] ^ a1;
+            if (wb < 17) {
+                st.lo[wb] = SET ? b0 : st.lo[wb] ^ b0;
+                st.hi[wb] = SET ? b1 : st.hi[wb] ^ b1;
+            } else {
+                w17 = make_uint2(prev.z, prev.w);
+            }
+            prev = cur;
+            asm volatile("" ::: "memory");
+        }
+        return w17;
+    };
+    using Set = std::true_type;
+    using Xor = std::false_type;
     uint64_t g = blockIdx.x;
-    uint2 tnext = make_uint2(0, 0);
-    if (g < ngroups) {
-        dma(g, 0, 0);
-        tnext = tail(g, 0);
-    }
+    if (g < ngroups) dma(g, 0, 0);
 #pragma unroll 1
     for (; g < ngroups; g += gridDim.x) {
         const uint64_t gn = g + gridDim.x;
@@ -2383,37 +2419,35 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
             if (PIPE && i == 2 && (wv == 12 || wv == 13)) prev_slot(5);  // slot 7
             if (PIPE && i == 3 && wv == 14) prev_slot(6);              // slot 10
             State s;
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 0 and the tail word landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 0 landed
             flush();
             qp = nullptr;
-            const uint2 tl = tnext;
-#pragma unroll
-            for (int w = 0; w < 17; ++w) {
-                const uint2 v = Bw2[18 * lane + (i & 1) + w];
-                s.lo[w] = v.x;
-                s.hi[w] = v.y;
-            }
+            absorb(s, i & 1, Set{});
 #pragma unroll
             for (int w = 17; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: block 1 may land
             keccak_f_lock_mid<MK_TRIE_DMA_ROUND>(s, [&] { dma(g, i, 1); });
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 1 landed
-#pragma unroll
-            for (int w = 0; w < 17; ++w) {
-                const uint2 v = Bw2[18 * lane + ((i + 1) & 1) + w];
-                s.lo[w] ^= v.x;
-                s.hi[w] ^= v.y;
-            }
+            // the 8-B tail word (deposit bytes 272..279): an odd slot's block 1
+            // image ends with it (the block starts 16-B aligned, 9 units = 144
+            // B); an even slot's is the first word of the NEXT slot's block 0
+            // image (that deposit starts 8 B into the unit holding it), read
+            // after its DMA lands below -- no per-lane load of its own
+            // an odd slot's block 1 starts 16-B aligned and ends with the tail word
+            uint2 tl = absorb(s, (i + 1) & 1, Xor{});
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             keccak_f_lock_mid<MK_TRIE_DMA_ROUND>(s, [&] {
-                if (i + 1 < DPT) {
+                if (i + 1 < DPT)
                     dma(g, i + 1, 0);
-                    tnext = tail(g, i + 1);
-                } else if (gn < ngroups) {
+                else if (gn < ngroups)
                     dma(gn, 0, 0);
-                    tnext = tail(gn, 0);
-                }
             });
+            if (!(i & 1)) {  // slot i + 1 < DPT of this group: its block 0 holds the tail
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const uint4 v = Bw[9 * lane];
+                tl = make_uint2(v.x, v.y);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
             s.lo[0] ^= tl.x;  // word 34, then the domain pad byte (word 35 = lane 1)
             s.hi[0] ^= tl.y;
             s.lo[1] ^= 1u;

@@ -431,13 +431,18 @@ def test_trie_pipeline_pipe_submits_from_two_streams(gpu):
         D.synth_fill(d, SEED + 995 + t)
         datas.append(d)
     torch.cuda.synchronize()
+    got = []
     for t, d in enumerate(datas):
         with torch.cuda.stream(streams[t % 2]):
             handles.append(pipe.submit(d))
+        if t:  # a root is produced by the next submit and valid for two more (four sets rotate)
+            torch.cuda.synchronize()
+            got.append(bytes(handles[t - 1].cpu().numpy()))
     with torch.cuda.stream(streams[1]):
         pipe.flush()
     torch.cuda.synchronize()
+    got.append(bytes(handles[-1].cpu().numpy()))
     for t, d in enumerate(datas):
         host = d.cpu().numpy()
         want = O.deposit_trie_levels([bytes(host[i * ln:(i + 1) * ln]) for i in range(n)])[0]
-        assert bytes(handles[t].cpu().numpy()) == want, t
+        assert got[t] == want, t

@@ -160,10 +160,50 @@ def ab_trie(a, libs, dev):
             assert bytes(souts[(S - 1) % 2].cpu().numpy()).hex() == roots[v], v
             if r:
                 stream_ms[v].append(e0.elapsed_time(e1) / S)
+    # the C5 bench's form since round 4: the pipelined front (trie i's locked
+    # front also builds levels 3-7 of trie i-1; trie i-1's top on the side
+    # stream beside trie i+1's front), pipeline.TriePipeline(front="pipe")
+    pipe_ms = {v: [] for v in a.variants}
+    P = 100
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    if first.mk_deposit_trie_pipe_ok(vp(data), n, ln, depth, st):
+        plv = [torch.empty_like(lv) for _ in range(4)]
+        prt = [torch.empty(32, dtype=torch.uint8, device=dev) for _ in range(4)]
+        for r in range(a.rounds + 1):
+            for v, L in libs.items():
+                torch.cuda.synchronize()
+                done = {}
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                prev = None
+                for i in range(P):
+                    s = i % 4
+                    if i % 2 == 0 and (i - 3) in done:
+                        torch.cuda.current_stream().wait_event(done[i - 3])
+                    assert L.mk_dev_deposit_trie_build_pipe(None, vp(plv[s]), None if prev is None else vp(plv[prev]),
+                                                            n, vp(data), n, ln, depth, st) == 0
+                    if prev is not None:
+                        side.wait_stream(torch.cuda.current_stream())
+                        assert L.mk_dev_deposit_trie_pipe_top(None, vp(plv[prev]), n, n, depth, vp(prt[prev]),
+                                                              sst) == 0
+                        done[i - 1] = torch.cuda.Event()
+                        done[i - 1].record(side)
+                    prev = s
+                side.wait_stream(torch.cuda.current_stream())
+                assert L.mk_dev_deposit_trie_levels(None, vp(plv[prev]), n, n, 2, depth, depth, vp(prt[prev]),
+                                                    sst) == 0
+                torch.cuda.current_stream().wait_stream(side)
+                e1.record()
+                torch.cuda.synchronize()
+                assert bytes(prt[prev].cpu().numpy()).hex() == roots[v], v
+                if r:
+                    pipe_ms[v].append(e0.elapsed_time(e1) / P)
     for v in a.variants:
         print(json.dumps({"variant": v, "trie_log2n": a.log2n, "median_ms": statistics.median(times[v]),
                           "min_ms": min(times[v]), "stream_median_ms": statistics.median(stream_ms[v]),
-                          "stream_min_ms": min(stream_ms[v])}))
+                          "stream_min_ms": min(stream_ms[v]),
+                          "pipe_median_ms": statistics.median(pipe_ms[v]) if pipe_ms[v] else None,
+                          "pipe_min_ms": min(pipe_ms[v]) if pipe_ms[v] else None}))
     print(json.dumps({"root": next(iter(roots.values()), None)}))
 
 
