@@ -1140,6 +1140,12 @@ __device__ __forceinline__ void wave3_spread_levels(uint32_t* lds, uint64_t& c, 
 // slot nor the arrival word -- so it cannot clear the current pair's bits.  The first finisher of an epoch zeroes pair[64..96)
 // before it sets its bit, so a pair that never completes reads back as
 // zeros, never as the previous epoch's root.
+// How far `epoch` is ahead of an arrival word's epoch (mod 2^30; >= 2^29:
+// behind).  A word whose epoch is 0 was never used (valid epochs are >= 1):
+// every epoch is ahead of it.
+__device__ __forceinline__ uint32_t epoch_ahead(uint32_t epoch, uint32_t word) {
+    return (word >> 2) == 0u ? 1u : (epoch - (word >> 2)) & 0x3FFFFFFFu;
+}
 __device__ __forceinline__ void spread_store_digest(uint32_t e, uint32_t o, uint32_t L, uint32_t* out) {
     if (L < 4u) {
         out[2 * L] = ilv::spread16(e) | (ilv::spread16(o) << 1);
@@ -1165,7 +1171,7 @@ __device__ __forceinline__ void wave3_spread_final(const uint32_t* lds, uint64_t
     spread::keccak_f(e, o, cst);
     if (pair) {  // a late finisher of an older epoch than the word's leaves the block alone
         uint32_t stale = 0;
-        if (L == 0) stale = ((epoch - (atomicAdd(pair + 24, 0u) >> 2)) & 0x3FFFFFFFu) >= (1u << 29);
+        if (L == 0) stale = epoch_ahead(epoch, atomicAdd(pair + 24, 0u)) >= (1u << 29);
         if (__shfl(stale, 0)) return;
     }
     spread_store_digest(e, o, L, out);
@@ -1176,7 +1182,7 @@ __device__ __forceinline__ void wave3_spread_final(const uint32_t* lds, uint64_t
         uint32_t* word = pair + 24;
         uint32_t old = atomicAdd(word, 0u);  // an atomic read of the arrival word
         for (;;) {
-            const uint32_t ahead = (epoch - (old >> 2)) & 0x3FFFFFFFu;
+            const uint32_t ahead = epoch_ahead(epoch, old);
             if (ahead >= (1u << 29)) break;  // an older epoch than the word's: a late finisher, ignored
             if (ahead != 0u || (old & 3u) == 0u) {  // first of this epoch (so far): clear the pair root
                 for (uint32_t w = 16; w < 24; ++w) pair[w] = 0u;
