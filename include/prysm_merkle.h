@@ -276,34 +276,40 @@ int mk_dev_ssz_struct_list_level1(mk_call* call, const void* d_records, uint64_t
                                   const void* d_values, uint64_t nvalues, uint32_t value_len, void* d_value_nodes,
                                   void* stream);
 /* A stream of states (the State{registry, balances} of BASELINE config 3,
- * hash.go:118-159, one TreeHash per state) with each state's registry tree
- * folded into the NEXT state's struct launch: mk_dev_ssz_struct_list_level1
- * plus, in the same launch, levels 2..10 of the PREVIOUS state's registry
- * tree from its level-1 nodes d_prev_nodes (NULL for the first state), over
- * every complete 512-node subtree, into d_prev_levels
- * (mk_ssz_struct_pipe_levels_bytes(n)).  Then
- * mk_dev_ssz_struct_pipe_top(d_prev_nodes, .., d_prev_levels, ..) finishes
- * the previous state's registry root (the ragged last subtree, the ~245-node
- * top and the length mix-in; on another stream, beside the next launch).
- * Takes what mk_ssz_struct_pipe_ok accepts on the same stream (as
+ * hash.go:118-159, one TreeHash per state) with each state's trees folded
+ * into the NEXT state's struct launch: mk_dev_ssz_struct_list_level1 plus,
+ * in the same launch, levels 2..10 of the PREVIOUS state's registry tree from
+ * its level-1 nodes d_prev_nodes (NULL for the first state) over every
+ * complete 512-node subtree, into d_prev_levels, and levels 2..4 of its
+ * second list's tree from d_prev_value_nodes over every complete 128-node
+ * subtree, into d_prev_value_levels (NULL: none).  Buffer sizes from
+ * mk_ssz_struct_pipe_levels_bytes(n, nvalues, value_len, which): which = 0
+ * the registry's, 1 the second list's.  Then mk_dev_ssz_struct_pipe_top
+ * finishes each of the previous state's trees (the ragged last subtree, the
+ * levels above the slots and the length mix-in) as one field of a pair
+ * block, on another stream, beside the next launch.  Takes what
+ * mk_ssz_struct_pipe_ok accepts on the same stream (as
  * mk_ssz_struct_list_level1_ok, with exactly 4 groups of 1024 records per
- * workgroup: 3 x 2^18 < n <= 2^20 on 256 CUs); MK_EINVAL otherwise.  The
- * previous state must have the same n. */
+ * workgroup: 3 x 2^18 < n <= 2^20 on 256 CUs; a second list of at most 128
+ * windows per workgroup, e.g. n 8-B balances); MK_EINVAL otherwise.  The
+ * previous state must have the same n and second-list shape. */
 int mk_ssz_struct_pipe_ok(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
                           uint32_t nfields, void* stream);
-uint64_t mk_ssz_struct_pipe_levels_bytes(uint64_t n);
-uint64_t mk_ssz_struct_pipe_top_workspace_bytes(uint64_t n);
+uint64_t mk_ssz_struct_pipe_levels_bytes(uint64_t n, uint64_t nvalues, uint32_t value_len, uint32_t which);
+uint64_t mk_ssz_struct_pipe_top_workspace_bytes(uint64_t n, uint64_t nvalues, uint32_t value_len, uint32_t which);
 int mk_dev_ssz_struct_list_level1_pipe(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
                                        const mk_field* fields, uint32_t nfields, void* d_roots, void* d_nodes,
                                        const void* d_values, uint64_t nvalues, uint32_t value_len,
                                        void* d_value_nodes, const void* d_prev_nodes, void* d_prev_levels,
-                                       void* stream);
-/* The registry root of a state whose levels 2..10 a later pipelined launch
- * built (d_nodes: its level-1 nodes, d_levels: those levels), as one field
- * of a pair block (mk_dev_ssz_merkle_finish_nodes_pair semantics: slot,
- * epoch, the second finisher hashes the struct root). */
-int mk_dev_ssz_struct_pipe_top(mk_call* call, const void* d_nodes, uint64_t n, void* d_levels, void* d_pair_block,
-                               uint32_t slot, uint32_t epoch, void* d_ws, uint64_t ws_bytes, void* stream);
+                                       const void* d_prev_value_nodes, void* d_prev_value_levels, void* stream);
+/* One tree's root of a state whose slot levels a later pipelined launch
+ * built (d_nodes: its level-1 nodes, d_levels: those levels; which = 0 the
+ * registry of n records, 1 the second list of nvalues items of value_len
+ * bytes), as one field of a pair block (mk_dev_ssz_merkle_finish_nodes_pair
+ * semantics: slot, epoch, the second finisher hashes the struct root). */
+int mk_dev_ssz_struct_pipe_top(mk_call* call, const void* d_nodes, uint64_t n, uint64_t nvalues,
+                               uint32_t value_len, uint32_t which, void* d_levels, void* d_pair_block, uint32_t slot,
+                               uint32_t epoch, void* d_ws, uint64_t ws_bytes, void* stream);
 
 /* ---- hashutil.MerkleRoot (merkleRoot.go:12-30) -------------------------- */
 /* Root of the heap o[i] = Hash(o[2i] || o[2i+1]) over leaves

@@ -83,11 +83,11 @@ _SIGS = {
     "mk_ssz_struct_list_level1_ok": (_int, [_vp, _u64, _u32, _vp, _u32]),
     "mk_dev_ssz_struct_list_level1": (_int, [_cp, _vp, _u64, _u32, _vp, _u32, _vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "mk_ssz_struct_pipe_ok": (_int, [_vp, _u64, _u32, _vp, _u32, _vp]),
-    "mk_ssz_struct_pipe_levels_bytes": (_u64, [_u64]),
-    "mk_ssz_struct_pipe_top_workspace_bytes": (_u64, [_u64]),
+    "mk_ssz_struct_pipe_levels_bytes": (_u64, [_u64, _u64, _u32, _u32]),
+    "mk_ssz_struct_pipe_top_workspace_bytes": (_u64, [_u64, _u64, _u32, _u32]),
     "mk_dev_ssz_struct_list_level1_pipe": (_int, [_cp, _vp, _u64, _u32, _vp, _u32, _vp, _vp, _vp, _u64, _u32, _vp,
-                                                  _vp, _vp, _vp]),
-    "mk_dev_ssz_struct_pipe_top": (_int, [_cp, _vp, _u64, _vp, _vp, _u32, _u32, _vp, _u64, _vp]),
+                                                  _vp, _vp, _vp, _vp, _vp]),
+    "mk_dev_ssz_struct_pipe_top": (_int, [_cp, _vp, _u64, _u64, _u32, _u32, _vp, _vp, _u32, _u32, _vp, _u64, _vp]),
     "mk_ssz_struct_list_root": (_int, [_cp, _vp, _u64, _u32, _vp, _u32, _vp]),
     "mk_merkle_root": (_int, [_cp, _vp, _vp, _u64, _vp, _vp]),
     "mk_merkle_root_workspace_bytes": (_u64, [_u64]),

@@ -1960,21 +1960,32 @@ int mk_dev_ssz_struct_list_level1(mk_call* call, const void* d_records, uint64_t
 }
 
 // ---- a stream of states (registry.StatePipeline) ----------------------------
-// The registry tree's level-1 nodes of workgroup b of the pipelined launch,
-// [512 b, 512 b + 512), form a complete subtree whose levels 2..10 the NEXT
-// launch builds (k_struct_lock<true>); d_levels holds level k (2..10) of
-// subtree b at node offset 511 nfull - (1024 >> (k - 2)) nfull + (512 >>
-// (k - 1)) b, i.e. the levels back to back, level 10 last with room for the
-// ragged last subtree's node after the nfull complete ones.
-constexpr uint64_t kPipeSub = 512;  // level-1 nodes per workgroup (4 groups x 1024 records / 8)
-uint64_t pipe_nfull(uint64_t n) { return ceil_div(n, 8) / kPipeSub; }
-uint64_t pipe_level_off(uint64_t nfull, uint32_t k) {  // nodes before level k
-    uint64_t off = 0;
-    for (uint32_t j = 2; j < k; ++j) off += (kPipeSub >> (j - 1)) * nfull;
-    return off;
-}
+// Workgroup b of the pipelined launch writes the level-1 nodes [sub b, sub b +
+// sub) of each tree -- sub = 512 for the registry (4 groups x 1024 records /
+// 8), 128 for the second list (the balances) -- a complete subtree whose
+// levels 2..K the NEXT launch builds in its slots (k_struct_lock<true>): K =
+// 10 for the registry (1 node per subtree), 4 for the second list (16).  A
+// levels buffer holds level k (2..K) of subtree b at node offset
+// level_off(k) + (sub >> (k - 1)) b, the levels back to back, level K last
+// with room after the nfull complete subtrees' nodes for the ragged last
+// subtree's (its level-1 nodes reduced on the finisher's stream).
+struct PipeTree {
+    uint64_t sub;   // level-1 nodes per subtree
+    uint32_t K;     // the highest level the slots build
+    uint64_t c1;    // level-1 nodes of the whole tree
+    uint64_t nfull() const { return c1 / sub; }
+    uint64_t per_top() const { return sub >> (K - 1); }
+    uint64_t level_off(uint32_t k) const {  // nodes before level k
+        uint64_t off = 0;
+        for (uint32_t j = 2; j < k; ++j) off += (sub >> (j - 1)) * nfull();
+        return off;
+    }
+    uint64_t levels_bytes() const { return 32 * (level_off(K + 1) + per_top()); }
+};
+PipeTree pipe_reg(uint64_t n) { return {512, 10, ceil_div(n, 8)}; }
+PipeTree pipe_val(uint64_t nvalues, uint32_t value_len) { return {128, 4, ceil_div(nvalues * value_len, 256)}; }
 bool struct_pipe_ok(const void* d_rec, uint64_t n, const mk::StructSpec& sp, hipStream_t st) {
-    return struct_win_ok(d_rec, n, sp) && struct_gpw(n, st) == 4 && pipe_nfull(n) >= 1;
+    return struct_win_ok(d_rec, n, sp) && struct_gpw(n, st) == 4 && pipe_reg(n).nfull() >= 1;
 }
 
 int mk_ssz_struct_pipe_ok(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
@@ -1985,75 +1996,105 @@ int mk_ssz_struct_pipe_ok(const void* d_records, uint64_t n, uint32_t record_len
     return S.done(struct_pipe_ok(d_records, n, sp, (hipStream_t)stream) ? 1 : 0);
 }
 
-uint64_t mk_ssz_struct_pipe_levels_bytes(uint64_t n) {
-    return 32 * (pipe_level_off(pipe_nfull(n), 11) + 1);
+uint64_t mk_ssz_struct_pipe_levels_bytes(uint64_t n, uint64_t nvalues, uint32_t value_len, uint32_t which) {
+    if (which > 1 || (which == 1 && (value_len == 0 || nvalues == 0))) return 0;
+    return which ? pipe_val(nvalues, value_len).levels_bytes() : pipe_reg(n).levels_bytes();
 }
 
-uint64_t mk_ssz_struct_pipe_top_workspace_bytes(uint64_t n) {
-    Scope S(nullptr, false);
-    const uint64_t nfull = pipe_nfull(n), rag = ceil_div(n, 8) - kPipeSub * nfull;
-    uint64_t ws = std::max<uint64_t>(256, finish_ws_bytes(nfull + 1));
+static uint64_t pipe_top_ws(const PipeTree& t) {
+    const uint64_t rag = t.c1 - t.sub * t.nfull();
+    uint64_t ws = std::max<uint64_t>(256, finish_ws_bytes(t.nfull() * t.per_top() + t.per_top()));
     Plan p;
-    if (rag && mk::make_plan(rag, 32, true, 9, true, true, p, true, 0) == MK_OK)
+    if (rag && mk::make_plan(rag, 32, true, 63 - __builtin_clzll(t.sub), true, true, p, true,
+                             63 - __builtin_clzll(t.per_top())) == MK_OK)
         ws = std::max<uint64_t>(ws, mk::plan_ws_bytes(p));
     return ws;
+}
+
+uint64_t mk_ssz_struct_pipe_top_workspace_bytes(uint64_t n, uint64_t nvalues, uint32_t value_len, uint32_t which) {
+    Scope S(nullptr, false);
+    if (which > 1 || (which == 1 && (value_len == 0 || nvalues == 0))) return 0;
+    return pipe_top_ws(which ? pipe_val(nvalues, value_len) : pipe_reg(n));
 }
 
 int mk_dev_ssz_struct_list_level1_pipe(mk_call* call, const void* d_records, uint64_t n, uint32_t record_len,
                                        const mk_field* fields, uint32_t nfields, void* d_roots, void* d_nodes,
                                        const void* d_values, uint64_t nvalues, uint32_t value_len,
                                        void* d_value_nodes, const void* d_prev_nodes, void* d_prev_levels,
-                                       void* stream) {
+                                       const void* d_prev_value_nodes, void* d_prev_value_levels, void* stream) {
     Scope S(call);
     int rc = bind_stream((hipStream_t)stream);
     if (rc) return S.done(rc);
     mk::StructSpec sp;
     rc = make_spec(fields, nfields, record_len, sp);
     if (rc) return S.done(rc);
-    if (!d_records || !d_roots || !d_nodes || (d_prev_nodes && !d_prev_levels))
+    if (!d_records || !d_roots || !d_nodes || (d_prev_nodes && !d_prev_levels) ||
+        (d_prev_value_nodes && !d_prev_value_levels))
         return S.done(fail(MK_EINVAL, "null pointer"));
     if (!struct_pipe_ok(d_records, n, sp, (hipStream_t)stream))
         return S.done(fail(MK_EINVAL, "pipelined struct launch needs ValidatorRecords at a 16-B aligned address, "
                                       "4 groups of 1024 per workgroup (n = %llu)", (unsigned long long)n));
-    if (d_prev_nodes == d_nodes) return S.done(fail(MK_EINVAL, "the previous state's nodes alias this state's"));
+    if (d_prev_nodes && d_prev_nodes == d_nodes)
+        return S.done(fail(MK_EINVAL, "the previous state's nodes alias this state's"));
+    const uint64_t grid = ceil_div(ceil_div(n, mk::kLockThreads), 4);
     if (nvalues) {
         if (!d_values || !d_value_nodes) return S.done(fail(MK_EINVAL, "null pointer"));
         if (value_len % 8 || value_len == 0 || 128 % value_len || ((uintptr_t)d_values % 16))
             return S.done(fail(MK_EINVAL, "second list: items of 8, 16, 32, 64 or 128 B at a 16-B aligned address"));
         if (nvalues * value_len <= 128)
             return S.done(fail(MK_EINVAL, "second list of one chunk has no level-1 window"));
+        if (pipe_val(nvalues, value_len).c1 > 128 * grid)
+            return S.done(fail(MK_EINVAL, "second list longer than 128 windows per workgroup"));
+        if (d_prev_value_nodes && d_prev_value_nodes == d_value_nodes)
+            return S.done(fail(MK_EINVAL, "the previous state's second-list nodes alias this state's"));
+    } else if (d_prev_value_nodes) {
+        return S.done(fail(MK_EINVAL, "previous second list without this state's"));
     }
+    const PipeTree reg = pipe_reg(n), val = pipe_val(nvalues, value_len);
     mk::StructPrev prev{};
-    prev.nfull = (uint32_t)pipe_nfull(n);
+    prev.nfull = (uint32_t)reg.nfull();
     prev.live = d_prev_nodes ? 1u : 0u;
     prev.l1 = (const uint4*)d_prev_nodes;
     for (uint32_t k = 2; k <= 10; ++k)
-        prev.lv[k - 2] = d_prev_levels ? (uint4*)d_prev_levels + 2 * pipe_level_off(prev.nfull, k) : nullptr;
+        prev.lv[k - 2] = d_prev_levels ? (uint4*)d_prev_levels + 2 * reg.level_off(k) : nullptr;
+    // the second list's slots (waves 13-15) only with a previous second list
+    prev.nvfull = d_prev_value_nodes ? (uint32_t)val.nfull() : 0u;
+    prev.v1 = (const uint4*)d_prev_value_nodes;
+    for (uint32_t k = 2; k <= 4; ++k)
+        prev.vlv[k - 2] = d_prev_value_levels ? (uint4*)d_prev_value_levels + 2 * val.level_off(k) : nullptr;
     return S.done(dev_struct_level1(d_records, n, d_roots, d_nodes, (hipStream_t)stream, d_values,
                                     nvalues * (uint64_t)value_len, d_value_nodes, &prev));
 }
 
-int mk_dev_ssz_struct_pipe_top(mk_call* call, const void* d_nodes, uint64_t n, void* d_levels, void* d_pair_block,
-                               uint32_t slot, uint32_t epoch, void* d_ws, uint64_t ws_bytes, void* stream) {
+int mk_dev_ssz_struct_pipe_top(mk_call* call, const void* d_nodes, uint64_t n, uint64_t nvalues,
+                               uint32_t value_len, uint32_t which, void* d_levels, void* d_pair_block, uint32_t slot,
+                               uint32_t epoch, void* d_ws, uint64_t ws_bytes, void* stream) {
     Scope S(call);
     int rc = bind_stream((hipStream_t)stream);
     if (rc) return S.done(rc);
     if (!d_nodes || !d_levels || !d_pair_block) return S.done(fail(MK_EINVAL, "null pointer"));
+    if (which > 1 || (which == 1 && (value_len == 0 || nvalues == 0)))
+        return S.done(fail(MK_EINVAL, "tree %u: 0 = the registry, 1 = a non-empty second list", which));
     if (slot > 1) return S.done(fail(MK_EINVAL, "pair slot %u out of range (0..1)", slot));
     if (epoch == 0 || epoch >= (1u << 30)) return S.done(fail(MK_EINVAL, "pair epoch %u out of range (1..2^30-1)", epoch));
     if ((uintptr_t)d_pair_block % 16) return S.done(fail(MK_EINVAL, "pair block not 16-B aligned"));
-    const uint64_t nfull = pipe_nfull(n), c1 = ceil_div(n, 8), rag = c1 - kPipeSub * nfull;
-    if (nfull == 0) return S.done(fail(MK_EINVAL, "no complete subtree (n = %llu)", (unsigned long long)n));
-    uint8_t* top = (uint8_t*)d_levels + 32 * pipe_level_off(nfull, 10);  // level 10: nfull (+1) nodes
-    if (rag) {  // the ragged last subtree from level 1 to level 10, the odd rule at every level (pad_at_one)
+    const PipeTree t = which ? pipe_val(nvalues, value_len) : pipe_reg(n);
+    const uint64_t nfull = t.nfull(), rag = t.c1 - t.sub * nfull;
+    if (nfull == 0) return S.done(fail(MK_EINVAL, "no complete subtree"));
+    if (ws_bytes < pipe_top_ws(t)) return S.done(fail(MK_ENOMEM, "workspace too small"));
+    uint8_t* top = (uint8_t*)d_levels + 32 * t.level_off(t.K);  // level K: per_top nodes per subtree
+    uint64_t count = nfull * t.per_top();
+    if (rag) {  // the ragged last subtree from level 1 to level K, the odd rule at every level (pad_at_one)
         Plan p;
-        rc = mk::make_plan(rag, 32, true, 9, true, ((uintptr_t)d_nodes % 16) == 0, p, true, 0);
+        const uint32_t h = 63 - __builtin_clzll(t.sub), f = 63 - __builtin_clzll(t.per_top());
+        rc = mk::make_plan(rag, 32, true, h, true, ((uintptr_t)d_nodes % 16) == 0, p, true, f);
         if (rc) return S.done(rc);
-        rc = launch_plan(p, (const uint8_t*)d_nodes + 32 * kPipeSub * nfull, top + 32 * nfull, (uint8_t*)d_ws,
+        rc = launch_plan(p, (const uint8_t*)d_nodes + 32 * t.sub * nfull, top + 32 * count, (uint8_t*)d_ws,
                          ws_bytes, (hipStream_t)stream);
         if (rc) return S.done(rc);
+        count += f ? p.out_nodes : 1;
     }
-    return S.done(dev_finish_nodes(top, nfull + (rag ? 1 : 0), n, nullptr, d_ws, ws_bytes, (hipStream_t)stream,
+    return S.done(dev_finish_nodes(top, count, which ? nvalues : n, nullptr, d_ws, ws_bytes, (hipStream_t)stream,
                                    d_pair_block, slot, epoch));
 }
 

@@ -1871,8 +1871,10 @@ __device__ constexpr uint32_t kValLen[9] = {48, 32, 32, 8, 8, 8, 8, 8, 8};
 // node permutations -- and writes its level-10 node, so what is left of that
 // tree is a 245-node top.  Each wave does ONE of them as an extra lock-step
 // permutation (level 2 on waves 0-3, 3 on 4-5, then levels 4..10 on waves
-// 6..12, one node per lane; waves 13-15 a discarded one), so every wave runs
-// 21 permutations and the same barriers.  Level k sits before the field
+// 6..12, one node per lane), so every wave runs 21 permutations and the
+// same barriers; waves 13-15 take levels 2, 3, 4 of the previous state's
+// second list (the balances: 128 windows per workgroup, 64 + 32 + 16 node
+// permutations), leaving 16 nodes per workgroup.  Level k sits before the field
 // permutation at position 2 (k - 2) of the 16 (4 groups x f0, f1, f2, s1);
 // level 10 at position 15 (before the last struct message): the writer
 // waits for its store in the middle of the field permutation that follows,
@@ -1890,17 +1892,23 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint32_t* Bw = buf[wave];
     const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
-    // the previous state's level this wave builds (2..10; 11 = a discarded
-    // permutation on waves 13-15) and its slot position
-    const uint32_t my_level = wv < 4 ? 2u : wv < 6 ? 3u : wv < 13 ? wv - 2u : 11u;
-    auto prev_slot = [&](uint32_t k) {
-        const uint32_t w0 = k == 2 ? 0u : k == 3 ? 4u : k + 2u;  // first wave of level k
-        const uint32_t per = k <= 10 ? 512u >> (k - 1) : 0u;     // level-k nodes per subtree
+    // this wave's slot: the registry's level my_k (waves 0-12: 2 on 0-3, 3 on
+    // 4-5, 4..10 on 6..12) or the second list's (waves 13-15: levels 2, 3,
+    // 4), at position my_pos (2 (k - 2); the registry's level 10 at 15)
+    const bool my_val = wv >= 13;
+    const uint32_t my_k = my_val ? wv - 11u : wv < 4 ? 2u : wv < 6 ? 3u : wv - 2u;
+    const uint32_t my_pos = my_k == 10 ? 15u : 2u * (my_k - 2u);
+    auto prev_slot = [&] {
+        const uint32_t k = my_k;
+        const uint32_t sub = my_val ? 128u : 512u;                           // level-1 nodes per subtree
+        const uint32_t w0 = my_val ? wv : k == 2 ? 0u : k == 3 ? 4u : k + 2u;  // first wave of level k
+        const uint32_t per = sub >> (k - 1);                                 // level-k nodes per subtree
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));  // computed here, not hoisted and kept live across the loop
         const uint32_t j = 64u * (wv - w0) + ln;
-        const bool act = prev.live && blockIdx.x < prev.nfull && j < per;
-        const uint4* src = k == 2 ? prev.l1 + 2 * (512u * blockIdx.x) : prev.lv[k <= 10 ? k - 3 : 0] + 4 * (per * blockIdx.x);
+        const bool act = prev.live && blockIdx.x < (my_val ? prev.nvfull : prev.nfull) && j < per;
+        const uint4* src = k == 2 ? (my_val ? prev.v1 : prev.l1) + 2 * (sub * blockIdx.x)
+                                  : (my_val ? prev.vlv[k - 3] : prev.lv[k - 3]) + 4 * (per * blockIdx.x);
         asm volatile("" ::: "memory");
         State s;
 #pragma unroll
@@ -1919,7 +1927,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
         if (act) {
             uint4 d0, d1;
             digest(s, d0, d1);
-            uint4* dst = prev.lv[k - 2] + 2 * (per * blockIdx.x + j);
+            uint4* dst = (my_val ? prev.vlv[k - 2] : prev.lv[k - 2]) + 2 * (per * blockIdx.x + j);
             dst[0] = d0;
             dst[1] = d1;
         }
@@ -1963,8 +1971,8 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
 #pragma unroll
         for (int f = 0; f < 3; ++f) {  // Keccak(le32(len) || bytes), one block
             // this wave's slot of the previous state's tree (f = 0, 2 only: positions 2 (k - 2))
-            const bool slot_here = slots && (f == 0 || f == 2) && my_level <= 10 && 2u * (my_level - 2u) == pos0 + f;
-            if (slot_here) prev_slot(my_level);
+            const bool slot_here = slots && (f == 0 || f == 2) && my_pos == pos0 + f;
+            if (slot_here) prev_slot();
             const uint32_t len = kValLen[f], off = kValOff[f] / 4, nd = len / 4 + 1;
             State s;
 #pragma unroll
@@ -1992,10 +2000,10 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
             R[off + 0] = s.lo[0]; R[off + 1] = s.hi[0]; R[off + 2] = s.lo[1]; R[off + 3] = s.hi[1];
             R[off + 4] = s.lo[2]; R[off + 5] = s.hi[2]; R[off + 6] = s.lo[3]; R[off + 7] = s.hi[3];
         }
-        // level 10 (wave 12; waves 13-15 discard theirs) before the last
-        // group's struct message: it reads level 9, whose writer waited in the
-        // field-2 permutation just before; nothing in this launch reads it
-        if (slots && my_level >= 10 && pos0 == 12u) prev_slot(my_level);
+        // the registry's level 10 (wave 12) before the last group's struct
+        // message: it reads level 9, whose writer waited in the field-2
+        // permutation just before; nothing in this launch reads it
+        if (slots && my_pos == 15u && pos0 == 12u) prev_slot();
         // struct message (hash.go:141-159): the digests of fields 0..2, then
         // the six uint64 raw: 36 dwords = block 1 (34) + 2 dwords of block 2
         State s;
@@ -2037,7 +2045,10 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     __syncthreads();
     const uint64_t r0 = g_begin * kLockThreads, r1 = g_end * kLockThreads < n ? g_end * kLockThreads : n;
     const uint64_t w0 = r0 / 8, nw = (r1 - r0 + 7) / 8;
-    const uint64_t vw_total = (vbytes + 255) / 256, vpw = (vw_total + gridDim.x - 1) / gridDim.x;
+    // PREV: 128 windows per workgroup (the subtrees the next launch's slots
+    // take; 128 >= ceil(vw_total / grid) for the State's 8-B balances)
+    const uint64_t vw_total = (vbytes + 255) / 256;
+    const uint64_t vpw = PREV && gpw == 4 ? 128u : (vw_total + gridDim.x - 1) / gridDim.x;
     const uint64_t v0 = (uint64_t)blockIdx.x * vpw;
     const uint64_t nv = vals && v0 < vw_total ? (vw_total - v0 < vpw ? vw_total - v0 : vpw) : 0;
 #pragma unroll 1

@@ -48,13 +48,17 @@ __global__ void k_struct_reg(const uint8_t* rec, uint64_t n, StructSpec sp, uint
 // gpw > 0: contiguous groups per workgroup plus the level-1 windows of the roots' merkleHash
 // (and of a second list of vbytes bytes at vals, when vals != nullptr)
 // PREV (a stream of states, gpw == 4): the same launch also builds levels
-// 2..10 of the PREVIOUS state's registry tree over its level-1 windows, one
-// extra lock-step permutation per wave (see the kernel); workgroups b <
-// nfull each take the complete 512-window subtree [512 b, 512 b + 512).
+// 2..10 of the PREVIOUS state's registry tree over its level-1 windows and
+// levels 2..4 of its second list's, one extra lock-step permutation per wave
+// (see the kernel); workgroup b < nfull takes the complete 512-window
+// registry subtree [512 b, 512 b + 512), b < nvfull the 128-window one.
 struct StructPrev {
     const uint4* l1;   // the previous state's level-1 windows (complete)
     uint4* lv[9];      // its levels 2..10: level k node j of subtree b at lv[k - 2][(512 >> (k - 1)) b + j]
-    uint32_t nfull;    // subtrees (workgroups) with all 512 windows
+    const uint4* v1;   // the previous state's second-list level-1 windows (128 per workgroup)
+    uint4* vlv[3];     // its levels 2..4: level k node j of subtree b at vlv[k - 2][(128 >> (k - 1)) b + j]
+    uint32_t nfull;    // registry subtrees (workgroups) with all 512 windows
+    uint32_t nvfull;   // second-list subtrees with all 128 windows
     uint32_t live;     // 0: no previous state (the slots hash zeros, store nothing)
 };
 template <bool PREV>

@@ -120,21 +120,25 @@ def struct_pipe_ok(records: torch.Tensor, n: int, record_len: int, spec) -> bool
                                                   _stream(records.device)))
 
 
-def struct_pipe_levels_bytes(n: int) -> int:
-    return int(_lib.load().mk_ssz_struct_pipe_levels_bytes(n))
+def struct_pipe_levels_bytes(n: int, nvalues: int = 0, value_len: int = 8, which: int = 0) -> int:
+    """Bytes of one tree's slot-levels buffer (which 0: the registry of n
+    records, 1: the second list of nvalues x value_len)."""
+    return int(_lib.load().mk_ssz_struct_pipe_levels_bytes(n, nvalues, value_len, which))
 
 
-def struct_pipe_top_workspace(n: int, device) -> torch.Tensor:
-    return torch.empty(max(256, int(_lib.load().mk_ssz_struct_pipe_top_workspace_bytes(n))), dtype=torch.uint8,
-                       device=device)
+def struct_pipe_top_workspace(n: int, device, nvalues: int = 0, value_len: int = 8, which: int = 0) -> torch.Tensor:
+    nb = int(_lib.load().mk_ssz_struct_pipe_top_workspace_bytes(n, nvalues, value_len, which))
+    return torch.empty(max(256, nb), dtype=torch.uint8, device=device)
 
 
 def struct_list_level1_pipe(records: torch.Tensor, n: int, record_len: int, spec, roots: torch.Tensor,
                             nodes: torch.Tensor, prev_nodes, prev_levels, values: torch.Tensor = None,
-                            nvalues: int = 0, value_len: int = 8, value_nodes: torch.Tensor = None) -> torch.Tensor:
+                            nvalues: int = 0, value_len: int = 8, value_nodes: torch.Tensor = None,
+                            prev_value_nodes=None, prev_value_levels=None) -> torch.Tensor:
     """struct_list_level1, and in the same launch levels 2..10 of the
     PREVIOUS state's registry tree (its level-1 ``prev_nodes``; None for the
-    first state) into ``prev_levels`` (struct_pipe_levels_bytes(n))."""
+    first state) into ``prev_levels`` and levels 2..4 of its second list's
+    tree (``prev_value_nodes``) into ``prev_value_levels``."""
     from .registry import _fields
 
     if roots.numel() < 32 * n or nodes.numel() < 32 * -(-n // 8):
@@ -145,22 +149,28 @@ def struct_list_level1_pipe(records: torch.Tensor, n: int, record_len: int, spec
     if nvalues and (values is None or value_nodes is None or
                     value_nodes.numel() < 32 * -(-nvalues * value_len // 256)):
         raise ValueError("second list: values / value_nodes missing or too small")
+    if prev_value_nodes is not None and (
+            prev_value_levels is None or
+            prev_value_levels.numel() < struct_pipe_levels_bytes(n, nvalues, value_len, 1)):
+        raise ValueError("previous state's second-list levels buffer too small")
+    vp = lambda t: _p(t) if t is not None else None  # noqa: E731
     _lib.invoke("mk_dev_ssz_struct_list_level1_pipe", _p(records), n, record_len, _fields(spec), len(spec),
-                _p(roots), _p(nodes), _p(values) if nvalues else None, nvalues, value_len,
-                _p(value_nodes) if nvalues else None, _p(prev_nodes) if prev_nodes is not None else None,
-                _p(prev_levels) if prev_nodes is not None else None, _stream(records.device), device=_dev(records))
+                _p(roots), _p(nodes), vp(values) if nvalues else None, nvalues, value_len,
+                vp(value_nodes) if nvalues else None, vp(prev_nodes), vp(prev_levels) if prev_nodes is not None else None,
+                vp(prev_value_nodes), vp(prev_value_levels) if prev_value_nodes is not None else None,
+                _stream(records.device), device=_dev(records))
     return nodes
 
 
 def struct_pipe_top(nodes: torch.Tensor, n: int, levels: torch.Tensor, pair_block: torch.Tensor, slot: int,
-                    epoch: int, ws: torch.Tensor) -> None:
-    """The registry root of a state whose levels 2..10 the next pipelined
-    launch built, into slot ``slot`` of a pair block (merkle_finish_nodes_pair
-    semantics)."""
+                    epoch: int, ws: torch.Tensor, nvalues: int = 0, value_len: int = 8, which: int = 0) -> None:
+    """One tree's root of a state whose slot levels the next pipelined launch
+    built (which 0: the registry, 1: the second list), into slot ``slot`` of a
+    pair block (merkle_finish_nodes_pair semantics)."""
     if pair_block.numel() < 128:
         raise ValueError("pair block of 128 bytes")
-    _lib.invoke("mk_dev_ssz_struct_pipe_top", _p(nodes), n, _p(levels), _p(pair_block), slot, epoch, _p(ws),
-                ws.numel(), _stream(nodes.device), device=_dev(nodes))
+    _lib.invoke("mk_dev_ssz_struct_pipe_top", _p(nodes), n, nvalues, value_len, which, _p(levels), _p(pair_block),
+                slot, epoch, _p(ws), ws.numel(), _stream(nodes.device), device=_dev(nodes))
 
 
 def merkle_workspace(n: int, item_len: int, device) -> torch.Tensor:

@@ -248,22 +248,23 @@ class DeviceStateHasher:
 class StatePipeline:
     """TreeHash of a stream of States{ValidatorRegistry, ValidatorBalances}
     (BASELINE config 3, one state per ``submit``; hash.go:118-159) with each
-    state's registry tree folded into the NEXT state's struct launch.
+    state's two trees folded into the NEXT state's struct launch.
 
     State i's launch (mk_dev_ssz_struct_list_level1_pipe) writes its struct
-    roots, both trees' level-1 nodes, and levels 2..10 of state i-1's
-    registry tree in one extra lock-step permutation per wave (DESIGN.md
-    §4.3).  Beside state i+1's launch, on the CUs its grid leaves free: state
-    i's balances tree (level 2 up) on one high-priority side stream, state
-    i-1's registry top (the ragged last subtree and ~245 nodes) on another;
-    whichever finishes second hashes the state root into the state's pair
-    block.  **A state's root is therefore written one submit later**: the
-    tensor ``submit`` returns is produced once the next ``submit`` or
-    ``flush()`` has been called and the side streams have run (synchronise,
-    or ``wait()``).  Four buffer sets rotate; a root stays valid for the next
-    two submits after it is produced.  Takes what mk_ssz_struct_pipe_ok
-    accepts (ValidatorRecords at a 16-B aligned address, 16-B aligned
-    balances, 3 x 2^18 < n <= 2^20 on 256 CUs); ValueError otherwise."""
+    roots and both trees' level-1 nodes, and in one extra lock-step
+    permutation per wave levels 2..10 of state i-1's registry tree and levels
+    2..4 of its balances tree.  Beside state i+1's launch, on
+    the CUs its grid leaves free, two high-priority side streams finish state
+    i-1's trees (the ragged last subtrees, the ~245-node registry top, the
+    ~3,900-node balances top); whichever finishes second hashes the state
+    root into the state's pair block.  **A state's root is therefore written
+    one submit later**: the tensor ``submit`` returns is produced once the
+    next ``submit`` or ``flush()`` has been called and the side streams have
+    run (synchronise, or ``wait()``).  Four buffer sets rotate; a root stays
+    valid for the next two submits after it is produced.  Takes what
+    mk_ssz_struct_pipe_ok accepts (ValidatorRecords at a 16-B aligned
+    address, 16-B aligned balances, 3 x 2^18 < n <= 2^20 on 256 CUs);
+    ValueError otherwise."""
 
     SETS = 4
 
@@ -280,17 +281,19 @@ class StatePipeline:
         self.nodes = [mk(32 * self.c1) for _ in range(self.SETS)]
         self.bnodes = [mk(32 * self.cb1) for _ in range(self.SETS)]
         self.levels = [mk(D.struct_pipe_levels_bytes(n)) for _ in range(self.SETS)]
+        self.blevels = [mk(D.struct_pipe_levels_bytes(n, n, 8, 1)) for _ in range(self.SETS)]
         self.pairs = [torch.zeros(128, dtype=torch.uint8, device=self.dev) for _ in range(self.SETS)]
         self.epochs = [0] * self.SETS
         self.top_ws = D.struct_pipe_top_workspace(n, self.dev)
-        self.bal_ws = D.finish_workspace(self.cb1, self.dev)
+        self.btop_ws = D.struct_pipe_top_workspace(n, self.dev, n, 8, 1)
         self.flush_ws = D.finish_workspace(self.c1, self.dev)
-        # high priority: each its own hardware queue
+        self.bflush_ws = D.finish_workspace(self.cb1, self.dev)
+        # high priority: each its own hardware queue where the runtime has one
         self.reg_side = torch.cuda.Stream(device=self.dev, priority=-1)
         self.bal_side = torch.cuda.Stream(device=self.dev, priority=-1)
         self._i = 0
-        self._pending = None  # the set of the state whose registry levels 2.. are not built yet
-        self._done = {}       # state index -> (registry top event, balances event)
+        self._pending = None  # the set of the state whose trees' slot levels are not built yet
+        self._done = {}       # state index -> (registry top event, balances top event)
 
     def submit(self, records, balances):
         """records: (n*160,) uint8 device tensor; balances: (n*8,) uint8, both
@@ -310,59 +313,61 @@ class StatePipeline:
         s = i % self.SETS
         self._i += 1
         # set s was last used by state i - 4, set (i + 1) % 4 by state i - 3: one
-        # wait every second submit on state i - 3's side work covers both (each
-        # side stream runs in order); it ran beside launch i - 1
+        # wait every second submit on state i - 3's tops covers both (each side
+        # stream runs in order); they ran beside launch i - 1
         if i % 2 == 0:
             for ev in self._done.get(i - self.SETS + 1, ()):
-                if ev is not None:
-                    cur.wait_event(ev)
+                cur.wait_event(ev)
         self._done.pop(i - self.SETS - 1, None)
         prev = self._pending
+        p = prev is not None
         D.struct_list_level1_pipe(records, n, 160, VALIDATOR_FIELDS, self.roots, self.nodes[s],
-                                  self.nodes[prev] if prev is not None else None,
-                                  self.levels[prev] if prev is not None else None,
-                                  values=balances, nvalues=n, value_len=8, value_nodes=self.bnodes[s])
-        k_ev = torch.cuda.Event()
-        k_ev.record(cur)
-        balances.record_stream(self.bal_side)
+                                  self.nodes[prev] if p else None, self.levels[prev] if p else None,
+                                  values=balances, nvalues=n, value_len=8, value_nodes=self.bnodes[s],
+                                  prev_value_nodes=self.bnodes[prev] if p else None,
+                                  prev_value_levels=self.blevels[prev] if p else None)
         self.epochs[s] = self.epochs[s] % ((1 << 30) - 1) + 1
-        self.bal_side.wait_event(k_ev)
-        with torch.cuda.stream(self.bal_side):  # state i's balances tree, beside launch i + 1
-            D.merkle_finish_nodes_pair(self.bnodes[s], self.cb1, n, self.pairs[s], 1, self.epochs[s], ws=self.bal_ws)
-            ev_b = torch.cuda.Event()
-            ev_b.record(self.bal_side)
-        self._done[i] = (None, ev_b)
-        if prev is not None:  # state i - 1's registry top: its levels 2..10 were built by launch i
-            self._reg_top(i - 1, prev, k_ev, pipelined=True)
+        if p:  # state i - 1's two tops: their slot levels were built by launch i
+            k_ev = torch.cuda.Event()
+            k_ev.record(cur)
+            self._tops(i - 1, prev, k_ev, pipelined=True)
         self._pending = s
         return self.pairs[s][64:96]
 
-    def _reg_top(self, state: int, s: int, after, pipelined: bool) -> None:
+    def _tops(self, state: int, s: int, after, pipelined: bool) -> None:
         import torch
 
         from . import device as D
 
-        self.reg_side.wait_event(after)
-        with torch.cuda.stream(self.reg_side):
-            if pipelined:
-                D.struct_pipe_top(self.nodes[s], self.n, self.levels[s], self.pairs[s], 0, self.epochs[s],
-                                  self.top_ws)
-            else:  # the last state: levels 2.. from its level-1 nodes
-                D.merkle_finish_nodes_pair(self.nodes[s], self.c1, self.n, self.pairs[s], 0, self.epochs[s],
-                                           ws=self.flush_ws)
-            ev = torch.cuda.Event()
-            ev.record(self.reg_side)
-        self._done[state] = (ev, self._done[state][1])
+        evs = []
+        for side, which in ((self.reg_side, 0), (self.bal_side, 1)):
+            side.wait_event(after)
+            with torch.cuda.stream(side):
+                if pipelined:
+                    D.struct_pipe_top(self.nodes[s] if which == 0 else self.bnodes[s], self.n,
+                                      self.levels[s] if which == 0 else self.blevels[s], self.pairs[s], which,
+                                      self.epochs[s], self.top_ws if which == 0 else self.btop_ws,
+                                      nvalues=self.n, value_len=8, which=which)
+                elif which == 0:  # the last state: each tree from its level-1 nodes
+                    D.merkle_finish_nodes_pair(self.nodes[s], self.c1, self.n, self.pairs[s], 0, self.epochs[s],
+                                               ws=self.flush_ws)
+                else:
+                    D.merkle_finish_nodes_pair(self.bnodes[s], self.cb1, self.n, self.pairs[s], 1, self.epochs[s],
+                                               ws=self.bflush_ws)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            evs.append(ev)
+        self._done[state] = tuple(evs)
 
     def flush(self) -> None:
-        """Finish the last submitted state's registry tree (its level-1 nodes
-        up, on the side stream); a no-op when nothing is pending."""
+        """Finish the last submitted state's trees (from their level-1 nodes,
+        on the side streams); a no-op when nothing is pending."""
         import torch
 
         if self._pending is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.dev))
-            self._reg_top(self._i - 1, self._pending, ev, pipelined=False)
+            self._tops(self._i - 1, self._pending, ev, pipelined=False)
             self._pending = None
 
     def wait(self, stream=None) -> None:

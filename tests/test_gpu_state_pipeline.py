@@ -91,9 +91,10 @@ def test_state_pipeline_golden_1m(gpu):
 
 
 def test_state_pipeline_slot_levels_vs_oracle(gpu):
-    """Levels 2..10 the second launch built for the first state, subtree by
-    subtree (first, middle, last complete one), against the oracle's node
-    hashes over the first launch's level-1 nodes."""
+    """The slot levels the second launch built for the first state -- the
+    registry's 2..10 and the balances' 2..4 -- subtree by subtree (first,
+    middle, last complete one), against the oracle's node hashes over the
+    first launch's level-1 nodes."""
     import torch
 
     from oracle import oracle as O
@@ -107,20 +108,22 @@ def test_state_pipeline_slot_levels_vs_oracle(gpu):
     p.flush()
     p.wait()
     torch.cuda.synchronize()
-    l1 = p.nodes[0].cpu().numpy()[:32 * p.c1].reshape(-1, 32)
-    lv = p.levels[0].cpu().numpy().reshape(-1, 32)
-    nfull = p.c1 // 512
-    offs, o = {}, 0
-    for k in range(2, 11):
-        offs[k] = o
-        o += (512 >> (k - 1)) * nfull
-    for b in (0, nfull // 2, nfull - 1):
-        level = [bytes(x) for x in l1[512 * b:512 * b + 512]]
-        for k in range(2, 11):
-            level = [O.keccak256(level[2 * j] + level[2 * j + 1]) for j in range(len(level) // 2)]
-            per = 512 >> (k - 1)
-            got = [bytes(x) for x in lv[offs[k] + per * b:offs[k] + per * b + per]]
-            assert got == level, (b, k)
+    for nodes, levels, c1, sub, top in ((p.nodes[0], p.levels[0], p.c1, 512, 10),
+                                        (p.bnodes[0], p.blevels[0], p.cb1, 128, 4)):
+        l1 = nodes.cpu().numpy()[:32 * c1].reshape(-1, 32)
+        lv = levels.cpu().numpy().reshape(-1, 32)
+        nfull = c1 // sub
+        offs, o = {}, 0
+        for k in range(2, top + 1):
+            offs[k] = o
+            o += (sub >> (k - 1)) * nfull
+        for b in (0, nfull // 2, nfull - 1):
+            level = [bytes(x) for x in l1[sub * b:sub * b + sub]]
+            for k in range(2, top + 1):
+                level = [O.keccak256(level[2 * j] + level[2 * j + 1]) for j in range(len(level) // 2)]
+                per = sub >> (k - 1)
+                got = [bytes(x) for x in lv[offs[k] + per * b:offs[k] + per * b + per]]
+                assert got == level, (sub, b, k)
 
 
 def test_state_pipeline_flush_mid_stream_and_refusals(gpu):
