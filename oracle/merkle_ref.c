@@ -23,7 +23,7 @@
  * Synthetic inputs: counter-based SplitMix64 — byte b of a
  * synthetic stream is byte (b % 8) (little-endian) of word b/8, word k =
  * mix(seed + k * 0x9E3779B97F4A7C15).  The HIP product generates the same
- * stream on the device (prysm_amd/csrc/synth.hip).
+ * stream on the device (k_synth in prysm_amd/csrc/merkle_kernels.hip).
  */
 #include <stdint.h>
 #include <stdlib.h>

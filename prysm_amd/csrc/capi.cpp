@@ -2002,6 +2002,7 @@ uint64_t mk_ssz_struct_pipe_levels_bytes(uint64_t n, uint64_t nvalues, uint32_t 
 }
 
 static uint64_t pipe_top_ws(const PipeTree& t) {
+    mk::WideWaves wide;  // the plans mk_dev_ssz_struct_pipe_top makes
     const uint64_t rag = t.c1 - t.sub * t.nfull();
     uint64_t ws = std::max<uint64_t>(256, finish_ws_bytes(t.nfull() * t.per_top() + t.per_top()));
     Plan p;
@@ -2081,6 +2082,7 @@ int mk_dev_ssz_struct_pipe_top(mk_call* call, const void* d_nodes, uint64_t n, u
     const PipeTree t = which ? pipe_val(nvalues, value_len) : pipe_reg(n);
     const uint64_t nfull = t.nfull(), rag = t.c1 - t.sub * nfull;
     if (nfull == 0) return S.done(fail(MK_EINVAL, "no complete subtree"));
+    mk::WideWaves wide;  // beside the next pipelined launch: whole-CU workgroups only
     if (ws_bytes < pipe_top_ws(t)) return S.done(fail(MK_ENOMEM, "workspace too small"));
     uint8_t* top = (uint8_t*)d_levels + 32 * t.level_off(t.K);  // level K: per_top nodes per subtree
     uint64_t count = nfull * t.per_top();

@@ -87,6 +87,10 @@ uint32_t levels_to_one(uint64_t count) {
 }
 
 // ---- merkleHash pass plan ---------------------------------------------------------
+thread_local bool t_wide_waves = false;
+WideWaves::WideWaves() : prev(t_wide_waves) { t_wide_waves = true; }
+WideWaves::~WideWaves() { t_wide_waves = prev; }
+
 int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool pad_at_one, bool aligned16, Plan& p,
               bool node_input, uint32_t frontier, uint64_t mixin_n, bool leaf_ni1) {
     p = Plan();
@@ -163,7 +167,7 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
             // per wave once a level has at most NT/64 parents, so 16 waves run
             // the last 4 levels and the mix-in in the spread form (one launch
             // to the root)
-            if (c1 <= kW3MaxNt / 2) nt = kW3MaxNt;
+            if (c1 <= kW3MaxNt / 2 || t_wide_waves) nt = kW3MaxNt;
         }
         // throughput pass: 2 window pairs per thread on wide passes, 1 on mid-size
         // leaf passes so they still spread over the CUs

@@ -34,6 +34,17 @@ uint32_t ilog2(uint64_t v);
 uint32_t levels_to_one(uint64_t count);  // hashing levels from `count` nodes to one
 
 // ---- merkleHash pass plan --------------------------------------------------
+// Plans made while a WideWaves is alive on this thread give every latency
+// (k_wave3) pass full 1024-thread workgroups: the finishers that run beside a
+// CU-filling phase-locked launch then only land on the CUs its grid leaves
+// free, instead of squeezing one-wave workgroups in beside its locked waves
+// (starved ~10x there).
+struct WideWaves {
+    WideWaves();
+    ~WideWaves();
+    bool prev;
+};
+
 struct Pass {
     bool leaf;
     bool wave;  // latency pass (k_wave*) instead of the throughput pass (k_reduce)
