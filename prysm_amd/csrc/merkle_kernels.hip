@@ -1330,6 +1330,13 @@ template __global__ void k_wave3<256, true>(ReduceArgs);
 template __global__ void k_wave3<512, true>(ReduceArgs);
 template __global__ void k_wave3<1024, true>(ReduceArgs);
 
+// Wave priority of the trie's latency-bound top kernels (s_setprio): they run
+// beside a phase-locked front at one wave per SIMD (the pipelined C5 stream),
+// where the locked waves otherwise take most of the issue slots and the top's
+// dependent chain, not the front, sets the step.  0: default.
+#ifndef MK_TRIE_TOP_PRIO
+#define MK_TRIE_TOP_PRIO 0
+#endif
 // Narrow top of the deposit trie, bit-interleaved lane pairs (mk::ilv): the
 // workgroup owns NT input nodes of level d (NT/2 lane pairs) and writes
 // `levels` levels to the (plain) level array; once the count is 1 it goes on
@@ -1339,6 +1346,7 @@ template __global__ void k_wave3<1024, true>(ReduceArgs);
 template <uint32_t NT>
 __global__ __launch_bounds__(NT) void k_trie_top3(const uint32_t* __restrict__ in, uint64_t cin,
                                                   uint32_t* __restrict__ lv_out, uint32_t levels, uint64_t capn) {
+    if constexpr (MK_TRIE_TOP_PRIO > 0) __builtin_amdgcn_s_setprio(MK_TRIE_TOP_PRIO);
     constexpr uint32_t kPairs = NT / 2;
     __shared__ uint32_t lds[8 * kPairs];
     const uint32_t tid = threadIdx.x, k = tid >> 1, p = tid & 1u;
@@ -2679,6 +2687,7 @@ template <uint32_t NW>
 __global__ __launch_bounds__(64 * NW) void k_trie_spread(uint32_t* __restrict__ levels, uint64_t cap, uint32_t d0,
                                                          uint64_t lo, uint64_t c, uint32_t d_end, uint32_t depth,
                                                          uint32_t* __restrict__ root_out, SpreadLeaves lv) {
+    if constexpr (MK_TRIE_TOP_PRIO > 0) __builtin_amdgcn_s_setprio(MK_TRIE_TOP_PRIO);
     __shared__ uint2 lds[2][4 * NW];
     const uint32_t w = threadIdx.x >> 6, L = threadIdx.x & 63u;
     const spread::LaneLH cst = spread::lane_consts_lh(L);
