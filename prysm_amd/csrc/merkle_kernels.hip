@@ -1333,9 +1333,12 @@ template __global__ void k_wave3<1024, true>(ReduceArgs);
 // Wave priority of the trie's latency-bound top kernels (s_setprio): they run
 // beside a phase-locked front at one wave per SIMD (the pipelined C5 stream),
 // where the locked waves otherwise take most of the issue slots and the top's
-// dependent chain, not the front, sets the step.  0: default.
+// dependent chain, not the front, sets the step.  One
+// process A/B (profiles/r05/c5_front_ab/ab_knobs.txt): the pipelined stream
+// 0.4386 -> 0.4231 ms/step at priority 1 (0.4239 at 3); 0 = the default
+// wave priority.
 #ifndef MK_TRIE_TOP_PRIO
-#define MK_TRIE_TOP_PRIO 0
+#define MK_TRIE_TOP_PRIO 1
 #endif
 // Narrow top of the deposit trie, bit-interleaved lane pairs (mk::ilv): the
 // workgroup owns NT input nodes of level d (NT/2 lane pairs) and writes
