@@ -254,12 +254,12 @@ class StatePipeline:
     roots and both trees' level-1 nodes, and in one extra lock-step
     permutation per wave levels 2..10 of state i-1's registry tree and levels
     2..4 of its balances tree.  Beside state i+1's launch, on
-    the CUs its grid leaves free, two high-priority side streams finish state
-    i-1's trees (the ragged last subtrees, the ~245-node registry top, the
-    ~3,900-node balances top); whichever finishes second hashes the state
-    root into the state's pair block.  **A state's root is therefore written
+    the CUs its grid leaves free, one high-priority side stream finishes
+    state i-1's trees in turn (the ragged last subtrees, the ~245-node
+    registry top, the ~3,900-node balances top); the second of the two tops
+    hashes the state root into the state's pair block.  **A state's root is therefore written
     one submit later**: the tensor ``submit`` returns is produced once the
-    next ``submit`` or ``flush()`` has been called and the side streams have
+    next ``submit`` or ``flush()`` has been called and the side stream has
     run (synchronise, or ``wait()``).  Four buffer sets rotate; a root stays
     valid for the next two submits after it is produced.  Takes what
     mk_ssz_struct_pipe_ok accepts (ValidatorRecords at a 16-B aligned
@@ -288,9 +288,15 @@ class StatePipeline:
         self.btop_ws = D.struct_pipe_top_workspace(n, self.dev, n, 8, 1)
         self.flush_ws = D.finish_workspace(self.c1, self.dev)
         self.bflush_ws = D.finish_workspace(self.cb1, self.dev)
-        # high priority: each its own hardware queue where the runtime has one
-        self.reg_side = torch.cuda.Stream(device=self.dev, priority=-1)
-        self.bal_side = torch.cuda.Stream(device=self.dev, priority=-1)
+        # ONE high-priority side stream for both tops, in order: the 245-
+        # workgroup grid leaves 1-2 CUs free per XCD, and a kernel's first
+        # workgroup goes to the same XCD each time, so two tops launched side
+        # by side on two queues queue behind each other for that XCD's free
+        # CU, the second until the struct launch ends (0.53 vs 0.49 ms/step,
+        # profiles/r05/c3_stream/); in order, the chain (~250 us) fits
+        # beside the launch
+        self.side = torch.cuda.Stream(device=self.dev, priority=-1)
+        self.reg_side = self.bal_side = self.side
         self._i = 0
         self._pending = None  # the set of the state whose trees' slot levels are not built yet
         self._done = {}       # state index -> (registry top event, balances top event)
@@ -341,7 +347,8 @@ class StatePipeline:
 
         evs = []
         for side, which in ((self.reg_side, 0), (self.bal_side, 1)):
-            side.wait_event(after)
+            if which == 0 or side is not self.reg_side:
+                side.wait_event(after)
             with torch.cuda.stream(side):
                 if pipelined:
                     D.struct_pipe_top(self.nodes[s] if which == 0 else self.bnodes[s], self.n,
@@ -376,8 +383,7 @@ class StatePipeline:
         import torch
 
         st = stream or torch.cuda.current_stream(self.dev)
-        st.wait_stream(self.reg_side)
-        st.wait_stream(self.bal_side)
+        st.wait_stream(self.side)
 
 
 FAR_FUTURE_EPOCH = (1 << 64) - 1  # shared/params/config.go:118
