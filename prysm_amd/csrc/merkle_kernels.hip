@@ -2306,6 +2306,9 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 #ifndef MK_TRIE_LOCK_AUX
 #define MK_TRIE_LOCK_AUX 0  // global_load_lds policy of the deposit DMA (2 = nt)
 #endif
+#ifndef MK_TRIE_PROBE
+#define MK_TRIE_PROBE 0  // A/B probes only (wrong roots): 1 = no DMA staging, 2 = no LDS block reads
+#endif
 #ifndef MK_TRIE_DMA_ROUND
 // round of a block's permutation after which the next block's DMA goes out;
 // 12 (mid-permutation) over 0: one trie 1.2-2.3 % faster on two boxes, the
@@ -2339,6 +2342,7 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
     uint4* const lv[4] = {L0, L1, L2, L3};
     auto first = [&](uint64_t g) { return (g * NT + 64 * wave) * DPT; };  // lane 0's first deposit
     auto dma = [&](uint64_t g, int i, int b) {
+        if constexpr ((MK_TRIE_PROBE & 1) != 0) return;  // probe: no staging (wrong roots)
         const uint8_t* region = reinterpret_cast<const uint8_t*>(in + first(g) * NW);
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));  // recompute the offsets here (see lock_dma_c)
@@ -2406,6 +2410,13 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
     // Returns word 17 (the word after the block when o8 = 0).
     auto absorb = [&](State& st, uint32_t o8, auto setc) {
         constexpr bool SET = decltype(setc)::value;
+        if constexpr ((MK_TRIE_PROBE & 2) != 0) {  // probe: no LDS reads (wrong roots)
+            if constexpr (SET) {
+#pragma unroll
+                for (int w = 0; w < 17; ++w) st.lo[w] = st.hi[w] = lane + w;
+            }
+            return make_uint2(lane, o8);
+        }
         const bool sh = o8 != 0;
         uint4 prev = Bw[9 * lane];
         uint2 w17 = make_uint2(0, 0);

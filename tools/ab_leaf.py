@@ -123,7 +123,8 @@ def ab_trie(a, libs, dev):
             if r:
                 times[v].append(e0.elapsed_time(e1))
     roots = {v: bytes(o.cpu().numpy()).hex() for v, o in outs.items()}
-    assert len(set(roots.values())) == 1, roots
+    # "nl_*" variants are compute probes (MK_TRIE_PROBE): their roots differ
+    assert len({r for v, r in roots.items() if not v.startswith("nl_")}) == 1, roots
     # the C5 bench's form: a stream of tries, each trie's front (leaves + levels
     # wider than 2^17 nodes) on the main stream, its top on a high-priority
     # side stream overlapping the next front (pipeline.TriePipeline, 2 slots)
@@ -157,7 +158,7 @@ def ab_trie(a, libs, dev):
             torch.cuda.current_stream().wait_stream(side)
             e1.record()
             torch.cuda.synchronize()
-            assert bytes(souts[(S - 1) % 2].cpu().numpy()).hex() == roots[v], v
+            assert v.startswith("nl_") or bytes(souts[(S - 1) % 2].cpu().numpy()).hex() == roots[v], v
             if r:
                 stream_ms[v].append(e0.elapsed_time(e1) / S)
     # the C5 bench's form since round 4: the pipelined front (trie i's locked
@@ -195,7 +196,7 @@ def ab_trie(a, libs, dev):
                 torch.cuda.current_stream().wait_stream(side)
                 e1.record()
                 torch.cuda.synchronize()
-                assert bytes(prt[prev].cpu().numpy()).hex() == roots[v], v
+                assert v.startswith("nl_") or bytes(prt[prev].cpu().numpy()).hex() == roots[v], v
                 if r:
                     pipe_ms[v].append(e0.elapsed_time(e1) / P)
     for v in a.variants:
