@@ -291,6 +291,20 @@ __device__ __forceinline__ void keccak_f_lock_mid(State& s, F&& mid) {
 #pragma unroll kRoundUnroll
     for (int r = K; r < 24; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
 }
+// Locked permutation with `m1` run after round K1 and `m2` after round K2
+// (0 < K1 < K2 < 24).
+template <int K1, int K2, typename F1, typename F2>
+__device__ __forceinline__ void keccak_f_lock_mid2(State& s, F1&& m1, F2&& m2) {
+    static_assert(K1 > 0 && K1 < K2 && K2 < 24, "mid points");
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < K1; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    m1();
+#pragma unroll kRoundUnroll
+    for (int r = K1; r < K2; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    m2();
+#pragma unroll kRoundUnroll
+    for (int r = K2; r < 24; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+}
 // `mid` runs after round K (K = 0: before the permutation), e.g. the issue of
 // the next window's DMA in k_leaf_lock_sc.
 template <int K = 0, typename F>

@@ -2309,6 +2309,9 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 #ifndef MK_TRIE_PROBE
 #define MK_TRIE_PROBE 0  // A/B probes only (wrong roots): 1 = no DMA staging, 2 = no LDS block reads
 #endif
+#ifndef MK_TRIE_DMA_SPLIT
+#define MK_TRIE_DMA_SPLIT 0  // > 0: units 0-4 of the next block go out after this round, 5-8 after MK_TRIE_DMA_ROUND
+#endif
 #ifndef MK_TRIE_DMA_ROUND
 // round of a block's permutation after which the next block's DMA goes out;
 // 12 (mid-permutation) over 0: one trie 1.2-2.3 % faster on two boxes, the
@@ -2341,13 +2344,14 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
     uint4* Bw = buf[wave];
     uint4* const lv[4] = {L0, L1, L2, L3};
     auto first = [&](uint64_t g) { return (g * NT + 64 * wave) * DPT; };  // lane 0's first deposit
-    auto dma = [&](uint64_t g, int i, int b) {
+    // units [k0, k1) of the 9 (MK_TRIE_DMA_SPLIT: issued in two parts)
+    auto dma = [&](uint64_t g, int i, int b, int k0 = 0, int k1 = 9) {
         if constexpr ((MK_TRIE_PROBE & 1) != 0) return;  // probe: no staging (wrong roots)
         const uint8_t* region = reinterpret_cast<const uint8_t*>(in + first(g) * NW);
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));  // recompute the offsets here (see lock_dma_c)
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {
+        for (int k = k0; k < k1; ++k) {
             const uint32_t U = 64u * k + ln;
             const uint32_t m = U / 9, u = U - m * 9;
             const uint32_t start = (DPT * m + i) * (8 * NW) + 136 * b;
@@ -2465,7 +2469,11 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
 #pragma unroll
             for (int w = 17; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: block 1 may land
-            keccak_f_lock_mid<MK_TRIE_DMA_ROUND>(s, [&] { dma(g, i, 1); });
+            if constexpr (MK_TRIE_DMA_SPLIT > 0)
+                keccak_f_lock_mid2<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_ROUND>(s, [&] { dma(g, i, 1, 0, 5); },
+                                                                         [&] { dma(g, i, 1, 5, 9); });
+            else
+                keccak_f_lock_mid<MK_TRIE_DMA_ROUND>(s, [&] { dma(g, i, 1); });
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 1 landed
             // the 8-B tail word (deposit bytes 272..279): an odd slot's block 1
             // image ends with it (the block starts 16-B aligned, 9 units = 144
@@ -2475,12 +2483,17 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
             // an odd slot's block 1 starts 16-B aligned and ends with the tail word
             uint2 tl = absorb(s, (i + 1) & 1, Xor{});
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            keccak_f_lock_mid<MK_TRIE_DMA_ROUND>(s, [&] {
+            auto next_dma = [&](int k0, int k1) {
                 if (i + 1 < DPT)
-                    dma(g, i + 1, 0);
+                    dma(g, i + 1, 0, k0, k1);
                 else if (gn < ngroups)
-                    dma(gn, 0, 0);
-            });
+                    dma(gn, 0, 0, k0, k1);
+            };
+            if constexpr (MK_TRIE_DMA_SPLIT > 0)
+                keccak_f_lock_mid2<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_ROUND>(s, [&] { next_dma(0, 5); },
+                                                                         [&] { next_dma(5, 9); });
+            else
+                keccak_f_lock_mid<MK_TRIE_DMA_ROUND>(s, [&] { next_dma(0, 9); });
             if (!(i & 1)) {  // slot i + 1 < DPT of this group: its block 0 holds the tail
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 const uint4 v = Bw[9 * lane];
