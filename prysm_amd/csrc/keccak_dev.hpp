@@ -305,6 +305,22 @@ __device__ __forceinline__ void keccak_f_lock_mid2(State& s, F1&& m1, F2&& m2) {
 #pragma unroll kRoundUnroll
     for (int r = K2; r < 24; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
 }
+// ... with m1, m2, m3 after rounds K1 < K2 < K3.
+template <int K1, int K2, int K3, typename F1, typename F2, typename F3>
+__device__ __forceinline__ void keccak_f_lock_mid3(State& s, F1&& m1, F2&& m2, F3&& m3) {
+    static_assert(K1 > 0 && K1 < K2 && K2 < K3 && K3 < 24, "mid points");
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < K1; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    m1();
+#pragma unroll kRoundUnroll
+    for (int r = K1; r < K2; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    m2();
+#pragma unroll kRoundUnroll
+    for (int r = K2; r < K3; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    m3();
+#pragma unroll kRoundUnroll
+    for (int r = K3; r < 24; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+}
 // `mid` runs after round K (K = 0: before the permutation), e.g. the issue of
 // the next window's DMA in k_leaf_lock_sc.
 template <int K = 0, typename F>

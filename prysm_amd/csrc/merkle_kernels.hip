@@ -2312,6 +2312,9 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 #ifndef MK_TRIE_DMA_SPLIT
 #define MK_TRIE_DMA_SPLIT 0  // > 0: units 0-4 of the next block go out after this round, 5-8 after MK_TRIE_DMA_ROUND
 #endif
+#ifndef MK_TRIE_DMA_SPLIT3
+#define MK_TRIE_DMA_SPLIT3 0  // > 0 (with MK_TRIE_DMA_SPLIT): units 0-2, 3-5, 6-8 after rounds SPLIT, SPLIT3, ROUND
+#endif
 #ifndef MK_TRIE_DMA_ROUND
 // round of a block's permutation after which the next block's DMA goes out;
 // 12 (mid-permutation) over 0: one trie 1.2-2.3 % faster on two boxes, the
@@ -2469,7 +2472,10 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
 #pragma unroll
             for (int w = 17; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: block 1 may land
-            if constexpr (MK_TRIE_DMA_SPLIT > 0)
+            if constexpr (MK_TRIE_DMA_SPLIT3 > 0)
+                keccak_f_lock_mid3<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_SPLIT3, MK_TRIE_DMA_ROUND>(
+                    s, [&] { dma(g, i, 1, 0, 3); }, [&] { dma(g, i, 1, 3, 6); }, [&] { dma(g, i, 1, 6, 9); });
+            else if constexpr (MK_TRIE_DMA_SPLIT > 0)
                 keccak_f_lock_mid2<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_ROUND>(s, [&] { dma(g, i, 1, 0, 5); },
                                                                          [&] { dma(g, i, 1, 5, 9); });
             else
@@ -2489,7 +2495,10 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                 else if (gn < ngroups)
                     dma(gn, 0, 0, k0, k1);
             };
-            if constexpr (MK_TRIE_DMA_SPLIT > 0)
+            if constexpr (MK_TRIE_DMA_SPLIT3 > 0)
+                keccak_f_lock_mid3<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_SPLIT3, MK_TRIE_DMA_ROUND>(
+                    s, [&] { next_dma(0, 3); }, [&] { next_dma(3, 6); }, [&] { next_dma(6, 9); });
+            else if constexpr (MK_TRIE_DMA_SPLIT > 0)
                 keccak_f_lock_mid2<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_ROUND>(s, [&] { next_dma(0, 5); },
                                                                          [&] { next_dma(5, 9); });
             else
