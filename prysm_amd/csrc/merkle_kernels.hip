@@ -2312,6 +2312,9 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 #ifndef MK_TRIE_DMA_SPLIT
 #define MK_TRIE_DMA_SPLIT 0  // > 0: units 0-4 of the next block go out after this round, 5-8 after MK_TRIE_DMA_ROUND
 #endif
+#ifndef MK_TRIE_DMA_EACH
+#define MK_TRIE_DMA_EACH 0  // > 0: unit k of the next block goes out after round MK_TRIE_DMA_ROUND + k x EACH
+#endif
 #ifndef MK_TRIE_DMA_SPLIT3
 #define MK_TRIE_DMA_SPLIT3 0  // > 0 (with MK_TRIE_DMA_SPLIT): units 0-2, 3-5, 6-8 after rounds SPLIT, SPLIT3, ROUND
 #endif
@@ -2362,6 +2365,17 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                                              (__attribute__((address_space(3))) void*)(Bw + 64 * k), 16, 0,
                                              MK_TRIE_LOCK_AUX);
         }
+    };
+    // one unit k (runtime, wave-uniform) of the 9 (MK_TRIE_DMA_EACH)
+    auto dma_unit = [&](uint64_t g, int i, int b, int k) {
+        if constexpr ((MK_TRIE_PROBE & 1) != 0) return;
+        const uint8_t* region = reinterpret_cast<const uint8_t*>(in + first(g) * NW);
+        const uint32_t U = 64u * (uint32_t)k + lane;
+        const uint32_t m = U / 9, u = U - m * 9;
+        const uint32_t start = (DPT * m + i) * (8 * NW) + 136 * b;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(region + (start & ~15u) + 16 * u),
+                                         (__attribute__((address_space(3))) void*)(Bw + 64 * k), 16, 0,
+                                         MK_TRIE_LOCK_AUX);
     };
     // a node is stored after the next slot's first wait, so no wait covers a
     // store issued just before it (stores count in vmcnt)
@@ -2472,7 +2486,13 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
 #pragma unroll
             for (int w = 17; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: block 1 may land
-            if constexpr (MK_TRIE_DMA_SPLIT3 > 0)
+            if constexpr (MK_TRIE_DMA_EACH > 0)
+                keccak_f_lock_each(s, [&](int r) {
+                    const int q = r - MK_TRIE_DMA_ROUND;
+                    if (q >= 0 && q % MK_TRIE_DMA_EACH == 0 && q / MK_TRIE_DMA_EACH < 9)
+                        dma_unit(g, i, 1, q / MK_TRIE_DMA_EACH);
+                });
+            else if constexpr (MK_TRIE_DMA_SPLIT3 > 0)
                 keccak_f_lock_mid3<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_SPLIT3, MK_TRIE_DMA_ROUND>(
                     s, [&] { dma(g, i, 1, 0, 3); }, [&] { dma(g, i, 1, 3, 6); }, [&] { dma(g, i, 1, 6, 9); });
             else if constexpr (MK_TRIE_DMA_SPLIT > 0)
@@ -2495,7 +2515,17 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                 else if (gn < ngroups)
                     dma(gn, 0, 0, k0, k1);
             };
-            if constexpr (MK_TRIE_DMA_SPLIT3 > 0)
+            if constexpr (MK_TRIE_DMA_EACH > 0)
+                keccak_f_lock_each(s, [&](int r) {
+                    const int q = r - MK_TRIE_DMA_ROUND;
+                    if (q >= 0 && q % MK_TRIE_DMA_EACH == 0 && q / MK_TRIE_DMA_EACH < 9) {
+                        if (i + 1 < DPT)
+                            dma_unit(g, i + 1, 0, q / MK_TRIE_DMA_EACH);
+                        else if (gn < ngroups)
+                            dma_unit(gn, 0, 0, q / MK_TRIE_DMA_EACH);
+                    }
+                });
+            else if constexpr (MK_TRIE_DMA_SPLIT3 > 0)
                 keccak_f_lock_mid3<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_SPLIT3, MK_TRIE_DMA_ROUND>(
                     s, [&] { next_dma(0, 3); }, [&] { next_dma(3, 6); }, [&] { next_dma(6, 9); });
             else if constexpr (MK_TRIE_DMA_SPLIT > 0)
