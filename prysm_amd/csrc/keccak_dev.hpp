@@ -305,16 +305,6 @@ __device__ __forceinline__ void keccak_f_lock_mid2(State& s, F1&& m1, F2&& m2) {
 #pragma unroll kRoundUnroll
     for (int r = K2; r < 24; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
 }
-// Locked permutation with hook(r) run after every round r (r a runtime,
-// wave-uniform value: the hook branches on it).
-template <typename F>
-__device__ __forceinline__ void keccak_f_lock_each(State& s, F&& hook) {
-#pragma unroll kRoundUnroll
-    for (int r = 0; r < 24; ++r) {
-        round_asm<true>(s, kRcLo[r], kRcHi[r]);
-        hook(r);
-    }
-}
 // ... with m1, m2, m3 after rounds K1 < K2 < K3.
 template <int K1, int K2, int K3, typename F1, typename F2, typename F3>
 __device__ __forceinline__ void keccak_f_lock_mid3(State& s, F1&& m1, F2&& m2, F3&& m3) {

@@ -2303,26 +2303,33 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 // during block 0's permutation, block 0 of slot i + 1 (or of the next group)
 // during block 1's; the 8-B tail words are loaded per lane one slot ahead.
 // Whole groups only (the host runs the rest with k_keccak_rec + k_trie_level).
-#ifndef MK_TRIE_LOCK_AUX
-#define MK_TRIE_LOCK_AUX 0  // global_load_lds policy of the deposit DMA (2 = nt)
-#endif
+// global_load_lds policy of the deposit DMA: 0 (nt = 2: +0.7 % on the
+// pipelined stream, profiles/r05/c5_front_ab/)
+#define MK_TRIE_LOCK_AUX 0
 #ifndef MK_TRIE_PROBE
 #define MK_TRIE_PROBE 0  // A/B probes only (wrong roots): 1 = no DMA staging, 2 = no LDS block reads
 #endif
+// The next block's 9-unit DMA goes out in parts spread over the current
+// block's permutation: units 0-2, 3-5, 6-8 after rounds MK_TRIE_DMA_SPLIT,
+// MK_TRIE_DMA_SPLIT3 and MK_TRIE_DMA_ROUND (SPLIT3 = 0: units 0-4 / 5-8
+// after SPLIT / ROUND; SPLIT = 0: all after ROUND).  Issued all at once, 16
+// waves' DMA instructions burst together and the locked waves wait on the
+// slowest issue.  One process A/B (profiles/r05/c5_front_ab/ab_dma_split*.txt,
+// 9 interleaved rounds each, two boxes): pipelined stream 0.4086 -> 0.4017
+// and 0.4163 -> 0.4092 ms/step (4/10/16 against all after 12), one trie
+// 0.543 -> 0.515 and 0.561 -> 0.534 ms; two parts -1.1 %, one unit per round
+// or two -0.4 to -1.1 %.
 #ifndef MK_TRIE_DMA_SPLIT
-#define MK_TRIE_DMA_SPLIT 0  // > 0: units 0-4 of the next block go out after this round, 5-8 after MK_TRIE_DMA_ROUND
-#endif
-#ifndef MK_TRIE_DMA_EACH
-#define MK_TRIE_DMA_EACH 0  // > 0: unit k of the next block goes out after round MK_TRIE_DMA_ROUND + k x EACH
+#define MK_TRIE_DMA_SPLIT 4
 #endif
 #ifndef MK_TRIE_DMA_SPLIT3
-#define MK_TRIE_DMA_SPLIT3 0  // > 0 (with MK_TRIE_DMA_SPLIT): units 0-2, 3-5, 6-8 after rounds SPLIT, SPLIT3, ROUND
+#define MK_TRIE_DMA_SPLIT3 10
 #endif
 #ifndef MK_TRIE_DMA_ROUND
-// round of a block's permutation after which the next block's DMA goes out;
-// 12 (mid-permutation) over 0: one trie 1.2-2.3 % faster on two boxes, the
-// stream of tries unchanged (profiles/r04/trie_dma_ab/)
-#define MK_TRIE_DMA_ROUND 12
+// round of a block's permutation after which the next block's DMA (its last
+// part) goes out; as one part: 12 (mid-permutation) over 0, one trie 1.2-2.3
+// % faster on two boxes (profiles/r04/trie_dma_ab/); in three parts: 16
+#define MK_TRIE_DMA_ROUND 16
 #endif
 
 // PIPE (a stream of tries, pipeline.TriePipeline): workgroup b also takes the
@@ -2365,17 +2372,6 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                                              (__attribute__((address_space(3))) void*)(Bw + 64 * k), 16, 0,
                                              MK_TRIE_LOCK_AUX);
         }
-    };
-    // one unit k (runtime, wave-uniform) of the 9 (MK_TRIE_DMA_EACH)
-    auto dma_unit = [&](uint64_t g, int i, int b, int k) {
-        if constexpr ((MK_TRIE_PROBE & 1) != 0) return;
-        const uint8_t* region = reinterpret_cast<const uint8_t*>(in + first(g) * NW);
-        const uint32_t U = 64u * (uint32_t)k + lane;
-        const uint32_t m = U / 9, u = U - m * 9;
-        const uint32_t start = (DPT * m + i) * (8 * NW) + 136 * b;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(region + (start & ~15u) + 16 * u),
-                                         (__attribute__((address_space(3))) void*)(Bw + 64 * k), 16, 0,
-                                         MK_TRIE_LOCK_AUX);
     };
     // a node is stored after the next slot's first wait, so no wait covers a
     // store issued just before it (stores count in vmcnt)
@@ -2486,13 +2482,7 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
 #pragma unroll
             for (int w = 17; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: block 1 may land
-            if constexpr (MK_TRIE_DMA_EACH > 0)
-                keccak_f_lock_each(s, [&](int r) {
-                    const int q = r - MK_TRIE_DMA_ROUND;
-                    if (q >= 0 && q % MK_TRIE_DMA_EACH == 0 && q / MK_TRIE_DMA_EACH < 9)
-                        dma_unit(g, i, 1, q / MK_TRIE_DMA_EACH);
-                });
-            else if constexpr (MK_TRIE_DMA_SPLIT3 > 0)
+            if constexpr (MK_TRIE_DMA_SPLIT3 > 0)
                 keccak_f_lock_mid3<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_SPLIT3, MK_TRIE_DMA_ROUND>(
                     s, [&] { dma(g, i, 1, 0, 3); }, [&] { dma(g, i, 1, 3, 6); }, [&] { dma(g, i, 1, 6, 9); });
             else if constexpr (MK_TRIE_DMA_SPLIT > 0)
@@ -2515,17 +2505,7 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
                 else if (gn < ngroups)
                     dma(gn, 0, 0, k0, k1);
             };
-            if constexpr (MK_TRIE_DMA_EACH > 0)
-                keccak_f_lock_each(s, [&](int r) {
-                    const int q = r - MK_TRIE_DMA_ROUND;
-                    if (q >= 0 && q % MK_TRIE_DMA_EACH == 0 && q / MK_TRIE_DMA_EACH < 9) {
-                        if (i + 1 < DPT)
-                            dma_unit(g, i + 1, 0, q / MK_TRIE_DMA_EACH);
-                        else if (gn < ngroups)
-                            dma_unit(gn, 0, 0, q / MK_TRIE_DMA_EACH);
-                    }
-                });
-            else if constexpr (MK_TRIE_DMA_SPLIT3 > 0)
+            if constexpr (MK_TRIE_DMA_SPLIT3 > 0)
                 keccak_f_lock_mid3<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_SPLIT3, MK_TRIE_DMA_ROUND>(
                     s, [&] { next_dma(0, 3); }, [&] { next_dma(3, 6); }, [&] { next_dma(6, 9); });
             else if constexpr (MK_TRIE_DMA_SPLIT > 0)
