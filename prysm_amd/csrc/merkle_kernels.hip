@@ -2307,7 +2307,7 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 // pipelined stream, profiles/r05/c5_front_ab/)
 #define MK_TRIE_LOCK_AUX 0
 #ifndef MK_TRIE_PROBE
-#define MK_TRIE_PROBE 0  // A/B probes only (wrong roots): 1 = no DMA staging, 2 = no LDS block reads
+#define MK_TRIE_PROBE 0  // A/B probes only (wrong roots): 1 = no DMA staging, 2 = no LDS block reads, 4 = no slot loads
 #endif
 // The next block's 9-unit DMA goes out in parts spread over the current
 // block's permutation: units 0-2, 3-5, 6-8 after rounds MK_TRIE_DMA_SPLIT,
@@ -2390,7 +2390,7 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));  // computed here, not hoisted and kept live across the loop
         const uint32_t j = 64u * (wv - w0) + ln;
-        const bool act = prev.live && j < per;
+        const bool act = prev.live && j < per && (MK_TRIE_PROBE & 4) == 0;  // probe 4: no slot loads / stores
         const uint32_t jg = blockIdx.x * per + j;  // < 2^19: 32-bit offsets from the uniform bases
         const uint4* src = k == 3 ? prev.l2 : prev.l[k - 4];
         asm volatile("" ::: "memory");
