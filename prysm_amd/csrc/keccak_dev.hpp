@@ -337,6 +337,26 @@ __device__ __forceinline__ void keccak_f_digest_lock(State& s, F&& mid) {
     asm volatile("" : "+v"(s.lo[0]), "+v"(s.hi[0]), "+v"(s.lo[1]), "+v"(s.hi[1]), "+v"(s.lo[2]), "+v"(s.hi[2]),
                  "+v"(s.lo[3]), "+v"(s.hi[3]));
 }
+// The digest-only form with m1, m2, m3 after rounds K1 < K2 < K3 <= 22.
+template <int K1, int K2, int K3, typename F1, typename F2, typename F3>
+__device__ __forceinline__ void keccak_f_digest_lock_mid3(State& s, F1&& m1, F2&& m2, F3&& m3) {
+    static_assert(K1 > 0 && K1 < K2 && K2 < K3 && K3 <= 22, "mid points");
+#pragma unroll kRoundUnroll
+    for (int r = 0; r < K1; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    m1();
+#pragma unroll kRoundUnroll
+    for (int r = K1; r < K2; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    m2();
+#pragma unroll kRoundUnroll
+    for (int r = K2; r < K3; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    m3();
+#pragma unroll kRoundUnroll
+    for (int r = K3; r < 22; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);
+    round_asm<true>(s, kRcLo[22], kRcHi[22]);
+    last_round_digest(s, kRcLo[23], kRcHi[23]);
+    asm volatile("" : "+v"(s.lo[0]), "+v"(s.hi[0]), "+v"(s.lo[1]), "+v"(s.hi[1]), "+v"(s.lo[2]), "+v"(s.hi[2]),
+                 "+v"(s.lo[3]), "+v"(s.hi[3]));
+}
 __device__ __forceinline__ void keccak_f_digest_lock(State& s) {
 #pragma unroll kRoundUnroll
     for (int r = 0; r < 22; ++r) round_asm<true>(s, kRcLo[r], kRcHi[r]);

@@ -477,40 +477,47 @@ k_reduce(ReduceArgs a) {
 #ifndef MK_LOCK_NT
 #define MK_LOCK_NT 1
 #endif
+#ifndef MK_LOCK_DMA_SPLIT
+#define MK_LOCK_DMA_SPLIT 0  // 1: phases A and B each issued in three parts over a permutation (A/B)
+#endif
 constexpr int kLockAux = MK_LOCK_NT ? 2 : 0;  // global_load_lds aux: nt
 // the side configs' locked kernels (C2 messages, C3 records): inputs read once
 #ifndef MK_SIDE_NT
 #define MK_SIDE_NT 0
 #endif
 constexpr int kSideAux = MK_SIDE_NT ? 2 : 0;
-template <int NU, int U0, int AUX = 0>
+template <int NU, int U0, int AUX = 0, int I0 = 0, int I1 = NU>
 __device__ __forceinline__ void lock_dma_c(uint4* Bw, const uint4* __restrict__ Rj, uint32_t lane) {
     // launder the lane index so the per-lane offsets are recomputed here (a
-    // few VALU per DMA) instead of being hoisted and held in 16+ VGPRs
+    // few VALU per DMA) instead of being hoisted and held in 16+ VGPRs;
+    // instructions [I0, I1) of the NU (a part of a split issue)
     asm volatile("" : "+v"(lane));
 #pragma unroll
-    for (int i = 0; i < NU; ++i) {
+    for (int i = I0; i < I1; ++i) {
         const uint32_t U = 64u * i + lane;
         const uint32_t m = U / NU, u = U - m * NU;
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Rj + m * 64 + U0 + u),
                                          (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, AUX);
     }
 }
-// phase A of a window step (block 1 = units 0..8)
+// phase A of a window step (block 1 = units 0..8); instructions [I0, I1) of
+// the 9 (+ the unit-8 copy with the last part)
+template <int I0 = 0, int I1 = 9>
 __device__ __forceinline__ void lock_dma_a(uint4* Bw, const uint4* __restrict__ Rj, uint32_t lane) {
     if constexpr (!MK_LOCK_NT) {
-        lock_dma_c<9, 0>(Bw, Rj, lane);
+        lock_dma_c<9, 0, 0, I0, I1>(Bw, Rj, lane);
     } else {
         asm volatile("" : "+v"(lane));
 #pragma unroll
-        for (int i = 0; i < 9; ++i) {
+        for (int i = I0; i < I1; ++i) {
             const uint32_t U = 64u * i + lane;
             const uint32_t m = U / 9, u = U - m * 9;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Rj + m * 64 + (u < 8 ? u : 7)),
                                              (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, kLockAux);
         }
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Rj + lane * 64 + 8),
-                                         (__attribute__((address_space(3))) void*)(Bw + 576), 16, 0, 0);
+        if constexpr (I1 == 9)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(Rj + lane * 64 + 8),
+                                             (__attribute__((address_space(3))) void*)(Bw + 576), 16, 0, 0);
     }
 }
 
@@ -538,8 +545,14 @@ __device__ __forceinline__ void hash_window_sc(uint4* Bw, uint32_t lane, const u
 #pragma unroll
     for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: phase B may overwrite them
-    lock_dma_c<7, 9, kLockAux>(Bw, Rj, lane);
-    keccak_f_lock(s);
+    if constexpr (MK_LOCK_DMA_SPLIT) {  // phase B in three parts over the first permutation
+        lock_dma_c<7, 9, kLockAux, 0, 3>(Bw, Rj, lane);
+        keccak_f_lock_mid2<4, 8>(s, [&] { lock_dma_c<7, 9, kLockAux, 3, 5>(Bw, Rj, lane); },
+                                 [&] { lock_dma_c<7, 9, kLockAux, 5, 7>(Bw, Rj, lane); });
+    } else {
+        lock_dma_c<7, 9, kLockAux>(Bw, Rj, lane);
+        keccak_f_lock(s);
+    }
     s.lo[0] ^= v8.z;
     s.hi[0] ^= v8.w;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // phase B has landed
@@ -557,9 +570,16 @@ __device__ __forceinline__ void hash_window_sc(uint4* Bw, uint32_t lane, const u
     // the next window's block 1 goes out MK_LOCK_DMA_ROUND rounds into this
     // permutation: late enough that little of the data streamed in between
     // evicts the line block 2 shares with it, early enough to land in time
-    keccak_f_digest_lock<MK_LOCK_DMA_ROUND>(s, [&] {
-        if (Rnext) lock_dma_a(Bw, Rnext, lane);
-    });
+    if constexpr (MK_LOCK_DMA_SPLIT) {  // phase A of the next window in three parts
+        keccak_f_digest_lock_mid3<4, 8, MK_LOCK_DMA_ROUND>(
+            s, [&] { if (Rnext) lock_dma_a<0, 3>(Bw, Rnext, lane); },
+            [&] { if (Rnext) lock_dma_a<3, 6>(Bw, Rnext, lane); },
+            [&] { if (Rnext) lock_dma_a<6, 9>(Bw, Rnext, lane); });
+    } else {
+        keccak_f_digest_lock<MK_LOCK_DMA_ROUND>(s, [&] {
+            if (Rnext) lock_dma_a(Bw, Rnext, lane);
+        });
+    }
     digest(s, d0, d1);
 }
 
