@@ -480,6 +480,18 @@ k_reduce(ReduceArgs a) {
 #ifndef MK_LOCK_DMA_SPLIT
 #define MK_LOCK_DMA_SPLIT 0  // 1: phases A and B each issued in three parts over a permutation (A/B)
 #endif
+// the rounds of the split issue: phase B (the window's second block) 3 + 2 +
+// 2 instructions before round 0 and after B1, B2 of the first permutation;
+// phase A (the next window's first block) 3 + 3 + 3 (+1) after A1, A2 and
+// MK_LOCK_DMA_ROUND of the second
+#define MK_LOCK_SPLIT_B1 4
+#define MK_LOCK_SPLIT_B2 8
+#ifndef MK_LOCK_SPLIT_A1
+#define MK_LOCK_SPLIT_A1 4
+#endif
+#ifndef MK_LOCK_SPLIT_A2
+#define MK_LOCK_SPLIT_A2 8
+#endif
 constexpr int kLockAux = MK_LOCK_NT ? 2 : 0;  // global_load_lds aux: nt
 // the side configs' locked kernels (C2 messages, C3 records): inputs read once
 #ifndef MK_SIDE_NT
@@ -547,8 +559,9 @@ __device__ __forceinline__ void hash_window_sc(uint4* Bw, uint32_t lane, const u
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: phase B may overwrite them
     if constexpr (MK_LOCK_DMA_SPLIT) {  // phase B in three parts over the first permutation
         lock_dma_c<7, 9, kLockAux, 0, 3>(Bw, Rj, lane);
-        keccak_f_lock_mid2<4, 8>(s, [&] { lock_dma_c<7, 9, kLockAux, 3, 5>(Bw, Rj, lane); },
-                                 [&] { lock_dma_c<7, 9, kLockAux, 5, 7>(Bw, Rj, lane); });
+        keccak_f_lock_mid2<MK_LOCK_SPLIT_B1, MK_LOCK_SPLIT_B2>(
+            s, [&] { lock_dma_c<7, 9, kLockAux, 3, 5>(Bw, Rj, lane); },
+            [&] { lock_dma_c<7, 9, kLockAux, 5, 7>(Bw, Rj, lane); });
     } else {
         lock_dma_c<7, 9, kLockAux>(Bw, Rj, lane);
         keccak_f_lock(s);
@@ -571,7 +584,7 @@ __device__ __forceinline__ void hash_window_sc(uint4* Bw, uint32_t lane, const u
     // permutation: late enough that little of the data streamed in between
     // evicts the line block 2 shares with it, early enough to land in time
     if constexpr (MK_LOCK_DMA_SPLIT) {  // phase A of the next window in three parts
-        keccak_f_digest_lock_mid3<4, 8, MK_LOCK_DMA_ROUND>(
+        keccak_f_digest_lock_mid3<MK_LOCK_SPLIT_A1, MK_LOCK_SPLIT_A2, MK_LOCK_DMA_ROUND>(
             s, [&] { if (Rnext) lock_dma_a<0, 3>(Bw, Rnext, lane); },
             [&] { if (Rnext) lock_dma_a<3, 6>(Bw, Rnext, lane); },
             [&] { if (Rnext) lock_dma_a<6, 9>(Bw, Rnext, lane); });
