@@ -477,21 +477,21 @@ k_reduce(ReduceArgs a) {
 #ifndef MK_LOCK_NT
 #define MK_LOCK_NT 1
 #endif
+// The DMA of each phase in three parts spread over a permutation instead of
+// one burst (the C5 front's finding): phase B (the window's
+// second block) 3 + 2 + 2 instructions before round 0 and after rounds B1,
+// B2 of the first permutation; phase A (the next window's first block) 3 +
+// 3 + 3 (+1) after rounds A1, A2 and MK_LOCK_DMA_ROUND of the second.  One
+// process A/B (profiles/r05/leaf_dma_split/, 7-9 interleaved rounds, two
+// boxes): 2^28 tree -0.6..-0.8 % (leaf pass 7.943 -> 7.885 ms at 2/8/14),
+// 2^25 -2.6 %.  0: one burst each (round 4's form).
 #ifndef MK_LOCK_DMA_SPLIT
-#define MK_LOCK_DMA_SPLIT 0  // 1: phases A and B each issued in three parts over a permutation (A/B)
+#define MK_LOCK_DMA_SPLIT 1
 #endif
-// the rounds of the split issue: phase B (the window's second block) 3 + 2 +
-// 2 instructions before round 0 and after B1, B2 of the first permutation;
-// phase A (the next window's first block) 3 + 3 + 3 (+1) after A1, A2 and
-// MK_LOCK_DMA_ROUND of the second
 #define MK_LOCK_SPLIT_B1 4
 #define MK_LOCK_SPLIT_B2 8
-#ifndef MK_LOCK_SPLIT_A1
-#define MK_LOCK_SPLIT_A1 4
-#endif
-#ifndef MK_LOCK_SPLIT_A2
+#define MK_LOCK_SPLIT_A1 2
 #define MK_LOCK_SPLIT_A2 8
-#endif
 constexpr int kLockAux = MK_LOCK_NT ? 2 : 0;  // global_load_lds aux: nt
 // the side configs' locked kernels (C2 messages, C3 records): inputs read once
 #ifndef MK_SIDE_NT
@@ -2339,9 +2339,6 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 // global_load_lds policy of the deposit DMA: 0 (nt = 2: +0.7 % on the
 // pipelined stream, profiles/r05/c5_front_ab/)
 #define MK_TRIE_LOCK_AUX 0
-#ifndef MK_TRIE_PROBE
-#define MK_TRIE_PROBE 0  // A/B probes only (wrong roots): 1 = no DMA staging, 2 = no LDS block reads, 4 = no slot loads
-#endif
 // The next block's 9-unit DMA goes out in parts spread over the current
 // block's permutation: units 0-2, 3-5, 6-8 after rounds MK_TRIE_DMA_SPLIT,
 // MK_TRIE_DMA_SPLIT3 and MK_TRIE_DMA_ROUND (SPLIT3 = 0: units 0-4 / 5-8
@@ -2392,7 +2389,6 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
     auto first = [&](uint64_t g) { return (g * NT + 64 * wave) * DPT; };  // lane 0's first deposit
     // units [k0, k1) of the 9 (MK_TRIE_DMA_SPLIT: issued in two parts)
     auto dma = [&](uint64_t g, int i, int b, int k0 = 0, int k1 = 9) {
-        if constexpr ((MK_TRIE_PROBE & 1) != 0) return;  // probe: no staging (wrong roots)
         const uint8_t* region = reinterpret_cast<const uint8_t*>(in + first(g) * NW);
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));  // recompute the offsets here (see lock_dma_c)
@@ -2423,7 +2419,7 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));  // computed here, not hoisted and kept live across the loop
         const uint32_t j = 64u * (wv - w0) + ln;
-        const bool act = prev.live && j < per && (MK_TRIE_PROBE & 4) == 0;  // probe 4: no slot loads / stores
+        const bool act = prev.live && j < per;
         const uint32_t jg = blockIdx.x * per + j;  // < 2^19: 32-bit offsets from the uniform bases
         const uint4* src = k == 3 ? prev.l2 : prev.l[k - 4];
         asm volatile("" ::: "memory");
@@ -2460,13 +2456,6 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
     // Returns word 17 (the word after the block when o8 = 0).
     auto absorb = [&](State& st, uint32_t o8, auto setc) {
         constexpr bool SET = decltype(setc)::value;
-        if constexpr ((MK_TRIE_PROBE & 2) != 0) {  // probe: no LDS reads (wrong roots)
-            if constexpr (SET) {
-#pragma unroll
-                for (int w = 0; w < 17; ++w) st.lo[w] = st.hi[w] = lane + w;
-            }
-            return make_uint2(lane, o8);
-        }
         const bool sh = o8 != 0;
         uint4 prev = Bw[9 * lane];
         uint2 w17 = make_uint2(0, 0);

@@ -28,7 +28,7 @@ constexpr uint32_t kLockThreads = 1024;
 constexpr uint64_t kLockWindows = 4 * kLockThreads;
 __global__ void k_leaf_lock_sc(ReduceArgs a, uint64_t ngroups);  // coalesced LDS-DMA staging, persistent grid
 #ifndef MK_LOCK_DMA_ROUND
-#define MK_LOCK_DMA_ROUND 12  // k_leaf_lock_sc: round of a window's second permutation after which the next block 1 is fetched
+#define MK_LOCK_DMA_ROUND 14  // k_leaf_lock_sc: round of a window's second permutation after which the last part of the next block 1 is fetched
 #endif
 #ifndef MK_LOCK_GRID
 #define MK_LOCK_GRID 256
