@@ -1484,12 +1484,13 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
     uint4* Bw = buf[wave];
     // a partial last group: lanes past n hash a copy of message n - 1 and store nothing
     const uint64_t ngroups = (n + kLockThreads - 1) / kLockThreads;
-    auto dma = [&](uint64_t g) {
+    // instructions [i0, i1) of the 5 (issued in parts over the permutation)
+    auto dma = [&](uint64_t g, uint32_t i0, uint32_t i1) {
         const uint64_t m0 = g * kLockThreads + 64 * wave;
         uint32_t ln = lane;
         asm volatile("" : "+v"(ln));
 #pragma unroll
-        for (uint32_t i = 0; i < 5; ++i) {
+        for (uint32_t i = i0; i < i1; ++i) {
             const uint32_t p = 64 * i + ln, m = p / 5, u = p - 5 * m;
             const uint64_t msg = m0 + m < n ? m0 + m : n - 1;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(in + 4 * msg + (u < 4 ? u : 3)),
@@ -1498,7 +1499,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
         }
     };
     uint64_t g = blockIdx.x;
-    if (g < ngroups) dma(g);
+    if (g < ngroups) dma(g, 0, 5);
     uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;  // the previous group's digest, stored after the next wait
     uint64_t qi = 0;
     bool pend = false;
@@ -1523,8 +1524,12 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
         s.lo[8] = 1u;  // byte 64
         s.hi[16] = 0x80000000u;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read: the next group's copy may land
-        if (g + gridDim.x < ngroups) dma(g + gridDim.x);
-        keccak_f_digest_lock(s);
+        // the next group's copy in three parts over the permutation, not one
+        // burst of 16 waves' DMA (the C5 front's finding)
+        const bool more = g + gridDim.x < ngroups;
+        keccak_f_digest_lock_mid3<2, 8, 14>(
+            s, [&] { if (more) dma(g + gridDim.x, 0, 2); }, [&] { if (more) dma(g + gridDim.x, 2, 4); },
+            [&] { if (more) dma(g + gridDim.x, 4, 5); });
         digest(s, q0, q1);
         qi = g * kLockThreads + threadIdx.x;
         pend = true;
@@ -1981,11 +1986,12 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     // (every wave still runs the same permutations and barriers) and store nothing
     const uint64_t ngroups = (n + kLockThreads - 1) / kLockThreads;
     const uint64_t last_unit = n * (kRecLen / 16) - 1;
-    auto dma = [&](uint64_t g) {
+    // instructions [i0, i1) of the kNinstr (issued in parts)
+    auto dma = [&](uint64_t g, uint32_t i0 = 0, uint32_t i1 = kNinstr) {
         const uint64_t u0 = (g * kLockThreads + 64 * wave) * (kRecLen / 16);
         const uint4* src = reinterpret_cast<const uint4*>(rec);
 #pragma unroll
-        for (uint32_t i = 0; i < kNinstr; ++i) {
+        for (uint32_t i = i0; i < i1; ++i) {
             const uint64_t u = u0 + 64 * i + lane;
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (u < last_unit ? u : last_unit)),
                                              (__attribute__((address_space(3))) void*)(Bw + 256 * i), 16, 0,
@@ -2063,8 +2069,12 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
         for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
         const uint32_t t0 = R[kValOff[3] / 4 + 10], t1 = R[kValOff[3] / 4 + 11];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // record read: the next group's copy may land
-        if (g + g_step < g_end) dma(g + g_step);
-        keccak_f_lock(s);
+        // the next group's copy in three parts over the first struct
+        // permutation, not one burst of 16 waves' DMA
+        const bool more = g + g_step < g_end;
+        keccak_f_lock_mid3<2, 8, 14>(s, [&] { if (more) dma(g + g_step, 0, 4); },
+                                     [&] { if (more) dma(g + g_step, 4, 7); },
+                                     [&] { if (more) dma(g + g_step, 7, 10); });
         s.lo[0] ^= t0;
         s.hi[0] ^= t1;
         s.lo[1] ^= 1u;  // domain pad at message byte 144 = block 2 byte 8
