@@ -1524,12 +1524,10 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
         s.lo[8] = 1u;  // byte 64
         s.hi[16] = 0x80000000u;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read: the next group's copy may land
-        // the next group's copy in three parts over the permutation, not one
-        // burst of 16 waves' DMA (the C5 front's finding)
-        const bool more = g + gridDim.x < ngroups;
-        keccak_f_digest_lock_mid3<2, 8, 14>(
-            s, [&] { if (more) dma(g + gridDim.x, 0, 2); }, [&] { if (more) dma(g + gridDim.x, 2, 4); },
-            [&] { if (more) dma(g + gridDim.x, 4, 5); });
+        // one burst (5 instructions; in three parts over the permutation:
+        // 1.476 -> 1.483 ms at 2^24, within noise, profiles/r05/side_dma_split/)
+        if (g + gridDim.x < ngroups) dma(g + gridDim.x, 0, 5);
+        keccak_f_digest_lock(s);
         digest(s, q0, q1);
         qi = g * kLockThreads + threadIdx.x;
         pend = true;
@@ -2070,7 +2068,8 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
         const uint32_t t0 = R[kValOff[3] / 4 + 10], t1 = R[kValOff[3] / 4 + 11];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // record read: the next group's copy may land
         // the next group's copy in three parts over the first struct
-        // permutation, not one burst of 16 waves' DMA
+        // permutation, not one burst of 16 waves' DMA (the
+        // 10^6 list root 0.600 -> 0.593 ms, profiles/r05/side_dma_split/)
         const bool more = g + g_step < g_end;
         keccak_f_lock_mid3<2, 8, 14>(s, [&] { if (more) dma(g + g_step, 0, 4); },
                                      [&] { if (more) dma(g + g_step, 4, 7); },
