@@ -23,6 +23,14 @@ every step's work completes inside the timed region.  Inputs are generated on th
 stay resident in HBM.  Total work is fixed as N grows ("strong" scaling);
 value = 2^log2n leaves x K / max-over-ranks wall time.  Rank 0 prints one
 JSON line; progress goes to stderr.
+
+N = 1: after the timed region, the CPU baseline (the oracle's C port with the
+unrolled permutation, oracle/keccak_fast.c) and every other BASELINE config
+(C2, C3, C5, C1: tools/bench_configs.py, device-resident, 200 timed steps
+each, roots checked against tests/golden/full_size_roots.json) go into the
+same line (`side_configs`).  N > 1: rank 0 also times the whole tree on its
+GPU alone after the timed region (`single_gpu_ms`), and the line carries
+`parallel_efficiency`, every rank's leaf fraction and the aggregate fraction.
 """
 from __future__ import annotations
 
