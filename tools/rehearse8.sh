@@ -12,8 +12,13 @@ grep '^{' gpurun_out/rehearse8.json | tail -1 | python -c "
 import json, sys
 d = json.loads(sys.stdin.read())
 c = d['config']
+r = d['roofline']
 print(json.dumps({'ranks_on_one_gpu': d['n_gpus'], 'n_items': c['n_items'], 'shard_height': c['shard_height'],
-                  'frontier_log2': c['frontier_log2'], 'pipelined': c.get('pipelined'), 'root': c['root']}))
+                  'frontier_log2': c['frontier_log2'], 'pipelined': c.get('pipelined'), 'root': c['root'],
+                  'single_gpu_ms': c.get('single_gpu_ms'), 'parallel_efficiency': c.get('parallel_efficiency'),
+                  'per_rank_leaf_frac': c.get('per_rank_leaf_frac'), 'step_frac_aggregate': r.get('step_frac_aggregate'),
+                  'traffic': r.get('traffic'), 'traffic_source': r.get('traffic_source')}))
 assert c['root'] == '54a62269279a90e4bda5a9da4b5bb0d5f3126bb3aacb1456cc0b0e47b9f50ba9', c['root']
 assert c.get('pipelined') is True
+assert c['single_gpu_ms'] and c['parallel_efficiency'] and len(c['per_rank_leaf_frac']) == 8
 " | tee gpurun_out/rehearse8_summary.json
