@@ -9,15 +9,16 @@ With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py launches
 itself as N ranks (torch.distributed.run as a child process, started before
 this process touches the GPU) and exits with the child's status.
 
-One step = one complete Merkleization of the whole tree.  N > 1: every rank
-reduces its shard to the level 10 below its shard root (1024 nodes, the
-"frontier"), one 32-KB-per-rank RCCL all-gather, rank 0 finishes the top
-levels and the length mix-in on a side stream that overlaps its next step.
-With --pipeline (default) everything above the leaf pass runs on a side
-stream that overlaps the next step's leaf pass: at N = 1 the node passes and
-the length mix-in (prysm_amd/pipeline.py, split at the leaf pass's output
-level, 21 below the root at 2^28); at N > 1 each rank's node passes down to its
-frontier, the all-gather and rank 0's finisher (parallel.ShardedMerklePipeline).
+One step = one complete Merkleization of the whole tree.  N = 1 (default):
+one stream, the persistent phase-locked leaf pass then the node passes and
+the length mix-in (device.merkle_hash).  N > 1: every rank reduces its shard
+to the level 10 below its shard root (1024 nodes, the "frontier"), one
+32-KB-per-rank RCCL all-gather, rank 0 finishes the top levels and the
+length mix-in; with --pipeline 1 (the N > 1 default) each rank's node passes
+down to its frontier, the all-gather and rank 0's finisher run on a side
+stream that overlaps the next step's leaf pass (parallel.ShardedMerklePipeline;
+at N = 1, --pipeline 1 splits the tree at the leaf pass's output level,
+prysm_amd/pipeline.py: 0.8-1.1 % slower than one stream on one GPU).
 The pipelined root is checked against the one-stream root before timing, and
 every step's work completes inside the timed region.  Inputs are generated on the device before timing and
 stay resident in HBM.  Total work is fixed as N grows ("strong" scaling);
@@ -275,11 +276,13 @@ def main():
     ap.add_argument("--frontier", type=int, default=10,
                     help="N>1: each rank gathers its tree level this many levels below its shard root "
                          "(2^k nodes) and rank 0 finishes the top (0 = gather the 32-B shard roots)")
-    ap.add_argument("--pipeline", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--pipeline", type=int, default=-1, choices=[-1, 0, 1],
                     help="1: everything above the leaf pass (5 levels above the chunks) runs on a side stream "
                          "overlapping the next step's leaf pass: N=1 the node passes and the length mix-in "
                          "(prysm_amd/pipeline.py), N>1 each rank's node passes, the all-gather and rank 0's "
-                         "finisher (parallel.ShardedMerklePipeline).  0 = one stream")
+                         "finisher (parallel.ShardedMerklePipeline).  0 = one stream.  -1 (default): 0 at N = 1 "
+                         "(the one-stream tree with the persistent locked leaf pass measured 0.8-1.1 %% faster than "
+                         "the pipelined form on two boxes, DESIGN.md §6), 1 at N > 1")
     ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c4tree", "c5"],
                     help="BASELINE.json config: c4 = headline (default); c1/c2/c3/c5 = single-GPU side benches; "
                          "c4tree = the C4 secondary, TreeHash([][32]byte) of 2^28 elements")
@@ -423,6 +426,8 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
     # stream that overlaps step i+1's leaf pass (N = 1: pipeline.py; N > 1:
     # node passes, the all-gather and rank 0's finisher, parallel.py)
     pipe = None
+    if args.pipeline < 0:
+        args.pipeline = 1 if world > 1 else 0
     if args.pipeline > 0:
         if world == 1:
             from prysm_amd.pipeline import MerklePipeline
@@ -528,7 +533,7 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
         per_rank_leaf_frac = [round(r[2] / (r[1] / 1e3) / PEAK_INT_OPS, 4) if r[1] > 0 else None for r in rows]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     t_max = t.item()
-    # N > 1: the same whole tree on rank 0's GPU alone (MerklePipeline, the
+    # N > 1: the same whole tree on rank 0's GPU alone (one stream, the
     # N = 1 bench's step, same steps/warmup), after the timed region, so the
     # line carries its own strong-scaling efficiency t_1 / (N t_N)
     single_gpu_ms = None
@@ -641,29 +646,29 @@ def run_ranks(args, world: int, rank: int, local: int) -> int:
 
 def single_gpu_step_ms(args, dev, n: int, item_len: int) -> float:
     """ms per step of the whole n-item tree on this GPU alone: the N = 1
-    bench's pipelined step (pipeline.MerklePipeline), args.warmup untimed
-    and args.steps timed steps, wall clock bracketed by synchronize()."""
+    bench's step (one stream, device.merkle_hash), args.warmup untimed and
+    args.steps timed steps, wall clock bracketed by synchronize()."""
     import torch
 
     from prysm_amd import device as D
-    from prysm_amd.pipeline import MerklePipeline
 
     log(f"rank 0: the whole 2^{args.log2n} tree on one GPU (parallel_efficiency) ...")
     items = torch.empty(n * item_len, dtype=torch.uint8, device=dev)
     D.synth_fill(items, SEED)
-    pipe = MerklePipeline(n, item_len, dev)
+    ws = D.merkle_workspace(n, item_len, dev)
+    out = torch.empty(32, dtype=torch.uint8, device=dev)
     for _ in range(args.warmup):
-        pipe.submit(items)
+        D.merkle_hash(items, n, item_len, out=out, ws=ws)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        r = pipe.submit(items)
+        r = D.merkle_hash(items, n, item_len, out=out, ws=ws)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / args.steps * 1e3
     want = golden_root(args.log2n, item_len)
     if want is not None and bytes(r.cpu().numpy()).hex() != want:
         raise RuntimeError("single-GPU root differs from the golden root")
-    del items, pipe
+    del items, ws
     torch.cuda.empty_cache()
     return ms
 
