@@ -18,7 +18,7 @@ length mix-in; with --pipeline 1 (the N > 1 default) each rank's node passes
 down to its frontier, the all-gather and rank 0's finisher run on a side
 stream that overlaps the next step's leaf pass (parallel.ShardedMerklePipeline;
 at N = 1, --pipeline 1 splits the tree at the leaf pass's output level,
-prysm_amd/pipeline.py: 0.8-1.1 % slower than one stream on one GPU).
+prysm_amd/pipeline.py: 1.0-1.9 % slower than one stream on one GPU, two boxes).
 The pipelined root is checked against the one-stream root before timing, and
 every step's work completes inside the timed region.  Inputs are generated on the device before timing and
 stay resident in HBM.  Total work is fixed as N grows ("strong" scaling);
@@ -281,7 +281,7 @@ def main():
                          "overlapping the next step's leaf pass: N=1 the node passes and the length mix-in "
                          "(prysm_amd/pipeline.py), N>1 each rank's node passes, the all-gather and rank 0's "
                          "finisher (parallel.ShardedMerklePipeline).  0 = one stream.  -1 (default): 0 at N = 1 "
-                         "(the one-stream tree with the persistent locked leaf pass measured 0.8-1.1 %% faster than "
+                         "(the one-stream tree with the persistent locked leaf pass measured 1.0-1.9 %% faster than "
                          "the pipelined form on two boxes, DESIGN.md §6), 1 at N > 1")
     ap.add_argument("--config", default="c4", choices=["c1", "c2", "c3", "c4", "c4tree", "c5"],
                     help="BASELINE.json config: c4 = headline (default); c1/c2/c3/c5 = single-GPU side benches; "
