@@ -229,6 +229,28 @@ int or_merkle_hash_gen(uint64_t n, uint32_t item_len, uint64_t seed, uint8_t out
     return 0;
 }
 
+/* ---- a level of 32-B nodes to the root (the finisher's semantics) ----------
+ * hash.go:225-237 continued from `count` nodes of a level above the chunks:
+ * the same loop (odd level -> append 0^128, Hash(c[2i] || c[2i+1])) and the
+ * length mix-in of the whole list's n_total items.  The device's node-input
+ * passes (mk_dev_ssz_merkle_finish_nodes) compute this. */
+struct node_ctx {
+    const uint8_t* nodes;
+};
+static uint64_t node_chunk(void* c, uint64_t i, uint8_t* buf) {
+    memcpy(buf, ((struct node_ctx*)c)->nodes + HASHLEN * i, HASHLEN);
+    return HASHLEN;
+}
+
+int or_merkle_nodes(const uint8_t* nodes, uint64_t count, uint64_t n_total, uint8_t out[32], int nthreads) {
+    if (count == 0 || !nodes) return -1;
+    struct node_ctx c = {nodes};
+    uint8_t root[HASHLEN];
+    uint64_t rl = reduce_levels(count, HASHLEN, node_chunk, &c, 0xFFFFFFFFu, 0, root, nthreads);
+    final_hash(root, rl, n_total, out);
+    return 0;
+}
+
 /* Root of shard `shard` (chunks [shard<<H, (shard+1)<<H)) at height H of the
  * synthetic tree: the per-GPU subtree root of the sharded path.
  * A ragged last shard keeps applying the odd rule (hash(node || 0^128))

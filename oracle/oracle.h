@@ -19,6 +19,7 @@ void or_fill_splitmix(uint8_t* out, uint64_t nbytes, uint64_t seed, uint64_t wor
 int or_merkle_hash(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t out[32], int nthreads);
 int or_merkle_hash_var(const uint8_t* data, const uint64_t* offs, uint64_t n, uint8_t out[32]);
 int or_merkle_hash_gen(uint64_t n, uint32_t item_len, uint64_t seed, uint8_t out[32], int nthreads);
+int or_merkle_nodes(const uint8_t* nodes, uint64_t count, uint64_t n_total, uint8_t out[32], int nthreads);
 int or_merkle_subtree_gen(uint64_t n, uint32_t item_len, uint64_t seed, uint64_t shard,
                           uint32_t shard_height, uint8_t out[32], int nthreads);
 

@@ -59,6 +59,7 @@ def lib():
         L.or_merkle_hash.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, u8p, ctypes.c_int]
         L.or_merkle_hash_var.argtypes = [u8p, u8p, ctypes.c_uint64, u8p]
         L.or_merkle_hash_gen.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, u8p, ctypes.c_int]
+        L.or_merkle_nodes.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint64, u8p, ctypes.c_int]
         L.or_merkle_subtree_gen.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                             ctypes.c_uint64, ctypes.c_uint32, u8p, ctypes.c_int]
         L.or_deposit_trie_build.argtypes = [u8p, u8p, ctypes.c_uint64, ctypes.c_uint32, u8p, u8p]
@@ -68,7 +69,7 @@ def lib():
         L.or_merkle_root.argtypes = [u8p, u8p, ctypes.c_uint64, u8p]
         L.or_struct_roots.argtypes = [u8p, ctypes.c_uint64, ctypes.c_uint32, u8p, u8p, u8p, ctypes.c_uint32,
                                       u8p, ctypes.c_int]
-        for name in ("or_merkle_hash", "or_merkle_hash_var", "or_merkle_hash_gen",
+        for name in ("or_merkle_hash", "or_merkle_hash_var", "or_merkle_hash_gen", "or_merkle_nodes",
                      "or_merkle_subtree_gen", "or_deposit_trie_build", "or_deposit_trie_incremental",
                      "or_verify_merkle_branch",
                      "or_merkle_root"):
@@ -196,6 +197,18 @@ def tree_hash_bytes_list(elems: np.ndarray, n: int, elem_len: int, nthreads: int
 def merkle_hash_gen(n: int, item_len: int, seed: int, nthreads: int = 1) -> bytes:
     out = ctypes.create_string_buffer(32)
     rc = lib().or_merkle_hash_gen(n, item_len, seed, out, nthreads)
+    if rc != 0:
+        raise RuntimeError(rc)
+    return out.raw
+
+
+def merkle_nodes(nodes: np.ndarray, count: int, n_total: int, nthreads: int = 1) -> bytes:
+    """merkleHash continued from a level of `count` 32-B nodes, then the
+    length mix-in of n_total items (or_merkle_nodes)."""
+    nodes = np.ascontiguousarray(nodes, dtype=np.uint8).reshape(-1)
+    assert nodes.size >= 32 * count
+    out = ctypes.create_string_buffer(32)
+    rc = lib().or_merkle_nodes(_ptr(nodes), count, n_total, out, nthreads)
     if rc != 0:
         raise RuntimeError(rc)
     return out.raw

@@ -372,7 +372,7 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                 if (c) HIPCHK(hipEventRecord(c->join, c->side));
             }
             uint64_t fast_base = 0;
-            if (ps.nlock && !a.elem_len) {  // phase-locked leaf workgroups first: 4 spans each, levels == 3
+            if (ps.nlock && ps.leaf && !a.elem_len) {  // phase-locked leaf workgroups first: 4 spans each, levels == 3
                 a.wg_base = 0;
                 // persistent grid (one 1024-thread workgroup per CU) for whole trees, one group per
                 // workgroup for subtree shards (planner.cpp)
@@ -381,6 +381,12 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
                                    dim3(mk::kLockThreads), 0, st, a, ps.nlock);
                 HIPCHK(hipGetLastError());
                 fast_base = ps.nlock * 4;
+            } else if (ps.nlock && !ps.leaf) {  // phase-locked node groups first: 16 spans each, levels == 5
+                a.wg_base = 0;
+                hipLaunchKernelGGL(mk::k_node_lock, dim3(std::min<uint64_t>(ps.nlock, lock_grid_cap(st))),
+                                   dim3(mk::kLockThreads), 0, st, a, ps.nlock);
+                HIPCHK(hipGetLastError());
+                fast_base = ps.nlock * mk::kNodeLockSpans;
             }
             if (ps.nfast > fast_base) {
                 a.wg_base = fast_base;

@@ -1538,6 +1538,94 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_keccak64_lock(const uint4* 
     }
 }
 
+// Phase-locked node pass (the wide node pass of a whole tree, planner.cpp):
+// 1024-thread workgroups, one per CU, persistent.  Thread t of group g folds
+// the 16 node pairs [16 (1024 g + t), +16) -- 32 consecutive nodes, a subtree
+// -- through 5 levels in registers (16 + 8 + 4 + 2 + 1 = 31 locked
+// permutations) into output node 1024 g + t: the spans of k_reduce<NODE>
+// workgroups 16 g .. 16 g + 15 with a.levels == 5, same output order.  Pair j
+// of every lane of a wave (64 B, lanes 1 KB apart) lands in the wave's 5 KB
+// of LDS by coalesced DMA in k_keccak64_lock's stride-5 image, issued as soon
+// as pair j - 1 has been read (one permutation or more ahead); pairs j and
+// j + 1 share a 128-B line, the second read an L2 hit.  All pairs are
+// complete (no odd padding): the host launches whole groups of full pairs.
+// Stores go right after a wait, as in k_leaf_lock_sc.
+__global__ __launch_bounds__(kLockThreads, 1) void k_node_lock(ReduceArgs a, uint64_t ngroups) {
+    __shared__ uint4 buf[kLockThreads / 64][5 * 64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint4* Bw = buf[wave];
+    const uint4* in = reinterpret_cast<const uint4*>(a.items);
+    uint4* out = reinterpret_cast<uint4*>(a.out);
+    auto dma = [&](uint64_t g, uint32_t j) {
+        const uint64_t p0 = (g * kLockThreads + 64 * wave) * kNodeLockPairs + j;  // lane 0's pair j
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (uint32_t i = 0; i < 5; ++i) {
+            const uint32_t p = 64 * i + ln, m = p / 5, u = p - 5 * m;
+            __builtin_amdgcn_global_load_lds(
+                reinterpret_cast<const void*>(in + 4 * (p0 + (uint64_t)kNodeLockPairs * m) + (u < 4 ? u : 3)),
+                (__attribute__((address_space(3))) void*)(Bw + 64 * i), 16, 0, 0);
+        }
+    };
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;  // the previous group's node, stored one group late
+    uint64_t qi = 0;
+    bool pend = false;
+    uint64_t g = blockIdx.x;
+    if (g < ngroups) dma(g, 0);
+    // pair j of group g: wait for its DMA, read it, send the next pair's
+    // DMA (pair j + 1, or pair 0 of the workgroup's next group), hash it
+    auto pair = [&](uint64_t gg, uint32_t j, uint4& d0, uint4& d1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (j == 0 && pend) {
+            out[2 * qi] = q0;
+            out[2 * qi + 1] = q1;
+            pend = false;
+        }
+        const uint4 l0 = Bw[5 * lane], l1 = Bw[5 * lane + 1], r0 = Bw[5 * lane + 2], r1 = Bw[5 * lane + 3];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // read: the next pair may land
+        if (j + 1 < kNodeLockPairs)
+            dma(gg, j + 1);
+        else if (gg + gridDim.x < ngroups)
+            dma(gg + gridDim.x, 0);
+        hash_node_lock(l0, l1, r0, r1, d0, d1);
+    };
+#pragma unroll 1
+    for (; g < ngroups; g += gridDim.x) {
+        uint4 a0 = q0, a1 = q1;  // level-3 node of the even quarter (the value is never read before it is set)
+        uint4 b0 = q0, b1 = q1;  // level-4 node of the first half
+#pragma unroll 1
+        for (uint32_t k = 0; k < kNodeLockPairs / 4; ++k) {
+            uint4 l0, l1, r0, r1, e0, e1;
+            pair(g, 4 * k, l0, l1);
+            pair(g, 4 * k + 1, r0, r1);
+            hash_node_lock(l0, l1, r0, r1, e0, e1);
+            pair(g, 4 * k + 2, l0, l1);
+            pair(g, 4 * k + 3, r0, r1);
+            hash_node_lock(l0, l1, r0, r1, l0, l1);
+            hash_node_lock(e0, e1, l0, l1, e0, e1);  // level 3
+            if ((k & 1) == 0) {
+                a0 = e0;
+                a1 = e1;
+            } else {
+                hash_node_lock(a0, a1, e0, e1, e0, e1);  // level 4
+                if (k == 1) {
+                    b0 = e0;
+                    b1 = e1;
+                } else {
+                    hash_node_lock(b0, b1, e0, e1, q0, q1);  // level 5: the thread's output node
+                }
+            }
+        }
+        qi = g * kLockThreads + threadIdx.x;
+        pend = true;
+    }
+    if (pend) {
+        out[2 * qi] = q0;
+        out[2 * qi + 1] = q1;
+    }
+}
+
 // n messages of fixed msg_len bytes (any length / alignment).
 __global__ __launch_bounds__(256) void k_keccak_fixed(const uint8_t* __restrict__ in, uint64_t n, uint32_t msg_len,
                                                       uint4* __restrict__ out) {

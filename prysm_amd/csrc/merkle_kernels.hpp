@@ -75,6 +75,8 @@ __global__ void k_wave3(ReduceArgs a);
 __global__ void k_final_small(const uint8_t* items, uint64_t total, uint64_t n, uint8_t* out);
 __global__ void k_keccak64(const uint4* in, uint64_t n, uint4* out);
 __global__ void k_keccak64_lock(const uint4* in, uint64_t n, uint4* out);  // any n (a partial last group)
+// phase-locked node pass: ngroups whole groups of 1024 x kNodeLockPairs complete node pairs, persistent grid
+__global__ void k_node_lock(ReduceArgs a, uint64_t ngroups);
 #define MK_K64_LOCK 1
 __global__ void k_keccak_fixed(const uint8_t* in, uint64_t n, uint32_t msg_len, uint4* out);
 __global__ void k_keccak_var(const uint8_t* in, const uint64_t* offs, uint64_t n, uint4* out);

@@ -16,6 +16,13 @@ constexpr uint32_t kMidThreads = 1024;               // largest k_wave3: 16 wave
 // Wide leaf passes of full windows run the phase-locked k_leaf_lock_sc
 // (merkle_kernels.hip, planner.cpp) instead of k_reduce's fused form.
 #define MK_LEAF_LOCK 1
+// Wide node passes of whole trees run the phase-locked k_node_lock: 16 node
+// pairs per thread folded 5 levels in registers (1024-thread workgroups of
+// 16 k_reduce spans each, the same output order).
+constexpr uint32_t kNodeLockPairs = 16;
+constexpr uint32_t kNodeLockLevels = 5;
+constexpr uint64_t kNodeLockSpans = 16;  // k_reduce node spans (2 * 2 * kReduceThreads pairs) per group
+static_assert(kNodeLockSpans * 4 * kReduceThreads == 1024ull * kNodeLockPairs, "a group = 16 spans");
 #ifndef MK_LOCK_BARS
 #define MK_LOCK_BARS 2  // s_barriers per locked Keccak round (keccak_dev.hpp round_asm)
 #endif

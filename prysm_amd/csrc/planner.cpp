@@ -67,6 +67,14 @@ constexpr bool kLeafLock = MK_LEAF_LOCK != 0;  // plan_types.hpp
 constexpr uint64_t kLeafLockMinC1 = 1ull << MK_LEAF_LOCK_MIN_LOG2;  // windows (first-level nodes)
 constexpr uint32_t kLockLevels = 3;
 constexpr uint64_t kLockSpans = 4;  // k_reduce spans (1024 windows) per k_leaf_lock_sc workgroup
+// Phase-locked node pass (k_node_lock): a wide node pass of complete pairs
+// runs whole multiples of kNodeLockGroupMul groups of 16 k_reduce spans
+// (16,384 pairs) each, one group per CU at a time; a pass with fewer groups
+// than CUs keeps k_reduce, which spreads over every CU.  One-process A/B at
+// 2^28 (profiles/r05/node_lock/): whole tree 9.004 -> 8.871 ms (the node pass
+// 0.836 -> 0.689 ms by rocprof), 9 interleaved rounds.
+constexpr uint64_t kNodeLockGroupMul = 256;
+#define MK_NODE_LOCK 1
 
 uint32_t ilog2(uint64_t v) {
     uint32_t l = 0;
@@ -183,6 +191,11 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
                           a.c1_full >= kLeafLockMinC1 && remaining > kLockLevels &&
                           a.c1_full / span >= kLockSpans;
         if (lock) lv = kLockLevels;
+        const uint64_t nodelock = (MK_NODE_LOCK && !leaf && !wave && !final_pass && ni == 2 && remaining > kNodeLockLevels &&
+                                   (in_slot >= 0 || aligned16))
+                                      ? (a.c1_full / span) / kNodeLockSpans / kNodeLockGroupMul * kNodeLockGroupMul
+                                      : 0;
+        if (nodelock) lv = kNodeLockLevels;
         for (uint32_t l = 1; l < lv; ++l) {  // fused levels above the first
             if (c <= 1 && !pad_at_one) break;
             perms += (double)(c / 2) + (c % 2 ? 2.0 : 0.0);
@@ -201,7 +214,7 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         ps.nwg = ceil_div(c1, span);
         ps.nfast = wave ? 0 : std::min<uint64_t>(ps.nwg, a.c1_full / span);
         ps.ni = ni;
-        ps.nlock = lock ? ps.nfast / kLockSpans : 0;
+        ps.nlock = lock ? ps.nfast / kLockSpans : nodelock;
         // a shard of a multi-GPU tree shares its device with the RCCL
         // all-gather and the side-stream passes of the previous step: one
         // group per workgroup there, so a CU held by another kernel delays a

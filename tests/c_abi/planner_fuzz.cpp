@@ -28,6 +28,7 @@ using namespace mk;
 // Replays a plan's node counts: pass p turns cin into c1 = ceil(cin/2)
 // (1 when cin == 1 and no pad_at_one), then `levels - 1` more halvings.
 static uint64_t g_lock_passes = 0;
+static uint64_t g_node_lock_passes = 0;
 
 static uint64_t replay(const Plan& p, uint64_t nchunks, bool pad) {
     uint64_t c = nchunks;
@@ -44,10 +45,16 @@ static uint64_t replay(const Plan& p, uint64_t nchunks, bool pad) {
             c = ceil_div(c, 2);
         }
         if (ps.out_ws >= 0) REQUIRE(p.slot_nodes[ps.out_ws] >= c);
-        if (ps.nlock) {  // k_leaf_lock: whole groups of 4 full spans, exactly 3 levels, never the final pass
+        if (ps.nlock && ps.leaf) {  // k_leaf_lock: whole groups of 4 full spans, exactly 3 levels, never the final pass
             ++g_lock_passes;
-            REQUIRE(ps.leaf && !ps.wave && !ps.sp && ps.ni == 2 && !ps.a.finalize && ps.a.levels == 3);
+            REQUIRE(!ps.wave && !ps.sp && ps.ni == 2 && !ps.a.finalize && ps.a.levels == 3);
             REQUIRE(4 * ps.nlock <= ps.nfast && ps.nfast * 2 * ps.ni * kReduceThreads <= ps.a.c1_full);
+        }
+        if (ps.nlock && !ps.leaf) {  // k_node_lock: whole multiples of 256 groups of 16 full spans, exactly 5 levels
+            ++g_node_lock_passes;
+            REQUIRE(!ps.wave && !ps.sp && ps.ni == 2 && !ps.a.finalize && ps.a.levels == kNodeLockLevels);
+            REQUIRE(ps.nlock % 256 == 0 && kNodeLockSpans * ps.nlock <= ps.nfast);
+            REQUIRE(ps.nlock * 1024 * kNodeLockPairs <= ps.a.c1_full && ps.a.c1_full == ps.a.cin / 2);
         }
         REQUIRE(ps.nfast <= ps.nwg);
         REQUIRE(ps.nwg >= 1);
@@ -155,6 +162,25 @@ int main(int argc, char** argv) {
         const uint64_t cap = pick(1, 1ull << 20);
         for (uint32_t d = 0; d < 33; ++d) REQUIRE(trie_level_off(cap, d + 1) == trie_level_off(cap, d) + trie_count(cap, d));
     }
+    // wide node passes (k_node_lock): whole trees of 2^27..2^29 32-B items and
+    // node-input plans of >= 2^23 nodes, ragged and aligned; planning only
+    const uint64_t wide[] = {1ull << 27, (1ull << 28) - 1, 1ull << 28, (1ull << 28) + 5, 3ull << 27, 1ull << 29};
+    for (uint64_t n : wide) {
+        Plan wp;
+        REQUIRE(make_plan(n, 32, false, 0, false, true, wp) == MK_OK);
+        REQUIRE(replay(wp, ceil_div(n, 4), false) == 1);
+        const uint64_t cnt = n / 32 + (n & 7);
+        Plan np;
+        REQUIRE(make_plan(cnt, 32, false, 0, false, true, np, true, 0, n) == MK_OK);
+        REQUIRE(replay(np, cnt, false) == 1);
+        REQUIRE(make_plan(cnt, 32, false, 0, false, false, np, true, 0, n) == MK_OK);  // unaligned: no lock
+        REQUIRE(np.passes[0].nlock == 0 && replay(np, cnt, false) == 1);
+    }
+    {
+        Plan wp;  // the 2^28 headline: leaf lock, then one node-lock pass of 256 groups
+        REQUIRE(make_plan(1ull << 28, 32, false, 0, false, true, wp) == MK_OK);
+        REQUIRE(wp.passes.size() >= 2 && wp.passes[1].nlock == 256 && wp.passes[1].nfast == 16 * 256);
+    }
     // invalid inputs are rejected, not crashed on
     Plan p;
     REQUIRE(make_plan(5, 0, false, 0, false, true, p) == MK_EINVAL);
@@ -164,7 +190,7 @@ int main(int argc, char** argv) {
     uint32_t h, ne;
     uint64_t b[2];
     REQUIRE(shard_plan(5, 32, 0, &h, &ne, b) == MK_EINVAL);
-    std::fprintf(stderr, "planner fuzz: %d cases clean (%llu phase-locked leaf passes)\n", cases,
-                 (unsigned long long)g_lock_passes);
+    std::fprintf(stderr, "planner fuzz: %d cases clean (%llu phase-locked leaf passes, %llu node passes)\n", cases,
+                 (unsigned long long)g_lock_passes, (unsigned long long)g_node_lock_passes);
     return 0;
 }

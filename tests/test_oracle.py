@@ -243,3 +243,32 @@ def test_tree_hash_bytes_list_oracle_routes():
                             for lo in range(0, 5000, 1000)])
     assert np.array_equal(one, parts)
     assert np.array_equal(O.elem_digests(items, 5000, 32, chunk=777), one)
+
+
+@pytest.mark.parametrize("count", [1, 2, 3, 5, 8, 13, 64, 1001])
+def test_merkle_nodes_oracle(count):
+    """or_merkle_nodes (a level of 32-B nodes to the root, the device
+    finisher's semantics) against the literal loop of hash.go:225-237 with
+    the pure-Python digest, and, from a flat tree's level-1 nodes, against
+    the whole flat tree's root."""
+    rng = np.random.default_rng(100 + count)
+    nodes = rng.integers(0, 256, 32 * count, dtype=np.uint8)
+    n_total = int(rng.integers(1, 1 << 40))
+    chunks = [bytes(nodes[32 * i:32 * i + 32]) for i in range(count)]
+    while len(chunks) > 1:
+        if len(chunks) % 2:
+            chunks.append(bytes(128))
+        chunks = [O.keccak256(chunks[i] + chunks[i + 1]) for i in range(0, len(chunks), 2)]
+    want = O.py_keccak256(chunks[0] + struct.pack("<Q", n_total) + bytes(24))
+    assert O.merkle_nodes(nodes, count, n_total) == want
+    assert O.merkle_nodes(nodes, count, n_total, nthreads=4) == want
+    # level-1 nodes of a flat 32-B tree (2 x 128-B chunks per window; the last
+    # window of an odd chunk count padded with 0^128) -> the flat root
+    n = 8 * count - 3 if count > 1 else 5
+    items = O.splitmix_bytes(32 * n, 0x5EED000000000004)
+    raw = bytes(items)
+    ch = [raw[i:i + 128] for i in range(0, len(raw), 128)]
+    if len(ch) % 2:
+        ch.append(bytes(128))
+    lv1 = np.frombuffer(b"".join(O.keccak256(ch[i] + ch[i + 1]) for i in range(0, len(ch), 2)), dtype=np.uint8)
+    assert O.merkle_nodes(lv1, len(ch) // 2, n) == O.merkle_hash_flat(items, n, 32)

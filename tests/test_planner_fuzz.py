@@ -36,6 +36,7 @@ def test_planner_fuzz_sanitized(fuzz_exe, seed):
     assert "cases clean" in r.stderr
     if "leaf_lock" in fuzz_exe:
         assert " 0 phase-locked" not in r.stderr, r.stderr[-300:]
+    assert " 0 node passes" not in r.stderr, r.stderr[-300:]  # the wide k_node_lock plans
     nshard = nfront = 0
     for line in r.stdout.splitlines():
         f = line.split()
