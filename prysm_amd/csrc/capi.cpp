@@ -374,10 +374,10 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
             uint64_t fast_base = 0;
             if (ps.nlock && ps.leaf && !a.elem_len) {  // phase-locked leaf workgroups first: 4 spans each, levels == 3
                 a.wg_base = 0;
-                // persistent grid (one 1024-thread workgroup per CU) for whole trees, one group per
-                // workgroup for subtree shards (planner.cpp)
-                hipLaunchKernelGGL(mk::k_leaf_lock_sc,
-                                   dim3(ps.lock_persist ? std::min<uint64_t>(ps.nlock, lock_grid_cap(st)) : ps.nlock),
+                // persistent grid (one 1024-thread workgroup per CU), whole trees and subtree shards
+                // alike: a shard's pipelined step beside its side-stream passes measured 1.2-3.7 %
+                // faster than one group per workgroup (profiles/r05/shard_persist/)
+                hipLaunchKernelGGL(mk::k_leaf_lock_sc, dim3(std::min<uint64_t>(ps.nlock, lock_grid_cap(st))),
                                    dim3(mk::kLockThreads), 0, st, a, ps.nlock);
                 HIPCHK(hipGetLastError());
                 fast_base = ps.nlock * 4;

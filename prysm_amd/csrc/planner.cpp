@@ -62,9 +62,6 @@ constexpr uint64_t kSpreadSpan = 16;  // windows per k_spread_leaf workgroup
 // 4 windows) in 1024-thread workgroups whose Keccak rounds hold an s_barrier;
 // the next (node) pass takes the levels the leaf pass used to fuse in LDS.
 constexpr bool kLeafLock = MK_LEAF_LOCK != 0;  // plan_types.hpp
-#ifndef MK_LOCK_SUBTREE_PERSIST
-#define MK_LOCK_SUBTREE_PERSIST 0
-#endif
 #define MK_LEAF_LOCK_MIN_LOG2 20
 constexpr uint64_t kLeafLockMinC1 = 1ull << MK_LEAF_LOCK_MIN_LOG2;  // windows (first-level nodes)
 constexpr uint32_t kLockLevels = 3;
@@ -217,11 +214,6 @@ int make_plan(uint64_t n, uint32_t item_len, bool subtree, uint32_t height, bool
         ps.nfast = wave ? 0 : std::min<uint64_t>(ps.nwg, a.c1_full / span);
         ps.ni = ni;
         ps.nlock = lock ? ps.nfast / kLockSpans : nodelock;
-        // a shard of a multi-GPU tree shares its device with the RCCL
-        // all-gather and the side-stream passes of the previous step: one
-        // group per workgroup there, so a CU held by another kernel delays a
-        // few groups instead of a persistent workgroup's whole share
-        ps.lock_persist = !subtree || MK_LOCK_SUBTREE_PERSIST;
         ps.in_ws = in_slot;
         if (final_pass) {
             if (!subtree) {

@@ -55,7 +55,6 @@ struct Pass {
     uint32_t ni;  // k_reduce: window pairs per thread (span 512 * ni)
     uint64_t nlock;  // leaf: k_leaf_lock_sc workgroups (4 spans each) before the k_reduce ones (levels == 3);
                      // node: k_node_lock groups (kNodeLockSpans spans each, levels == 5)
-    bool lock_persist;  // k_leaf_lock_sc on a persistent grid (one workgroup per CU): whole trees only
     ReduceArgs a;
     int in_ws;   // -1 = user input, else ping-pong slot
     int out_ws;  // -1 = user output, else ping-pong slot
