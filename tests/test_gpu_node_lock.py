@@ -55,15 +55,17 @@ def test_finish_nodes_wide(gpu, count):
     assert bytes(root.cpu().numpy()) == want
 
 
-def test_node_frontier_wide(gpu):
-    """Subtree mode (the sharded path's node passes): a full 2^23-node level
-    to a 1024-node frontier with the odd rule kept at count 1, then the
-    finisher: equals the whole level's root."""
+@pytest.mark.parametrize("count,h", [(1 << 23, 23), ((1 << 24) - 5, 24)])
+def test_node_frontier_wide(gpu, count, h):
+    """Subtree mode (the sharded path's node passes): a 2^23-node level (256
+    locked groups) or a ragged 2^24 - 5 one (256 locked groups, then k_reduce
+    spans and an odd node) to a 1024-node frontier with the odd rule kept at
+    count 1, then the finisher: equals the whole level's root."""
     import torch
 
     from prysm_amd import device as D
 
-    count, h, k = 1 << 23, 23, 10
+    k = 10
     nodes = _nodes(gpu, count, SEED + 1)
     lvl = D.merkle_node_frontier(nodes, count, h, k, True)
     root = D.merkle_finish_nodes(lvl, 1 << k, 12345)
