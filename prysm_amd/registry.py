@@ -368,7 +368,7 @@ class StatePipeline:
 
     def flush(self) -> None:
         """Finish the last submitted state's trees (from their level-1 nodes,
-        on the side streams); a no-op when nothing is pending."""
+        on the side stream); a no-op when nothing is pending."""
         import torch
 
         if self._pending is not None:
@@ -379,7 +379,7 @@ class StatePipeline:
 
     def wait(self, stream=None) -> None:
         """Make ``stream`` (default: the current one) wait for every root
-        produced so far (both side streams)."""
+        produced so far (the side stream's work)."""
         import torch
 
         st = stream or torch.cuda.current_stream(self.dev)
