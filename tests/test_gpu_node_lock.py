@@ -73,11 +73,14 @@ def test_node_frontier_wide(gpu, count, h):
     assert bytes(root.cpu().numpy()) == O.merkle_nodes(nodes.cpu().numpy(), count, 12345, nthreads=NTHREADS)
 
 
-@pytest.mark.parametrize("n,item_len", [((1 << 28) + 12345, 32), ((1 << 28) - 31, 32)])
+@pytest.mark.parametrize("n,item_len", [((1 << 28) + 12345, 32), ((1 << 28) - 31, 32), ((1 << 29) + 7, 32),
+                                        ((1 << 26) + 5, 128)])
 def test_whole_tree_ragged(gpu, n, item_len):
-    """merkleHash of a ragged 2^28-item tree: the locked leaf pass with its
-    ragged last windows, then the locked node pass (2^23 nodes either way)
-    followed by k_reduce spans and an odd node (2^28 + 12345)."""
+    """merkleHash of ragged 8-16 GiB trees: the locked leaf pass with its
+    ragged last windows, then the locked node pass (2^23 nodes for the
+    2^28-item trees, 2^24 -- two groups per CU -- for 2^29 + 7) followed by
+    k_reduce spans and an odd node; 2^26 + 5 items of 128 B (one chunk per
+    item) reach the same node level through the other chunk packing."""
     import torch
 
     from prysm_amd import device as D
