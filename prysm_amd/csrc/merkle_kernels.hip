@@ -2011,11 +2011,11 @@ __device__ constexpr uint32_t kValLen[9] = {48, 32, 32, 8, 8, 8, 8, 8, 8};
 // second list (the balances: 128 windows per workgroup, 64 + 32 + 16 node
 // permutations), leaving 16 nodes per workgroup.  Level k sits before the field
 // permutation at position 2 (k - 2) of the 16 (4 groups x f0, f1, f2, s1);
-// level 10 at position 15 (before the last struct message): the writer
-// waits for its store in the middle of the field permutation that follows,
-// so the reader of the next level, a position or two on, loads after the
-// barriers of that wait (through L2: this CU never read those lines, and its
-// L1 was invalidated at dispatch).
+// level 10 after the group loop: the writer waits for its store at round 12
+// of the field permutation that follows its slot, and counted in barriers
+// (waves line up by barrier count, not by position) every reader loads at
+// least half a permutation after that wait (through L2: this CU never read
+// those lines, and its L1 was invalidated at dispatch).
 template <bool PREV>
 __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* __restrict__ rec, uint64_t n,
                                                                  uint4* __restrict__ roots, uint32_t gpw,
@@ -2029,10 +2029,11 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
     // this wave's slot: the registry's level my_k (waves 0-12: 2 on 0-3, 3 on
     // 4-5, 4..10 on 6..12) or the second list's (waves 13-15: levels 2, 3,
-    // 4), at position my_pos (2 (k - 2); the registry's level 10 at 15)
+    // 4), at position my_pos (2 (k - 2); the registry's level 10 at 16, after
+    // the group loop)
     const bool my_val = wv >= 13;
     const uint32_t my_k = my_val ? wv - 11u : wv < 4 ? 2u : wv < 6 ? 3u : wv - 2u;
-    const uint32_t my_pos = my_k == 10 ? 15u : 2u * (my_k - 2u);
+    const uint32_t my_pos = my_k == 10 ? 16u : 2u * (my_k - 2u);
     auto prev_slot = [&] {
         const uint32_t k = my_k;
         const uint32_t sub = my_val ? 128u : 512u;                           // level-1 nodes per subtree
@@ -2136,10 +2137,6 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
             R[off + 0] = s.lo[0]; R[off + 1] = s.hi[0]; R[off + 2] = s.lo[1]; R[off + 3] = s.hi[1];
             R[off + 4] = s.lo[2]; R[off + 5] = s.hi[2]; R[off + 6] = s.lo[3]; R[off + 7] = s.hi[3];
         }
-        // the registry's level 10 (wave 12) before the last group's struct
-        // message: it reads level 9, whose writer waited in the field-2
-        // permutation just before; nothing in this launch reads it
-        if (slots && my_pos == 15u && pos0 == 12u) prev_slot();
         // struct message (hash.go:141-159): the digests of fields 0..2, then
         // the six uint64 raw: 36 dwords = block 1 (34) + 2 dwords of block 2
         State s;
@@ -2171,6 +2168,14 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
         qi = g * kLockThreads + threadIdx.x;
         pend = true;
     }
+    // the registry's level 10 (wave 12) after the loop.  Waves line up by
+    // barrier count: the level-9 writer (wave 11) stores at the end of its
+    // slot permutation (its 18th of 21) and waits for the store at round 12 of
+    // the next (group 3's f2); wave 12 runs f2 as its 18th, the two struct
+    // permutations as its 19th-20th and loads level 9 at the start of its
+    // 21st, 1.5 permutations after that wait (before the loop's end it would
+    // load at the writer's store).  Nothing in this launch reads it.
+    if (slots && my_pos == 16u) prev_slot();
     if (pend && qi < n) {
         roots[2 * qi] = q0;
         roots[2 * qi + 1] = q1;

@@ -62,7 +62,10 @@ constexpr uint64_t kSpreadSpan = 16;  // windows per k_spread_leaf workgroup
 // 4 windows) in 1024-thread workgroups whose Keccak rounds hold an s_barrier;
 // the next (node) pass takes the levels the leaf pass used to fuse in LDS.
 constexpr bool kLeafLock = MK_LEAF_LOCK != 0;  // plan_types.hpp
+// tests/test_planner_fuzz.py overrides it (-D) to reach the locked plan at fuzz sizes
+#ifndef MK_LEAF_LOCK_MIN_LOG2
 #define MK_LEAF_LOCK_MIN_LOG2 20
+#endif
 constexpr uint64_t kLeafLockMinC1 = 1ull << MK_LEAF_LOCK_MIN_LOG2;  // windows (first-level nodes)
 constexpr uint32_t kLockLevels = 3;
 constexpr uint64_t kLockSpans = 4;  // k_reduce spans (1024 windows) per k_leaf_lock_sc workgroup

@@ -15,14 +15,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 # the default build, and one with the phase-locked leaf pass (k_leaf_lock_sc)
-# enabled down to 2^12 windows so the fuzz sizes reach it
+# enabled down to 2^12 windows so the fuzz sizes reach it (-Werror: an
+# override the source ignores, a redefined macro, fails the build)
 @pytest.fixture(scope="module", params=[(), ("-DMK_LEAF_LOCK=1", "-DMK_LEAF_LOCK_MIN_LOG2=12")],
                 ids=["default", "leaf_lock"])
 def fuzz_exe(tmp_path_factory, request):
     out = str(tmp_path_factory.mktemp("fuzz") / ("planner_fuzz_" + ("leaf_lock" if request.param else "default")))
     csrc = os.path.join(ROOT, "prysm_amd", "csrc")
     subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
-                    "-fno-omit-frame-pointer", *request.param, "-I" + csrc, "-I" + os.path.join(ROOT, "include"),
+                    "-fno-omit-frame-pointer", "-Werror", *request.param, "-I" + csrc, "-I" + os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "c_abi", "planner_fuzz.cpp"), os.path.join(csrc, "planner.cpp"),
                     "-o", out], check=True)
     return out
