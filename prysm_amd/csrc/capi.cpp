@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -29,6 +30,11 @@ namespace {
 
 #define MK_SIDE_PRIO 1
 constexpr bool kSidePrio = MK_SIDE_PRIO != 0;  // library side/copy streams at high priority
+// a whole trie's top (every level from the first of <= 2^20 nodes) in one
+// launch, k_trie_top_fused (0: the k_trie_level / k_trie_top3 / k_trie_spread chain)
+#ifndef MK_TRIE_TOP_FUSED
+#define MK_TRIE_TOP_FUSED 1
+#endif
 #define MK_TRIE_TOP_MAX_LOG2 17
 constexpr uint64_t kTrieTopMax = 1ull << MK_TRIE_TOP_MAX_LOG2;  // trie levels at or below: k_trie_top3
 constexpr uint64_t kTrieTopWgs = 256;
@@ -1067,15 +1073,39 @@ int launch_trie_spread(void* d_levels, uint64_t cap, uint32_t d, uint64_t lo, ui
 // nt_max / spread_max: the largest k_trie_top3 workgroup and k_trie_spread
 // wave count (256 / 4: at most one wave per SIMD, which fits beside a
 // resident k_trie_rec_lock<1024, 4, true> workgroup of 104 VGPRs).
+// Arrival-counter slot of the next fused-top launch (mk::g_arrive, round
+// robin; the kernel's last workgroup resets it).
+uint32_t next_arrive_slot() {
+    static std::atomic<uint32_t> next{0};
+    return next.fetch_add(1, std::memory_order_relaxed) % mk::kArriveSlots;
+}
+
 int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from, uint32_t d_to, uint32_t depth,
                       void* d_root32, hipStream_t st, uint32_t nt_max = mk::kMidThreads,
-                      uint32_t spread_max = mk::kSpreadWavesMax) {
+                      uint32_t spread_max = mk::kSpreadWavesMax, bool fused = false) {
     // Wide levels: one launch per level (every lane busy); the narrow top
     // (<= 2^17 nodes) plus the zero-sibling tail: k_trie_top3 (bit-interleaved
     // lane pairs), log2(NT) levels per workgroup of NT inputs, the last
-    // launch to the top.
+    // launch to the top.  `fused` (a whole trie alone on the stream): every
+    // level from the first of <= 2^20 nodes to the root in one launch
+    // (k_trie_top_fused).
     uint64_t c = mk::trie_count(n, d_from);
     uint32_t d = d_from;
+    if (fused && MK_TRIE_TOP_FUSED && d_to == depth && d_root32) {
+        constexpr uint64_t NT = 1024;
+        while (d < d_to && c > NT * NT) {
+            const uint64_t cn = (c + 1) / 2;
+            hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(cn, 256)), dim3(256), 0, st,
+                               (const uint4*)trie_level(d_levels, cap, d), c, trie_level(d_levels, cap, d + 1));
+            HIPCHK(hipGetLastError());
+            c = cn;
+            ++d;
+        }
+        hipLaunchKernelGGL(mk::k_trie_top_fused<NT>, dim3(ceil_div(c, NT)), dim3(NT), 0, st, (uint32_t*)d_levels, cap,
+                           c, d, depth, (uint32_t*)d_root32, next_arrive_slot());
+        HIPCHK(hipGetLastError());
+        return MK_OK;
+    }
     while (d < d_to && c > kTrieTopMax) {
         const uint64_t cn = (c + 1) / 2;
         hipLaunchKernelGGL(mk::k_trie_level, dim3(ceil_div(cn, 256)), dim3(256), 0, st,
@@ -1161,7 +1191,8 @@ int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t*
                             : 0;
     if (!ng) {
         TRY(dev_leaf_hashes(d_data, d_offs, n, fixed_len, trie_level(d_levels, cap, 0), st));
-        return trie_levels_range(d_levels, cap, n, 0, d_to, depth, d_root32, st);
+        return trie_levels_range(d_levels, cap, n, 0, d_to, depth, d_root32, st, mk::kMidThreads,
+                                 mk::kSpreadWavesMax, d_to == depth);
     }
     if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
     uint4* L[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -1177,7 +1208,8 @@ int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t*
         TRY(dev_hash_batch((const uint8_t*)d_data + done * 280, n - done, 280, L[0] + 2 * done, st));
         TRY(trie_suffix_levels(d_levels, cap, n, done, nlv, st));
     }
-    return trie_levels_range(d_levels, cap, n, nlv, d_to, depth, d_root32, st);
+    return trie_levels_range(d_levels, cap, n, nlv, d_to, depth, d_root32, st, mk::kMidThreads, mk::kSpreadWavesMax,
+                             true);
 }
 
 // A stream of tries with the previous trie's wide top in the front's

@@ -2921,6 +2921,301 @@ template __global__ void k_trie_spread<4>(uint32_t*, uint64_t, uint32_t, uint64_
 template __global__ void k_trie_spread<16>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
                                            uint32_t*, SpreadLeaves);
 
+// ----------------------------------------------------------------------------
+// Fused tree tops (round 6): every level above a complete level of a tree in
+// ONE launch, for the callers that build one tree at a time (one trie from
+// its deposits, powchain/service.go:366-386; one state root,
+// core/state/state.go:168-174), where the latency-bound levels, not the
+// throughput passes, set the call's time.  Workgroup b reduces its NT nodes
+// of the start level to one node log2(NT) levels up inside the workgroup --
+// per level, bit-interleaved lane pairs (mk::ilv) while the parents outnumber
+// the waves, one state per wave (mk::spread) after (a level of <= 16 parents
+// costs one spread permutation, ~6.3 k cycles, instead of one lane-pair
+// permutation, ~12.8 k) -- then publishes that node (write-through store,
+// drained) and bumps an arrival counter; the LAST workgroup to arrive loads
+// the published nodes and reduces them to the root.  No launch boundary, no
+// narrow one-workgroup launch waiting for the wide one.
+
+// Arrival counters of the fused tops, one per launch in flight (the host
+// hands out slots round-robin, capi.cpp next_arrive_slot); zero at module
+// load, and the last arriver of a launch resets its slot, so at most
+// kArriveSlots fused launches may be in flight on one device.
+__device__ uint32_t g_arrive[kArriveSlots];
+// Diagnostic build only (tools/top_probe.hip: -DMK_TOP_STAMPS=1): s_memtime
+// at each level of a fused top, per workgroup; never in the shipped library.
+#ifndef MK_TOP_STAMPS
+#define MK_TOP_STAMPS 0
+#endif
+#if MK_TOP_STAMPS
+__device__ uint64_t g_top_stamps[1024 * 64];
+#define TOP_STAMP(k) \
+    do { if (threadIdx.x == 0) g_top_stamps[blockIdx.x * 64 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define TOP_STAMP(k) \
+    do { } while (0)
+#endif
+
+namespace {
+
+// ilv words (e, o) of a 64-bit lane -> its plain (lo, hi) dwords
+__device__ __forceinline__ void ilv_to_plain(uint32_t e, uint32_t o, uint32_t& lo, uint32_t& hi) {
+    lo = ilv::spread16(e) | (ilv::spread16(o) << 1);
+    hi = ilv::spread16(e >> 16) | (ilv::spread16(o >> 16) << 1);
+}
+
+// One level of a fused top inside the workgroup (every thread calls it): the
+// m <= NT nodes in lds (ilv words: node k at lds[8 k + 2 w + p]) -> ceil(m/2)
+// parents at lds[8 j ..].  TRIE: K(l || r) with a missing r = 0^32, 64 B
+// (deposit_trie.go:33-38); otherwise merkleHash's rule: the unpaired last
+// node is K(l || 0^128), 160 B (hash.go:229-236).  The form follows the
+// parent count (cycles per level measured in-kernel, tools/top_probe.hip):
+//   >= NT/4 parents: one state per lane (>= one wave per SIMD; 512 parents
+//       ~20 k cycles, against ~44 k as lane pairs at four waves per SIMD);
+//   > NT/128: bit-interleaved lane pairs (mk::ilv: ~13 k cycles a level for
+//       up to one wave per SIMD; 16 parents in one wave 12.8 k, against
+//       17.8 k as 16 spread waves, four per SIMD);
+//   <= NT/128 (<= two waves per SIMD): one state per wave (mk::spread).
+// Each parent also goes to lane_out(j, d0, d1) (plain digest), pair_out(j,
+// words, p) (ilv words of a lane pair) or wave_out(j, e, o, L) (lanes 0..3
+// of the wave hold the digest's ilv words).
+template <uint32_t NT, bool TRIE, typename LaneOut, typename PairOut, typename WaveOut>
+__device__ __forceinline__ void wg_level(uint32_t* lds, uint32_t m, const spread::Lane& cst, LaneOut&& lane_out,
+                                         PairOut&& pair_out, WaveOut&& wave_out) {
+    const uint32_t tid = threadIdx.x, mn = (m + 1) / 2;
+    if (mn >= NT / 4) {  // one state per lane
+        const bool act = tid < mn;
+        const bool right = 2 * tid + 1 < m;
+        State s;
+        if (act) {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                ilv_to_plain(lds[16 * tid + 2 * w], lds[16 * tid + 2 * w + 1], s.lo[w], s.hi[w]);
+                if (right)
+                    ilv_to_plain(lds[16 * tid + 8 + 2 * w], lds[16 * tid + 8 + 2 * w + 1], s.lo[4 + w], s.hi[4 + w]);
+                else
+                    s.lo[4 + w] = s.hi[4 + w] = 0u;
+            }
+        }
+        __syncthreads();
+        if (act) {
+#pragma unroll
+            for (int w = 8; w < 25; ++w) s.lo[w] = s.hi[w] = 0u;
+            if (!TRIE && !right) {  // K(l || 0^128): block 1 = l || 0, block 2 = 0^24 || pad
+                keccak_f(s);
+                s.lo[3] ^= 1u;
+            } else {
+                s.lo[8] ^= 1u;  // byte 64
+            }
+            s.hi[16] ^= 0x80000000u;
+            keccak_f_digest(s);
+            uint4 d0, d1;
+            digest(s, d0, d1);
+            const uint32_t lo4[4] = {d0.x, d0.z, d1.x, d1.z}, hi4[4] = {d0.y, d0.w, d1.y, d1.w};
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                lds[8 * tid + 2 * w] = ilv::to_ilv(lo4[w], hi4[w], 0);
+                lds[8 * tid + 2 * w + 1] = ilv::to_ilv(lo4[w], hi4[w], 1);
+            }
+            lane_out(tid, d0, d1);
+        }
+    } else if (mn > NT / 128) {  // lane pairs
+        const uint32_t k = tid >> 1, p = tid & 1u;
+        const bool act = k < mn;
+        uint32_t a[4], b[4] = {0, 0, 0, 0};
+        bool padded = false;
+        if (act) {
+            const bool right = 2 * k + 1 < m;
+            padded = !TRIE && !right;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) a[w] = lds[16 * k + 2 * w + p];
+            if (right) {
+#pragma unroll
+                for (int w = 0; w < 4; ++w) b[w] = lds[16 * k + 8 + 2 * w + p];
+            }
+        }
+        __syncthreads();
+        if (act) {
+            uint32_t h[4];
+            hash_pair3(a, b, padded, p, h);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) lds[8 * k + 2 * w + p] = h[w];
+            pair_out(k, h, p);
+        }
+    } else {  // one parent per wave
+        const uint32_t w = tid >> 6, L = tid & 63u;
+        const uint32_t i = cst.i;
+        uint32_t e = 0u, o = 0u;
+        if (w < mn) {  // wave-uniform
+            const bool right = 2 * w + 1 < m;
+            if (i < 4u) {
+                e = lds[16 * w + 2 * i];
+                o = lds[16 * w + 2 * i + 1];
+            } else if (i < 8u && right) {
+                e = lds[16 * w + 8 + 2 * (i - 4u)];
+                o = lds[16 * w + 8 + 2 * (i - 4u) + 1];
+            }
+            if (!TRIE && !right) {  // K(l || 0^128): 160 bytes, two blocks
+                spread::keccak_f(e, o, cst);
+                if (i == 3u) e ^= 1u;
+            } else if (i == 8u) {
+                e ^= 1u;
+            }
+            if (i == 16u) o ^= 0x80000000u;
+            spread::keccak_f(e, o, cst);
+        }
+        __syncthreads();
+        if (w < mn && L < 4u) {
+            lds[8 * w + 2 * L] = e;
+            lds[8 * w + 2 * L + 1] = o;
+            wave_out(w, e, o, L);
+        }
+    }
+    __syncthreads();
+}
+
+// plain node j of `in` (32 B) -> lds as ilv words, thread t loading node t;
+// SC1: agent-scope loads (nodes another CU published in this launch)
+template <bool SC1>
+__device__ __forceinline__ void wg_load_nodes(uint32_t* lds, const uint32_t* in, uint32_t m) {
+    const uint32_t t = threadIdx.x;
+    if (t < m) {
+        const uint64_t* q = reinterpret_cast<const uint64_t*>(in) + 4 * (uint64_t)t;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint64_t v = SC1 ? __hip_atomic_load(q + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : q[w];
+            lds[8 * t + 2 * w] = ilv::to_ilv((uint32_t)v, (uint32_t)(v >> 32), 0);
+            lds[8 * t + 2 * w + 1] = ilv::to_ilv((uint32_t)v, (uint32_t)(v >> 32), 1);
+        }
+    }
+    __syncthreads();
+}
+
+// node 0 of lds (ilv words) -> plain 32 B at out, by wave 0's lanes 0..3;
+// SC1: a write-through store, drained, so another CU may read it after the
+// arrival counter says so
+template <bool SC1>
+__device__ __forceinline__ void wg_store_node0(const uint32_t* lds, uint32_t* out) {
+    const uint32_t tid = threadIdx.x;
+    if (tid < 4u) {
+        const uint32_t e = lds[2 * tid], o = lds[2 * tid + 1];
+        const uint64_t v = (uint64_t)(ilv::spread16(e) | (ilv::spread16(o) << 1)) |
+                           ((uint64_t)(ilv::spread16(e >> 16) | (ilv::spread16(o >> 16) << 1)) << 32);
+        uint64_t* q = reinterpret_cast<uint64_t*>(out) + tid;
+        if (SC1)
+            __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            *q = v;
+    }
+    if (SC1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Arrival of this workgroup (after its published node's store drained); true
+// in every thread of the last workgroup of the grid, which also resets the slot.
+__device__ __forceinline__ bool wg_arrive_last(uint32_t slot, uint32_t* flag) {
+    if (threadIdx.x == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(&g_arrive[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = old + 1 == gridDim.x;
+        if (last) __hip_atomic_store(&g_arrive[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return *flag != 0u;
+}
+
+}  // namespace
+
+// The deposit trie above its complete level d0 (c0 nodes) up to the root, in
+// one launch: workgroup b takes level-d0 nodes [NT b, NT b +
+// NT) up to level d0 + log2(NT) (every node stored: GenerateMerkleBranch reads
+// them), the last workgroup to arrive the rest, including the zero-sibling
+// levels (deposit_trie.go:33-38) and the root.  grid = ceil(c0 / NT) <= NT.
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void k_trie_top_fused(uint32_t* __restrict__ levels, uint64_t cap, uint64_t c0,
+                                                       uint32_t d0, uint32_t depth, uint32_t* __restrict__ root_out,
+                                                       uint32_t slot) {
+    constexpr uint32_t kLog = NT == 1024 ? 10 : NT == 512 ? 9 : NT == 256 ? 8 : NT == 128 ? 7 : 6;
+    __shared__ uint32_t lds[8 * NT];
+    __shared__ uint32_t flag;
+    uint64_t off = 0, capd = cap;  // node offset and capacity of level d
+    for (uint32_t k = 0; k < d0; ++k) {
+        off += capd;
+        capd = (capd + 1) / 2;
+    }
+    const uint32_t dtop = depth - d0 < kLog ? depth : d0 + kLog;  // this workgroup's part ends at level dtop
+    uint64_t lo = (uint64_t)blockIdx.x * NT;                      // level-d node of lds[0]
+    uint32_t m = (uint32_t)(c0 - lo < NT ? c0 - lo : NT);
+    wg_load_nodes<false>(lds, levels + 8 * (off + lo), m);
+    uint32_t d = d0;
+    const uint32_t L = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const spread::Lane cst = spread::lane_consts(L);
+    uint32_t nst = 0;
+    TOP_STAMP(nst++);
+    auto run = [&](uint32_t d_end) {
+        for (; d < d_end && m > 1; ++d) {
+            TOP_STAMP(nst++);
+            uint32_t* out = levels + 8 * (off + capd + (lo >> 1));  // level d + 1, this part's first parent
+            wg_level<NT, true>(
+                lds, m, cst,
+                [&](uint32_t j, const uint4& d0, const uint4& d1) {
+                    reinterpret_cast<uint4*>(out)[2 * j] = d0;
+                    reinterpret_cast<uint4*>(out)[2 * j + 1] = d1;
+                },
+                [&](uint32_t j, const uint32_t(&h)[4], uint32_t p) { store_node3(out, j, false, p, h); },
+                [&](uint32_t j, uint32_t e, uint32_t o, uint32_t L) { spread_store_digest(e, o, L, out + 8 * j); });
+            m = (m + 1) / 2;
+            lo >>= 1;
+            off += capd;
+            capd = (capd + 1) / 2;
+        }
+        if (d < d_end) {
+            // one node left: the zero-sibling levels K(node || 0^32) as a
+            // chain on wave 0, the node kept in registers (no LDS round trip,
+            // no barrier per level)
+            const uint32_t i = cst.i;
+            uint32_t e = 0u, o = 0u;
+            if (w == 0 && i < 4u) {
+                e = lds[2 * i];
+                o = lds[2 * i + 1];
+            }
+            for (; d < d_end; ++d) {
+                TOP_STAMP(nst++);
+                if (w == 0) {
+                    if (i >= 4u) e = o = 0u;
+                    if (i == 8u) e ^= 1u;
+                    if (i == 16u) o ^= 0x80000000u;
+                    spread::keccak_f(e, o, cst);
+                    spread_store_digest(e, o, L, levels + 8 * (off + capd + (lo >> 1)));
+                }
+                lo >>= 1;
+                off += capd;
+                capd = (capd + 1) / 2;
+            }
+            if (w == 0 && L < 4u) {
+                lds[2 * L] = e;
+                lds[2 * L + 1] = o;
+            }
+            __syncthreads();
+        }
+    };
+    run(dtop);
+    if (gridDim.x > 1) {
+        // publish this part's node (level dtop, node blockIdx.x: already
+        // stored above, again write-through) and arrive
+        wg_store_node0<true>(lds, levels + 8 * (off + lo));
+        TOP_STAMP(nst++);
+        if (!wg_arrive_last(slot, &flag)) return;
+        TOP_STAMP(nst++);
+        lo = 0;
+        m = gridDim.x;
+        wg_load_nodes<true>(lds, levels + 8 * off, m);
+    }
+    run(depth);
+    wg_store_node0<false>(lds, root_out);
+    TOP_STAMP(nst++);
+}
+template __global__ void k_trie_top_fused<1024>(uint32_t*, uint64_t, uint64_t, uint32_t, uint32_t, uint32_t*,
+                                                uint32_t);
+
 // Small merkleHash leaf passes in spread form (one state per wave): a
 // workgroup of 16 waves owns 16 windows; wave w hashes window w (256 B, the
 // ragged last one, or one padded with 0^128: hash.go:205-222), then the

@@ -136,6 +136,11 @@ struct SpreadLeaves {
 template <uint32_t NW>
 __global__ void k_trie_spread(uint32_t* levels, uint64_t cap, uint32_t d0, uint64_t lo, uint64_t c, uint32_t d_end,
                               uint32_t depth, uint32_t* root_out, SpreadLeaves lv);
+// fused tree tops: arrival counter slots (one per fused launch in flight)
+constexpr uint32_t kArriveSlots = 4096;
+template <uint32_t NT>
+__global__ void k_trie_top_fused(uint32_t* levels, uint64_t cap, uint64_t c0, uint32_t d0, uint32_t depth,
+                                 uint32_t* root_out, uint32_t slot);
 template <uint32_t NW>
 __global__ void k_trie_prefix_roots(const uint4* levels, uint64_t cap, uint64_t count0, uint64_t m, uint32_t depth,
                                     uint4* roots);

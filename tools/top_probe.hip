@@ -1,0 +1,69 @@
+// Diagnostic probe: per-level timeline of the fused trie top
+// (k_trie_top_fused) from in-kernel s_memtime stamps (-DMK_TOP_STAMPS=1, a
+// build of the kernel source of its own, never the shipped library).  A
+// depth-32 trie's level-2 nodes (2^18 random, the C5 shape) reduced to the
+// root `iters` times; prints, per stamp, the median over workgroups of the
+// cycles since the workgroup's first stamp, and the last workgroup's stamps.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMK_TOP_STAMPS=1
+//        -I../prysm_amd/csrc -I../include top_probe.hip -o top_probe
+#include "../prysm_amd/csrc/merkle_kernels.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+int main(int argc, char** argv) {
+    const uint64_t n = 1u << 20, cap = n;
+    const uint32_t depth = 32, d0 = 2;
+    const int iters = argc > 1 ? atoi(argv[1]) : 5;
+    uint64_t total = 0, c = cap;
+    for (uint32_t d = 0; d <= depth; ++d) {
+        total += c;
+        c = (c + 1) / 2;
+    }
+    uint32_t *lv, *root;
+    (void)hipMalloc(&lv, total * 32);
+    (void)hipMalloc(&root, 32);
+    std::vector<uint32_t> h(total * 8);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (auto& v : h) {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        v = (uint32_t)x;
+    }
+    (void)hipMemcpy(lv, h.data(), total * 32, hipMemcpyHostToDevice);
+    const uint64_t c0 = n >> d0;
+    const uint32_t grid = (uint32_t)((c0 + 1023) / 1024);
+    std::vector<uint64_t> zero(1024 * 64, 0);
+    for (int it = 0; it < iters; ++it) {
+        if (it + 1 == iters) (void)hipMemcpyToSymbol(HIP_SYMBOL(mk::g_top_stamps), zero.data(), zero.size() * 8);
+        hipLaunchKernelGGL(mk::k_trie_top_fused<1024>, dim3(grid), dim3(1024), 0, 0, lv, cap, c0, d0, depth, root,
+                           (uint32_t)it);
+        (void)hipDeviceSynchronize();
+    }
+    std::vector<uint64_t> st(1024 * 64);
+    (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(mk::g_top_stamps), st.size() * 8);
+    // per stamp index: median over workgroups of (stamp - stamp 0) where set
+    uint64_t t0min = ~0ull;
+    for (uint32_t b = 0; b < grid; ++b) t0min = std::min(t0min, st[b * 64]);
+    printf("{\"grid\": %u, \"stamps_median_cycles\": [", grid);
+    for (int k = 0; k < 13; ++k) {
+        std::vector<uint64_t> v;
+        for (uint32_t b = 0; b < grid; ++b)
+            if (st[b * 64 + k]) v.push_back(st[b * 64 + k] - t0min);
+        std::sort(v.begin(), v.end());
+        printf("%s%llu", k ? ", " : "", v.empty() ? 0ull : (unsigned long long)v[v.size() / 2]);
+    }
+    // the last workgroup: the one with the most stamps
+    uint32_t lb = 0, best = 0;
+    for (uint32_t b = 0; b < grid; ++b) {
+        uint32_t k = 0;
+        while (k < 64 && st[b * 64 + k]) ++k;
+        if (k > best) best = k, lb = b;
+    }
+    printf("], \"last_wg\": %u, \"last_wg_cycles\": [", lb);
+    for (uint32_t k = 0; k < best; ++k) printf("%s%llu", k ? ", " : "", (unsigned long long)(st[lb * 64 + k] - t0min));
+    printf("]}\n");
+    return 0;
+}
