@@ -198,6 +198,25 @@ int mk_dev_ssz_merkle_finish_nodes(mk_call* call, const void* d_nodes, uint64_t 
 int mk_dev_ssz_merkle_finish_nodes_pair(mk_call* call, const void* d_nodes, uint64_t count, uint64_t n_total,
                                         void* d_pair_block, uint32_t slot, uint32_t epoch, void* d_ws,
                                         uint64_t ws_bytes, void* stream);
+/* One or two lists' trees above a complete node level, to the roots, in ONE
+ * launch (round 6): `count0` 32-B nodes at d_nodes0 (8-B
+ * aligned) forming one complete level of a list of `n0` items, reduced with
+ * the reference level loop (hash.go:225-236, odd -> 0^128) and mixed in
+ * (Keccak(root || le64(n0) || 0^24), :237-238); count1 == 0: d_out gets the
+ * 32-B list root.  count1 > 0: a second list (d_nodes1, count1, n1) side by
+ * side, and d_out is a pair block with mk_dev_ssz_merkle_finish_nodes_pair's
+ * semantics (list 0's root at [0, 32), list 1's at [32, 64), the struct root
+ * Keccak(d_out[0, 64)) at [64, 96) written by whichever list finishes second,
+ * `epoch` as there): the State root of BASELINE config 3 from the two trees'
+ * level-1 nodes in one call on one stream.  Each count is 1 .. 2^20; at most
+ * 4096 such launches in flight per device (arrival counters).  Workspace from
+ * mk_ssz_merkle_top_fused_workspace_bytes(count0, count1), 16-B aligned.
+ * Replaces: ssz.merkleHash's level loop (shared/ssz/hash.go:223-239) for a
+ * list whose lower levels are already built. */
+uint64_t mk_ssz_merkle_top_fused_workspace_bytes(uint64_t count0, uint64_t count1);
+int mk_dev_ssz_merkle_top_fused(mk_call* call, const void* d_nodes0, uint64_t count0, uint64_t n0,
+                                const void* d_nodes1, uint64_t count1, uint64_t n1, void* d_out, uint32_t epoch,
+                                void* d_ws, uint64_t ws_bytes, void* stream);
 /* Finisher on one device: the reference level loop over the `nroots`
  * gathered shard roots (odd -> 0^128 pad), then Keccak(root || le64(n) || 0^24). */
 int mk_dev_ssz_merkle_finish(mk_call* call, const void* d_roots, uint64_t nroots, uint64_t n_total, void* d_out32,

@@ -73,6 +73,8 @@ _SIGS = {
     "mk_ssz_merkle_finish_workspace_bytes": (_u64, [_u64]),
     "mk_dev_ssz_merkle_finish_nodes": (_int, [_cp, _vp, _u64, _u64, _vp, _vp, _u64, _vp]),
     "mk_dev_ssz_merkle_finish_nodes_pair": (_int, [_cp, _vp, _u64, _u64, _vp, _u32, _u32, _vp, _u64, _vp]),
+    "mk_ssz_merkle_top_fused_workspace_bytes": (_u64, [_u64, _u64]),
+    "mk_dev_ssz_merkle_top_fused": (_int, [_cp, _vp, _u64, _u64, _vp, _u64, _u64, _vp, _u32, _vp, _u64, _vp]),
     "mk_ssz_merkle_hash_multi": (_int, [_cp, _vp, _u64, _u32, _int, _vp, _vp]),
     "mk_dev_ssz_merkle_hash_multi": (_int, [_cp, _vp, _u64, _u32, _int, _vp, _vp]),
     "mk_ssz_struct_msg_len": (_u64, [_vp, _u32]),

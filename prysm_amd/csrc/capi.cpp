@@ -1896,6 +1896,104 @@ int mk_dev_ssz_merkle_finish_nodes(mk_call* call, const void* d_nodes, uint64_t 
     return S.done(rc ? rc : dev_finish_nodes(d_nodes, count, n_total, d_out32, d_ws, ws_bytes, (hipStream_t)stream));
 }
 
+// ---- fused list tops (k_merkle_top_fused) -------------------------------------------
+// Workgroups of NT = 1024 threads (one per CU).  Per list: nodes per
+// workgroup = the power of two that gives the list about 256 / nlists
+// workgroups, so the throughput-bound lower levels spread over the chip (two
+// lists side by side in one grid), 64..1024; a list of <= 1024 nodes runs in
+// one workgroup (no hand-off).  C3 (125,000 + 31,250 nodes): 123 + 123
+// workgroups.  (512-thread workgroups, two per CU, 245 + 245 of them:
+// C3 one state 0.5748 / 0.5819 against 0.5712 / 0.5719 ms, rejected.)
+struct TopPlan {
+    static constexpr uint32_t nt = 1024;
+    uint32_t span_log2[2] = {0, 0}, nwg[2] = {0, 0};
+    uint64_t ws = 0;
+};
+static int top_plan(const uint64_t* c, uint32_t nl, TopPlan& p) {
+    p = TopPlan();
+    for (uint32_t l = 0; l < nl; ++l) {
+        if (c[l] == 0) return fail(MK_EINVAL, "empty level");
+        if (c[l] > (1ull << 20)) return fail(MK_EINVAL, "fused top: %llu nodes > 2^20", (unsigned long long)c[l]);
+    }
+    const uint32_t lmax = 10;
+    const uint64_t target = 256 / nl;
+    for (uint32_t l = 0; l < nl; ++l) {
+        uint32_t sl = lmax;
+        if (c[l] > p.nt) {
+            sl = 6;
+            while (sl < lmax && (c[l] >> sl) >= target) ++sl;
+        }
+        p.span_log2[l] = sl;
+        p.nwg[l] = (uint32_t)ceil_div(c[l], 1ull << sl);
+        p.ws += 32 * (uint64_t)p.nwg[l];
+    }
+    p.ws = (p.ws + 255) & ~255ull;
+    return MK_OK;
+}
+
+static int launch_top_fused(const TopPlan& p, uint32_t nl, const void* const* nodes, const uint64_t* c,
+                            const uint64_t* nit, void* d_out, uint32_t epoch, void* d_ws, hipStream_t st);
+
+uint64_t mk_ssz_merkle_top_fused_workspace_bytes(uint64_t count0, uint64_t count1) {
+    const uint64_t c[2] = {count0, count1};
+    TopPlan p;
+    return top_plan(c, count1 ? 2 : 1, p) == MK_OK ? p.ws : 0;
+}
+
+int mk_dev_ssz_merkle_top_fused(mk_call* call, const void* d_nodes0, uint64_t count0, uint64_t n0,
+                                const void* d_nodes1, uint64_t count1, uint64_t n1, void* d_out, uint32_t epoch,
+                                void* d_ws, uint64_t ws_bytes, void* stream) {
+    Scope S(call);
+    int rc = bind_stream((hipStream_t)stream);
+    if (rc) return S.done(rc);
+    const uint32_t nl = count1 ? 2 : 1;
+    const uint64_t c[2] = {count0, count1};
+    const void* nodes[2] = {d_nodes0, d_nodes1};
+    const uint64_t nit[2] = {n0, n1};
+    TopPlan p;
+    rc = top_plan(c, nl, p);
+    if (rc) return S.done(rc);
+    if (!d_out || !d_ws || !d_nodes0 || (nl == 2 && !d_nodes1)) return S.done(fail(MK_EINVAL, "null pointer"));
+    if (ws_bytes < p.ws) return S.done(fail(MK_ENOMEM, "workspace too small: %llu < %llu", (unsigned long long)ws_bytes,
+                                            (unsigned long long)p.ws));
+    if ((uintptr_t)d_nodes0 % 8 || (uintptr_t)d_nodes1 % 8 || (uintptr_t)d_ws % 16)
+        return S.done(fail(MK_EINVAL, "nodes not 8-B aligned or workspace not 16-B aligned"));
+    if (nl == 2) {
+        if (epoch == 0 || epoch >= (1u << 30))
+            return S.done(fail(MK_EINVAL, "pair epoch %u out of range (1..2^30-1)", epoch));
+        if ((uintptr_t)d_out % 16) return S.done(fail(MK_EINVAL, "pair block not 16-B aligned"));
+    }
+    return S.done(launch_top_fused(p, nl, nodes, c, nit, d_out, epoch, d_ws, (hipStream_t)stream));
+}
+
+static int launch_top_fused(const TopPlan& p, uint32_t nl, const void* const* nodes, const uint64_t* c,
+                            const uint64_t* nit, void* d_out, uint32_t epoch, void* d_ws, hipStream_t st) {
+    if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
+    mk::MerkleTopArgs a{};
+    a.nlists = nl;
+    a.pair = nl == 2 ? (uint32_t*)d_out : nullptr;
+    a.epoch = epoch;
+    uint32_t wg = 0;
+    uint32_t* sub = (uint32_t*)d_ws;
+    for (uint32_t l = 0; l < nl; ++l) {
+        mk::MerkleTopList& t = a.l[l];
+        t.nodes = (const uint4*)nodes[l];
+        t.c = c[l];
+        t.n_items = nit[l];
+        t.sub = sub;
+        t.out = nl == 2 ? (uint32_t*)d_out + 8 * l : (uint32_t*)d_out;
+        t.wg0 = wg;
+        t.nwg = p.nwg[l];
+        t.span_log2 = p.span_log2[l];
+        t.slot = next_arrive_slot();
+        wg += t.nwg;
+        sub += 8 * t.nwg;
+    }
+    hipLaunchKernelGGL(mk::k_merkle_top_fused<1024>, dim3(wg), dim3(1024), 0, st, a);
+    HIPCHK(hipGetLastError());
+    return MK_OK;
+}
+
 int mk_dev_ssz_merkle_finish_nodes_pair(mk_call* call, const void* d_nodes, uint64_t count, uint64_t n_total,
                                         void* d_pair_block, uint32_t slot, uint32_t epoch, void* d_ws,
                                         uint64_t ws_bytes, void* stream) {

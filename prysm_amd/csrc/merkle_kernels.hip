@@ -1044,10 +1044,12 @@ __device__ __forceinline__ void hash_pair3(const uint32_t (&l)[4], const uint32_
 #pragma unroll 1
     for (int k = 0; k < nperm; ++k) {
         if (k == nperm - 1) {  // bit 0 of a lane is even (p = 0), bit 63 odd (p = 1)
-            if (p == 0)
-                s.v[padded ? 3 : 8] ^= 1u;
-            else
+            if (p == 1)
                 s.v[16] ^= 0x80000000u;
+            else if (padded)  // (two static indices: a runtime one sent the state to scratch)
+                s.v[3] ^= 1u;
+            else
+                s.v[8] ^= 1u;
         }
         ilv::keccak_f(s, p);
     }
@@ -2073,13 +2075,23 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     // (every wave still runs the same permutations and barriers) and store nothing
     const uint64_t ngroups = (n + kLockThreads - 1) / kLockThreads;
     const uint64_t last_unit = n * (kRecLen / 16) - 1;
-    // instructions [i0, i1) of the kNinstr (issued in parts)
+    // instructions [i0, i1) of the kNinstr (issued in parts).  Record m of
+    // the wave sits in 16-B slots [10 m, 10 m + 10) rotated by one unit when
+    // bit 3 of m is set (unit u in slot 10 m + (u + rot) mod 10): a
+    // ds_read_b128 of one unit by 16 consecutive lanes then hits 16 distinct
+    // 16-B bank groups (lanes 0-7 the even ones, 8-15 the odd ones) where the
+    // plain 160-B stride put lanes l and l + 8 on one (1.63 M
+    // SQ_LDS_BANK_CONFLICT per launch, profiles/r05/pmc/); the copy stays
+    // one contiguous 1-KB LDS write per instruction, each lane fetching the
+    // unit its slot holds
     auto dma = [&](uint64_t g, uint32_t i0 = 0, uint32_t i1 = kNinstr) {
         const uint64_t u0 = (g * kLockThreads + 64 * wave) * (kRecLen / 16);
         const uint4* src = reinterpret_cast<const uint4*>(rec);
 #pragma unroll
         for (uint32_t i = i0; i < i1; ++i) {
-            const uint64_t u = u0 + 64 * i + lane;
+            const uint32_t sl = 64 * i + lane, m = sl / 10u, v = sl - 10u * m;
+            const uint32_t rot = (m >> 3) & 1u;
+            const uint64_t u = u0 + 10u * m + (v >= rot ? v - rot : v + 10u - rot);
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (u < last_unit ? u : last_unit)),
                                              (__attribute__((address_space(3))) void*)(Bw + 256 * i), 16, 0,
                                              kSideAux);
@@ -2096,9 +2108,12 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     // the previous state's slots run in workgroups of exactly gpw == 4 groups
     // (uniform over the workgroup: all its waves run the same permutations)
     const bool slots = PREV && gpw == 4 && g_end - g_begin == 4;
+    // this lane's record: units 0..8 at R (rotated), unit 9 at R9
+    const uint32_t rot = (lane >> 3) & 1u;
+    uint32_t* const R = Bw + lane * kRw + 4u * rot;
+    const uint32_t* const R9 = Bw + lane * kRw + (rot ? 0u : 36u);
 #pragma unroll 1
     for (; g < g_end; g += g_step) {
-        uint32_t* R = Bw + lane * kRw;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wave's records have landed
         if (pend && qi < n) {
             roots[2 * qi] = q0;
@@ -2142,7 +2157,9 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
         State s;
 #pragma unroll
         for (int q = 0; q < 34; ++q) {
-            const uint32_t v = q < 24 ? R[kValOff[q / 8] / 4 + q % 8] : R[kValOff[3] / 4 + (q - 24)];
+            // the six uint64 are dwords 28..39: units 7, 8 and (dwords 36..39) 9
+            const uint32_t v = q < 24 ? R[kValOff[q / 8] / 4 + q % 8]
+                                      : (q < 32 ? R[kValOff[3] / 4 + (q - 24)] : R9[q - 32]);
             if (q & 1)
                 s.hi[q / 2] = v;
             else
@@ -2150,7 +2167,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
         }
 #pragma unroll
         for (int k = 17; k < 25; ++k) s.lo[k] = s.hi[k] = 0;
-        const uint32_t t0 = R[kValOff[3] / 4 + 10], t1 = R[kValOff[3] / 4 + 11];
+        const uint32_t t0 = R9[2], t1 = R9[3];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // record read: the next group's copy may land
         // the next group's copy in three parts over the first struct
         // permutation, not one burst of 16 waves' DMA (the
@@ -2969,8 +2986,8 @@ __device__ __forceinline__ void ilv_to_plain(uint32_t e, uint32_t o, uint32_t& l
 // (deposit_trie.go:33-38); otherwise merkleHash's rule: the unpaired last
 // node is K(l || 0^128), 160 B (hash.go:229-236).  The form follows the
 // parent count (cycles per level measured in-kernel, tools/top_probe.hip):
-//   >= NT/4 parents: one state per lane (>= one wave per SIMD; 512 parents
-//       ~20 k cycles, against ~44 k as lane pairs at four waves per SIMD);
+//   >= 256 parents: one state per lane (>= one wave per SIMD; 512 parents
+//       ~39 k cycles, against ~44 k as lane pairs at four waves per SIMD);
 //   > NT/128: bit-interleaved lane pairs (mk::ilv: ~13 k cycles a level for
 //       up to one wave per SIMD; 16 parents in one wave 12.8 k, against
 //       17.8 k as 16 spread waves, four per SIMD);
@@ -2982,7 +2999,7 @@ template <uint32_t NT, bool TRIE, typename LaneOut, typename PairOut, typename W
 __device__ __forceinline__ void wg_level(uint32_t* lds, uint32_t m, const spread::Lane& cst, LaneOut&& lane_out,
                                          PairOut&& pair_out, WaveOut&& wave_out) {
     const uint32_t tid = threadIdx.x, mn = (m + 1) / 2;
-    if (mn >= NT / 4) {  // one state per lane
+    if (mn >= 256) {  // one state per lane
         const bool act = tid < mn;
         const bool right = 2 * tid + 1 < m;
         State s;
@@ -3110,11 +3127,11 @@ __device__ __forceinline__ void wg_store_node0(const uint32_t* lds, uint32_t* ou
 }
 
 // Arrival of this workgroup (after its published node's store drained); true
-// in every thread of the last workgroup of the grid, which also resets the slot.
-__device__ __forceinline__ bool wg_arrive_last(uint32_t slot, uint32_t* flag) {
+// in every thread of the last of `total` workgroups, which also resets the slot.
+__device__ __forceinline__ bool wg_arrive_last(uint32_t slot, uint32_t total, uint32_t* flag) {
     if (threadIdx.x == 0) {
         const uint32_t old = __hip_atomic_fetch_add(&g_arrive[slot], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = old + 1 == gridDim.x;
+        const bool last = old + 1 == total;
         if (last) __hip_atomic_store(&g_arrive[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *flag = last ? 1u : 0u;
     }
@@ -3203,7 +3220,7 @@ __global__ __launch_bounds__(NT) void k_trie_top_fused(uint32_t* __restrict__ le
         // stored above, again write-through) and arrive
         wg_store_node0<true>(lds, levels + 8 * (off + lo));
         TOP_STAMP(nst++);
-        if (!wg_arrive_last(slot, &flag)) return;
+        if (!wg_arrive_last(slot, gridDim.x, &flag)) return;
         TOP_STAMP(nst++);
         lo = 0;
         m = gridDim.x;
@@ -3215,6 +3232,57 @@ __global__ __launch_bounds__(NT) void k_trie_top_fused(uint32_t* __restrict__ le
 }
 template __global__ void k_trie_top_fused<1024>(uint32_t*, uint64_t, uint64_t, uint32_t, uint32_t, uint32_t*,
                                                 uint32_t);
+
+// merkleHash above a complete level of one or two lists' trees, to the list
+// roots with the length mix-in (hash.go:194-239), in one launch: list l's
+// workgroups [wg0, wg0 + nwg) reduce 2^span_log2 nodes each by span_log2
+// levels (a ragged last part keeps the odd rule at count 1: the other parts
+// are even at every level below, so its count's parity is the level's),
+// publish their node to `sub`, and the last to arrive reduces the nwg nodes
+// to the root and mixes in the length.  Two lists (the State's registry and
+// balances, hash.go:141-159): each list's last workgroup is one finisher of
+// the pair block (wave3_spread_final), the second to complete hashes the
+// struct root -- the two trees' latency-bound tops run side by side in one
+// launch on one stream, where the "level1" schedule ran four launches on two
+// streams with an event between them.
+template <uint32_t NT>
+__global__ __launch_bounds__(NT) void k_merkle_top_fused(MerkleTopArgs a) {
+    __shared__ uint32_t lds[8 * NT];
+    __shared__ uint32_t flag;
+    const uint32_t li = a.nlists > 1 && blockIdx.x >= a.l[1].wg0 ? 1u : 0u;
+    const MerkleTopList t = li ? a.l[1] : a.l[0];  // no dynamic index into the kernarg (scratch)
+    const uint32_t b = blockIdx.x - t.wg0;
+    const spread::Lane cst = spread::lane_consts(threadIdx.x & 63u);
+    const uint64_t lo = (uint64_t)b << t.span_log2;
+    const uint64_t span = 1ull << t.span_log2;
+    uint32_t m = (uint32_t)(t.c - lo < span ? t.c - lo : span);
+    wg_load_nodes<false>(lds, reinterpret_cast<const uint32_t*>(t.nodes) + 8 * lo, m);
+    auto none3 = [](uint32_t, const uint4&, const uint4&) {};
+    auto none_p = [](uint32_t, const uint32_t(&)[4], uint32_t) {};
+    auto none_w = [](uint32_t, uint32_t, uint32_t, uint32_t) {};
+    uint32_t nst = 0;
+    TOP_STAMP(nst++);
+    if (t.nwg > 1) {
+        for (uint32_t k = 0; k < t.span_log2; ++k) {
+            wg_level<NT, false>(lds, m, cst, none3, none_p, none_w);
+            m = (m + 1) / 2;
+            TOP_STAMP(nst++);
+        }
+        wg_store_node0<true>(lds, t.sub + 8 * b);
+        if (!wg_arrive_last(t.slot, t.nwg, &flag)) return;
+        m = t.nwg;
+        wg_load_nodes<true>(lds, t.sub, m);
+        TOP_STAMP(nst++);
+    }
+    while (m > 1) {
+        wg_level<NT, false>(lds, m, cst, none3, none_p, none_w);
+        m = (m + 1) / 2;
+        TOP_STAMP(nst++);
+    }
+    if (threadIdx.x < 64) wave3_spread_final(lds, t.n_items, t.out, a.nlists > 1 ? a.pair : nullptr, li, a.epoch);
+    TOP_STAMP(nst++);
+}
+template __global__ void k_merkle_top_fused<1024>(MerkleTopArgs);
 
 // Small merkleHash leaf passes in spread form (one state per wave): a
 // workgroup of 16 waves owns 16 windows; wave w hashes window w (256 B, the

@@ -141,6 +141,25 @@ constexpr uint32_t kArriveSlots = 4096;
 template <uint32_t NT>
 __global__ void k_trie_top_fused(uint32_t* levels, uint64_t cap, uint64_t c0, uint32_t d0, uint32_t depth,
                                  uint32_t* root_out, uint32_t slot);
+// k_merkle_top_fused: one list's part of the launch
+struct MerkleTopList {
+    const uint4* nodes;  // a complete level of the list's tree (plain 32-B nodes)
+    uint64_t c;          // its node count
+    uint64_t n_items;    // the length mix-in (hash.go:237-238)
+    uint32_t* sub;       // workspace: one published node per workgroup (32 B each)
+    uint32_t* out;       // the list root (32 B; with a pair: its slot of the pair block)
+    uint32_t wg0, nwg;   // this list's workgroups
+    uint32_t span_log2;  // level nodes per workgroup
+    uint32_t slot;       // arrival counter (g_arrive)
+};
+struct MerkleTopArgs {
+    MerkleTopList l[2];
+    uint32_t nlists;
+    uint32_t* pair;  // two lists: the pair block (wave3_spread_final), else NULL
+    uint32_t epoch;
+};
+template <uint32_t NT>
+__global__ void k_merkle_top_fused(MerkleTopArgs a);
 template <uint32_t NW>
 __global__ void k_trie_prefix_roots(const uint4* levels, uint64_t cap, uint64_t count0, uint64_t m, uint32_t depth,
                                     uint4* roots);

@@ -338,6 +338,30 @@ def merkle_finish_nodes_pair(nodes: torch.Tensor, count: int, n_total: int, pair
                 ws.numel(), _stream(nodes.device), device=dev)
 
 
+def top_fused_workspace(count0: int, count1: int, device) -> torch.Tensor:
+    nb = _lib.load().mk_ssz_merkle_top_fused_workspace_bytes(count0, count1)
+    if nb == 0:
+        raise ValueError(f"fused top: bad counts {count0}, {count1}")
+    return torch.empty(nb, dtype=torch.uint8, device=device)
+
+
+def merkle_top_fused(nodes0: torch.Tensor, count0: int, n0: int, out: torch.Tensor, nodes1: torch.Tensor = None,
+                     count1: int = 0, n1: int = 0, epoch: int = 0, ws: torch.Tensor = None) -> torch.Tensor:
+    """The level loop + length mix-in of one list (count1 == 0: ``out`` gets
+    the 32-B root) or of two lists side by side (``out`` a 128-B pair block,
+    merkle_finish_nodes_pair semantics: the struct root at out[64:96],
+    ``epoch`` 1 .. 2^30 - 1 a new one per pair), from a complete node level of
+    each, in one launch (mk_dev_ssz_merkle_top_fused)."""
+    dev = _dev(nodes0)
+    if count1 and out.numel() < 128:
+        raise ValueError("pair block of 128 bytes")
+    if ws is None:
+        ws = top_fused_workspace(count0, count1, nodes0.device)
+    _lib.invoke("mk_dev_ssz_merkle_top_fused", _p(nodes0), count0, n0, _p(nodes1) if nodes1 is not None else None,
+                count1, n1, _p(out), epoch, _p(ws), ws.numel(), _stream(nodes0.device), device=dev)
+    return out
+
+
 def merkle_finish_nodes(nodes: torch.Tensor, count: int, n_total: int, out: torch.Tensor = None,
                         ws: torch.Tensor = None) -> torch.Tensor:
     """Reference level loop over one gathered tree level of `count` nodes +

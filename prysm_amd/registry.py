@@ -129,9 +129,15 @@ class DeviceStateHasher:
     one permutation latency each), run side by side on two streams so they
     fill each other's idle issue slots."""
 
-    def __init__(self, n: int, device, schedule: str = "level1"):
+    def __init__(self, n: int, device, schedule: str = "fused"):
         """``schedule``:
-        "level1" (default): one launch for the struct roots and the level-1
+        "fused" (default): the struct launch of "level1", then both trees
+            above level 1 and the state root in ONE launch on the caller's
+            stream (mk_dev_ssz_merkle_top_fused: each tree's lower levels
+            reduced per workgroup over the whole chip, the last workgroup of
+            each tree its top, the second tree to finish the state root; no
+            side stream, no event);
+        "level1": one launch for the struct roots and the level-1
             windows of BOTH trees (mk_dev_ssz_struct_list_level1: the
             balances' windows on the lanes the registry's leave free); then
             the two trees' latency-bound levels side by side on two streams,
@@ -151,7 +157,7 @@ class DeviceStateHasher:
 
         from . import device as D
 
-        if schedule not in ("level1", "list", "two"):
+        if schedule not in ("fused", "level1", "list", "two"):
             raise ValueError(f"unknown schedule {schedule!r}")
         self.n, self.dev, self.schedule = n, device, schedule
         L = _lib.load()
@@ -162,13 +168,15 @@ class DeviceStateHasher:
         self.reg_ws = D.merkle_workspace(n, 32, device)
         self.list_ws = torch.empty(L.mk_ssz_struct_list_workspace_bytes(n, f, len(VALIDATOR_FIELDS)) + 256,
                                    dtype=torch.uint8, device=device) if schedule == "list" else None
-        lv1 = schedule == "level1"
+        lv1 = schedule in ("level1", "fused")
         self.c1 = -(-n // 8)  # level-1 nodes of the registry tree
         self.nodes = torch.empty(max(32, 32 * self.c1), dtype=torch.uint8, device=device)
         self.fin_ws = D.finish_workspace(self.c1, device) if lv1 else None
         self.cb1 = -(-8 * n // 256)  # level-1 nodes of the balances tree
         self.bnodes = torch.empty(max(32, 32 * self.cb1), dtype=torch.uint8, device=device)
         self.bfin_ws = D.finish_workspace(self.cb1, device) if lv1 else None
+        self.top_ws = D.top_fused_workspace(self.c1, self.cb1, device) if (
+            schedule == "fused" and self.c1 <= (1 << 20) and self.cb1 <= (1 << 20)) else None
         # reg_root || bal_root || state root || arrival word (zero before first use)
         self.pair_block = torch.zeros(128, dtype=torch.uint8, device=device) if lv1 else None
         self.epoch = 0  # one per submit (mk_dev_ssz_merkle_finish_nodes_pair)
@@ -193,16 +201,27 @@ class DeviceStateHasher:
         sched = self.schedule
         if sched != "two" and not D.struct_list_level1_ok(records, n, 160, VALIDATOR_FIELDS):
             sched = "two"
+        if sched == "fused" and self.top_ws is None:
+            sched = "level1"
         # the level-1 front also takes the balances' windows: 16-B aligned, more
         # than one chunk (mk_dev_ssz_struct_list_level1); otherwise the one-call
         # list root with the balances tree beside it
-        if sched == "level1" and (balances.data_ptr() % 16 or n * 8 <= 128):
+        if sched in ("level1", "fused") and (balances.data_ptr() % 16 or n * 8 <= 128):
             sched = "list"
             if self.list_ws is None:
                 L = _lib.load()
                 self.list_ws = torch.empty(
                     L.mk_ssz_struct_list_workspace_bytes(n, _fields(VALIDATOR_FIELDS), len(VALIDATOR_FIELDS)) + 256,
                     dtype=torch.uint8, device=self.dev)
+        if sched == "fused":
+            # two launches on the caller's stream: struct roots + both trees'
+            # level-1 windows, then both trees to the state root
+            D.struct_list_level1(records, n, 160, VALIDATOR_FIELDS, self.roots, self.nodes, values=balances,
+                                 nvalues=n, value_len=8, value_nodes=self.bnodes)
+            self.epoch = self.epoch % ((1 << 30) - 1) + 1
+            D.merkle_top_fused(self.nodes, self.c1, n, self.pair_block, self.bnodes, self.cb1, n, epoch=self.epoch,
+                               ws=self.top_ws)
+            return self.out
         if sched == "level1":
             # one launch: struct roots + the level-1 windows of BOTH trees (the
             # balances' on the lanes the registry's windows leave free)

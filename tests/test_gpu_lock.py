@@ -228,10 +228,10 @@ def test_struct_list_root_windows_vs_oracle(gpu, n):
 
 
 def test_state_hasher_schedules_agree(gpu):
-    """registry.DeviceStateHasher under its three schedules (level-1 front +
-    finish beside the balances tree, the one-call list root, round 3's
-    two-call schedule) against the host-buffer state root, three submits
-    each."""
+    """registry.DeviceStateHasher under its four schedules (level-1 front +
+    both tops in one fused launch, level-1 front + the two finishers on two
+    streams, the one-call list root, round 3's two-call schedule) against the
+    host-buffer state root, three submits each."""
     import torch
 
     from prysm_amd import registry as R
@@ -242,7 +242,7 @@ def test_state_hasher_schedules_agree(gpu):
     want = R.state_root(reg, bal)
     rec = torch.from_numpy(reg.records.view(np.uint8).reshape(-1).copy()).to(gpu)
     dbal = torch.from_numpy(bal.view(np.uint8).copy()).to(gpu)
-    for sched in ("level1", "list", "two"):
+    for sched in ("fused", "level1", "list", "two"):
         h = R.DeviceStateHasher(n, gpu, schedule=sched)
         for _ in range(3):
             out = h.submit(rec, dbal)

@@ -170,7 +170,7 @@ def measure_c3(dev, steps, warmup):
     states through registry.StatePipeline (each state's registry levels 2..10
     in the next state's struct launch, its tops beside that launch; the last
     state's top inside the timed region).  Beside it, one state alone through
-    registry.DeviceStateHasher ("level1"; PRYSM_C3_SCHED: another schedule).
+    registry.DeviceStateHasher ("fused"; PRYSM_C3_SCHED: another schedule).
     PRYSM_C3_STREAM=0: time the one-state form as the step."""
     import torch
 
@@ -181,7 +181,7 @@ def measure_c3(dev, steps, warmup):
     n = g["n"]
     rec = R.synthetic_registry_device(n, g["seed"], dev)
     dbal = R.synthetic_balances_device(n, g["seed"], dev)
-    hasher = R.DeviceStateHasher(n, dev, schedule=os.environ.get("PRYSM_C3_SCHED", "level1"))
+    hasher = R.DeviceStateHasher(n, dev, schedule=os.environ.get("PRYSM_C3_SCHED", "fused"))
     out = hasher.out
     sec_one = _timeit(lambda: hasher.submit(rec, dbal), steps, warmup)
     one = bytes(out.cpu().numpy()).hex()

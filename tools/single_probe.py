@@ -45,7 +45,7 @@ def main():
             n = g["n"]
             rec = R.synthetic_registry_device(n, g["seed"], dev)
             dbal = R.synthetic_balances_device(n, g["seed"], dev)
-            h = R.DeviceStateHasher(n, dev, schedule=os.environ.get("PRYSM_C3_SCHED", "level1"))
+            h = R.DeviceStateHasher(n, dev, schedule=os.environ.get("PRYSM_C3_SCHED", "fused"))
             out = h.out
             fn = lambda: h.submit(rec, dbal)  # noqa: E731
             want = g["state_root"]
