@@ -189,7 +189,10 @@ int mk_dev_ssz_merkle_finish_nodes(mk_call* call, const void* d_nodes, uint64_t 
  * before the block's first use, then owned by the finishers.  Each pair takes
  * the next epoch of a counter over 1 .. 2^30 - 1 (wrapping; "newer" = ahead by
  * less than 2^29), so a pair left half-done by a failed call never completes
- * with the next one, and a late finisher of an older epoch is ignored.  The
+ * with the next one, and a finisher whose epoch is already behind the word's
+ * when it starts is ignored.  That check is best-effort (it precedes the
+ * finisher's slot store): two epochs' finishers of one slot must not run
+ * concurrently -- order them on one stream or by events.  The
  * first finisher of an epoch zeroes d_pair_block[64, 96), so a pair that
  * never completes reads back as zeros, not as the previous pair's root.  The
  * block is MK_PAIR_BLOCK_BYTES, 16-B aligned; the caller waits for both

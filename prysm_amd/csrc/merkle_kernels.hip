@@ -1172,7 +1172,10 @@ __device__ __forceinline__ void wave3_spread_levels(uint32_t* lds, uint64_t& c, 
 // 2^29): a finisher of a newer epoch than the word's starts the mask afresh,
 // so a pair left half-done (a failed launch) cannot pair with the next one; a
 // finisher of an OLDER epoch (a late one) is ignored -- it writes neither its
-// slot nor the arrival word -- so it cannot clear the current pair's bits.  The first finisher of an epoch zeroes pair[64..96)
+// slot nor the arrival word -- so it cannot clear the current pair's bits.
+// Best-effort: the epoch is read before the slot store, so a finisher that
+// falls behind while it runs may still overwrite its slot; callers never run
+// two epochs' finishers of one slot concurrently (include/prysm_merkle.h).  The first finisher of an epoch zeroes pair[64..96)
 // before it sets its bit, so a pair that never completes reads back as
 // zeros, never as the previous epoch's root.
 // How far `epoch` is ahead of an arrival word's epoch (mod 2^30; >= 2^29:
@@ -2077,20 +2080,21 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     const uint64_t last_unit = n * (kRecLen / 16) - 1;
     // instructions [i0, i1) of the kNinstr (issued in parts).  Record m of
     // the wave sits in 16-B slots [10 m, 10 m + 10) rotated by one unit when
-    // bit 3 of m is set (unit u in slot 10 m + (u + rot) mod 10): a
-    // ds_read_b128 of one unit by 16 consecutive lanes then hits 16 distinct
-    // 16-B bank groups (lanes 0-7 the even ones, 8-15 the odd ones) where the
-    // plain 160-B stride put lanes l and l + 8 on one (1.63 M
-    // SQ_LDS_BANK_CONFLICT per launch, profiles/r05/pmc/); the copy stays
-    // one contiguous 1-KB LDS write per instruction, each lane fetching the
-    // unit its slot holds
+    // bits 2 and 3 of m differ (unit u in slot 10 m + (u + rot) mod 10).  On
+    // gfx950 a ds_read_b128 is conflict-free when the slots of each 16
+    // consecutive lanes differ mod 16, a ds_write_b128 when those of each 8
+    // differ mod 8 (tools/lds_bank_probe.hip, profiles/r06/lds_bank_probe.txt);
+    // the plain 160-B stride fails both (lanes l, l + 8 and l, l + 4 collide:
+    // 1.63 M SQ_LDS_BANK_CONFLICT per launch, profiles/r05/pmc/), this
+    // rotation passes both.  The copy stays one contiguous 1-KB LDS write per
+    // instruction, each lane fetching the unit its slot holds
     auto dma = [&](uint64_t g, uint32_t i0 = 0, uint32_t i1 = kNinstr) {
         const uint64_t u0 = (g * kLockThreads + 64 * wave) * (kRecLen / 16);
         const uint4* src = reinterpret_cast<const uint4*>(rec);
 #pragma unroll
         for (uint32_t i = i0; i < i1; ++i) {
             const uint32_t sl = 64 * i + lane, m = sl / 10u, v = sl - 10u * m;
-            const uint32_t rot = (m >> 3) & 1u;
+            const uint32_t rot = ((m >> 2) ^ (m >> 3)) & 1u;
             const uint64_t u = u0 + 10u * m + (v >= rot ? v - rot : v + 10u - rot);
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + (u < last_unit ? u : last_unit)),
                                              (__attribute__((address_space(3))) void*)(Bw + 256 * i), 16, 0,
@@ -2109,7 +2113,7 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_struct_lock(const uint8_t* 
     // (uniform over the workgroup: all its waves run the same permutations)
     const bool slots = PREV && gpw == 4 && g_end - g_begin == 4;
     // this lane's record: units 0..8 at R (rotated), unit 9 at R9
-    const uint32_t rot = (lane >> 3) & 1u;
+    const uint32_t rot = ((lane >> 2) ^ (lane >> 3)) & 1u;
     uint32_t* const R = Bw + lane * kRw + 4u * rot;
     const uint32_t* const R9 = Bw + lane * kRw + (rot ? 0u : 36u);
 #pragma unroll 1

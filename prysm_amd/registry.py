@@ -276,7 +276,9 @@ class StatePipeline:
     the CUs its grid leaves free, one high-priority side stream finishes
     state i-1's trees in turn (the ragged last subtrees, the ~245-node
     registry top, the ~3,900-node balances top); the second of the two tops
-    hashes the state root into the state's pair block.  **A state's root is therefore written
+    hashes the state root into the state's pair block.  Submits and flush()
+    may come from different current streams: each waits for the previous
+    launch's event when the stream changed.  **A state's root is therefore written
     one submit later**: the tensor ``submit`` returns is produced once the
     next ``submit`` or ``flush()`` has been called and the side stream has
     run (synchronise, or ``wait()``).  Four buffer sets rotate; a root stays
@@ -319,6 +321,7 @@ class StatePipeline:
         self._i = 0
         self._pending = None  # the set of the state whose trees' slot levels are not built yet
         self._done = {}       # state index -> (registry top event, balances top event)
+        self._front_ev = None  # (stream, event) after the last struct launch
 
     def submit(self, records, balances):
         """records: (n*160,) uint8 device tensor; balances: (n*8,) uint8, both
@@ -346,15 +349,18 @@ class StatePipeline:
         self._done.pop(i - self.SETS - 1, None)
         prev = self._pending
         p = prev is not None
+        if p and self._front_ev is not None and self._front_ev[0] != cur:
+            cur.wait_event(self._front_ev[1])  # launch i - 1 (its nodes are read here) ran on another stream
         D.struct_list_level1_pipe(records, n, 160, VALIDATOR_FIELDS, self.roots, self.nodes[s],
                                   self.nodes[prev] if p else None, self.levels[prev] if p else None,
                                   values=balances, nvalues=n, value_len=8, value_nodes=self.bnodes[s],
                                   prev_value_nodes=self.bnodes[prev] if p else None,
                                   prev_value_levels=self.blevels[prev] if p else None)
         self.epochs[s] = self.epochs[s] % ((1 << 30) - 1) + 1
+        k_ev = torch.cuda.Event()
+        k_ev.record(cur)
+        self._front_ev = (cur, k_ev)
         if p:  # state i - 1's two tops: their slot levels were built by launch i
-            k_ev = torch.cuda.Event()
-            k_ev.record(cur)
             self._tops(i - 1, prev, k_ev, pipelined=True)
         self._pending = s
         return self.pairs[s][64:96]
@@ -391,8 +397,11 @@ class StatePipeline:
         import torch
 
         if self._pending is not None:
+            cur = torch.cuda.current_stream(self.dev)
+            if self._front_ev is not None and self._front_ev[0] != cur:
+                cur.wait_event(self._front_ev[1])  # the last launch ran on another stream
             ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(self.dev))
+            ev.record(cur)
             self._tops(self._i - 1, self._pending, ev, pipelined=False)
             self._pending = None
 

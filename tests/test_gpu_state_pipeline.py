@@ -149,3 +149,30 @@ def test_state_pipeline_flush_mid_stream_and_refusals(gpu):
         p.submit(rec, torch.cat([bal, bal[:8]])[8:])  # balances 8 B off alignment
     with pytest.raises(ValueError):
         R.StatePipeline(1 << 18, gpu).submit(*_states(1 << 18, [SEED], gpu)[0])  # 1 group per workgroup
+
+
+def test_state_pipeline_submits_from_two_streams(gpu):
+    """Submits alternating between two current streams, and flush() from a
+    third: each launch waits for the previous one's event when the stream
+    changed (it reads that launch's level-1 nodes), so every root equals the
+    one-state path's (no cross-stream dependency before)."""
+    import torch
+
+    from prysm_amd import registry as R
+
+    n = 1 << 20
+    states = _states(n, [SEED + 900 + t for t in range(5)], gpu)
+    want = _one_state_roots(n, states, gpu)
+    p = R.StatePipeline(n, gpu)
+    streams = [torch.cuda.Stream(device=gpu), torch.cuda.Stream(device=gpu), torch.cuda.Stream(device=gpu)]
+    handles = []
+    for t, (rec, bal) in enumerate(states):
+        with torch.cuda.stream(streams[t % 2]):
+            handles.append(p.submit(rec, bal))
+    with torch.cuda.stream(streams[2]):
+        p.flush()
+        p.wait()
+    torch.cuda.synchronize()
+    # roots stay valid for two submits after they are produced: read the last three
+    got = [bytes(h.cpu().numpy()) for h in handles[-3:]]
+    assert got == want[-3:]

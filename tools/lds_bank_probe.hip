@@ -18,7 +18,8 @@ __device__ __forceinline__ uint32_t slot_of(int P, uint32_t l) {
         case 5: return 10u * l + ((l >> 4) & 1u);        // +1 when bit 4 set
         case 6: return 10u * l + ((l >> 3) & 7u);        // +0..7 by bits 3-5
         case 7: return 10u * l + ((l >> 2) & 1u) + 2u * ((l >> 3) & 1u);
-        default: return 10u * l + (l >> 3);              // 8
+        case 8: return 10u * l + (l >> 3);               // +0..7 by bits 3-5
+        default: return 10u * l + (((l >> 2) ^ (l >> 3)) & 1u);  // 9: bit 2 xor bit 3 (k_struct_lock)
     }
 }
 
@@ -51,7 +52,7 @@ void run(uint4* d) {
 int main() {
     uint4* d;
     if (hipMalloc(&d, 64 * 16) != hipSuccess) return 1;
-    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d); run<7>(d); run<8>(d);
+    run<0>(d); run<1>(d); run<2>(d); run<3>(d); run<4>(d); run<5>(d); run<6>(d); run<7>(d); run<8>(d); run<9>(d);
     if (hipDeviceSynchronize() != hipSuccess) return 1;
     printf("ok\n");
     return 0;
