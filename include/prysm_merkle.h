@@ -207,11 +207,13 @@ int mk_dev_ssz_merkle_finish_nodes_pair(mk_call* call, const void* d_nodes, uint
  * the reference level loop (hash.go:225-236, odd -> 0^128) and mixed in
  * (Keccak(root || le64(n0) || 0^24), :237-238); count1 == 0: d_out gets the
  * 32-B list root.  count1 > 0: a second list (d_nodes1, count1, n1) side by
- * side, and d_out is a pair block with mk_dev_ssz_merkle_finish_nodes_pair's
- * semantics (list 0's root at [0, 32), list 1's at [32, 64), the struct root
- * Keccak(d_out[0, 64)) at [64, 96) written by whichever list finishes second,
- * `epoch` as there): the State root of BASELINE config 3 from the two trees'
- * level-1 nodes in one call on one stream.  Each count is 1 .. 2^20; at most
+ * side, and d_out is a pair block laid out as for
+ * mk_dev_ssz_merkle_finish_nodes_pair (list 0's root at [0, 32), list 1's at
+ * [32, 64), the struct root Keccak(d_out[0, 64)) at [64, 96) written by
+ * whichever list finishes second; both finishers are in this launch, so the
+ * arrival word at [96, 100) is not used; `epoch` 1 .. 2^30 - 1 is checked
+ * and otherwise unused): the State root of BASELINE config 3 from the two
+ * trees' level-1 nodes in one call on one stream.  Each count is 1 .. 2^20; at most
  * 4096 such launches in flight per device (arrival counters).  Workspace from
  * mk_ssz_merkle_top_fused_workspace_bytes(count0, count1), 16-B aligned.
  * Replaces: ssz.merkleHash's level loop (shared/ssz/hash.go:223-239) for a

@@ -1972,7 +1972,8 @@ static int launch_top_fused(const TopPlan& p, uint32_t nl, const void* const* no
     mk::MerkleTopArgs a{};
     a.nlists = nl;
     a.pair = nl == 2 ? (uint32_t*)d_out : nullptr;
-    a.epoch = epoch;
+    a.pair_slot = nl == 2 ? next_arrive_slot() : 0;
+    (void)epoch;  // both finishers are in this launch: an arrival counter, not the epoch word
     uint32_t wg = 0;
     uint32_t* sub = (uint32_t*)d_ws;
     for (uint32_t l = 0; l < nl; ++l) {

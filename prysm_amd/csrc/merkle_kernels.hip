@@ -3003,92 +3003,120 @@ template <uint32_t NT, bool TRIE, typename LaneOut, typename PairOut, typename W
 __device__ __forceinline__ void wg_level(uint32_t* lds, uint32_t m, const spread::Lane& cst, LaneOut&& lane_out,
                                          PairOut&& pair_out, WaveOut&& wave_out) {
     const uint32_t tid = threadIdx.x, mn = (m + 1) / 2;
-    if (mn >= 256) {  // one state per lane
-        const bool act = tid < mn;
-        const bool right = 2 * tid + 1 < m;
-        State s;
-        if (act) {
+    const uint32_t w = tid >> 6, L = tid & 63u, i = cst.i;
+    // spread form (one parent per wave): wave `sw` hashes parent `j`
+    auto spread_load = [&](uint32_t j, uint32_t& e, uint32_t& o) {
+        const bool right = 2 * j + 1 < m;
+        e = o = 0u;
+        if (i < 4u) {
+            e = lds[16 * j + 2 * i];
+            o = lds[16 * j + 2 * i + 1];
+        } else if (i < 8u && right) {
+            e = lds[16 * j + 8 + 2 * (i - 4u)];
+            o = lds[16 * j + 8 + 2 * (i - 4u) + 1];
+        }
+    };
+    auto spread_hash = [&](uint32_t j, uint32_t& e, uint32_t& o) {
+        if (!TRIE && !(2 * j + 1 < m)) {  // K(l || 0^128): 160 bytes, two blocks
+            spread::keccak_f(e, o, cst);
+            if (i == 3u) e ^= 1u;
+        } else if (i == 8u) {
+            e ^= 1u;
+        }
+        if (i == 16u) o ^= 0x80000000u;
+        spread::keccak_f(e, o, cst);
+    };
+    auto spread_store = [&](uint32_t j, uint32_t e, uint32_t o) {
+        if (L < 4u) {
+            lds[8 * j + 2 * L] = e;
+            lds[8 * j + 2 * L + 1] = o;
+            wave_out(j, e, o, L);
+        }
+    };
+    if (mn > NT / 128) {
+        // The unpaired last node of an odd merkleHash level is K(l || 0^128),
+        // two permutations: the last wave hashes it in spread form (2 x ~7 k
+        // cycles) beside the lane / pair forms' one permutation (13-20 k),
+        // where as one of theirs it doubled the level (C3's registry top: the
+        // 123 -> 62 and 31 -> 16 levels 29.6 k and 32.5 k cycles,
+        // tools/top_probe.hip)
+        const bool side = !TRIE && (m & 1u) && 2 * (mn - 1) <= NT - 64;
+        const uint32_t mh = side ? mn - 1 : mn;  // parents of the lane / pair forms
+        const bool sw = side && w == NT / 64 - 1;
+        uint32_t e = 0u, o = 0u;
+        if (sw) spread_load(mn - 1, e, o);
+        if (mh >= 256) {  // one state per lane
+            const bool act = tid < mh;
+            const bool right = 2 * tid + 1 < m;
+            State s;
+            if (act) {
 #pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                ilv_to_plain(lds[16 * tid + 2 * w], lds[16 * tid + 2 * w + 1], s.lo[w], s.hi[w]);
-                if (right)
-                    ilv_to_plain(lds[16 * tid + 8 + 2 * w], lds[16 * tid + 8 + 2 * w + 1], s.lo[4 + w], s.hi[4 + w]);
-                else
-                    s.lo[4 + w] = s.hi[4 + w] = 0u;
+                for (int q = 0; q < 4; ++q) {
+                    ilv_to_plain(lds[16 * tid + 2 * q], lds[16 * tid + 2 * q + 1], s.lo[q], s.hi[q]);
+                    if (right)
+                        ilv_to_plain(lds[16 * tid + 8 + 2 * q], lds[16 * tid + 8 + 2 * q + 1], s.lo[4 + q],
+                                     s.hi[4 + q]);
+                    else
+                        s.lo[4 + q] = s.hi[4 + q] = 0u;
+                }
+            }
+            __syncthreads();
+            if (act) {
+#pragma unroll
+                for (int q = 8; q < 25; ++q) s.lo[q] = s.hi[q] = 0u;
+                if (!TRIE && !right) {  // K(l || 0^128): block 1 = l || 0, block 2 = 0^24 || pad
+                    keccak_f(s);
+                    s.lo[3] ^= 1u;
+                } else {
+                    s.lo[8] ^= 1u;  // byte 64
+                }
+                s.hi[16] ^= 0x80000000u;
+                keccak_f_digest(s);
+                uint4 d0, d1;
+                digest(s, d0, d1);
+                const uint32_t lo4[4] = {d0.x, d0.z, d1.x, d1.z}, hi4[4] = {d0.y, d0.w, d1.y, d1.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    lds[8 * tid + 2 * q] = ilv::to_ilv(lo4[q], hi4[q], 0);
+                    lds[8 * tid + 2 * q + 1] = ilv::to_ilv(lo4[q], hi4[q], 1);
+                }
+                lane_out(tid, d0, d1);
+            }
+        } else {  // lane pairs
+            const uint32_t k = tid >> 1, p = tid & 1u;
+            const bool act = k < mh;
+            uint32_t a[4], b[4] = {0, 0, 0, 0};
+            bool padded = false;
+            if (act) {
+                const bool right = 2 * k + 1 < m;
+                padded = !TRIE && !right;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] = lds[16 * k + 2 * q + p];
+                if (right) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) b[q] = lds[16 * k + 8 + 2 * q + p];
+                }
+            }
+            __syncthreads();
+            if (act) {
+                uint32_t h[4];
+                hash_pair3(a, b, padded, p, h);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) lds[8 * k + 2 * q + p] = h[q];
+                pair_out(k, h, p);
             }
         }
-        __syncthreads();
-        if (act) {
-#pragma unroll
-            for (int w = 8; w < 25; ++w) s.lo[w] = s.hi[w] = 0u;
-            if (!TRIE && !right) {  // K(l || 0^128): block 1 = l || 0, block 2 = 0^24 || pad
-                keccak_f(s);
-                s.lo[3] ^= 1u;
-            } else {
-                s.lo[8] ^= 1u;  // byte 64
-            }
-            s.hi[16] ^= 0x80000000u;
-            keccak_f_digest(s);
-            uint4 d0, d1;
-            digest(s, d0, d1);
-            const uint32_t lo4[4] = {d0.x, d0.z, d1.x, d1.z}, hi4[4] = {d0.y, d0.w, d1.y, d1.w};
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                lds[8 * tid + 2 * w] = ilv::to_ilv(lo4[w], hi4[w], 0);
-                lds[8 * tid + 2 * w + 1] = ilv::to_ilv(lo4[w], hi4[w], 1);
-            }
-            lane_out(tid, d0, d1);
-        }
-    } else if (mn > NT / 128) {  // lane pairs
-        const uint32_t k = tid >> 1, p = tid & 1u;
-        const bool act = k < mn;
-        uint32_t a[4], b[4] = {0, 0, 0, 0};
-        bool padded = false;
-        if (act) {
-            const bool right = 2 * k + 1 < m;
-            padded = !TRIE && !right;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) a[w] = lds[16 * k + 2 * w + p];
-            if (right) {
-#pragma unroll
-                for (int w = 0; w < 4; ++w) b[w] = lds[16 * k + 8 + 2 * w + p];
-            }
-        }
-        __syncthreads();
-        if (act) {
-            uint32_t h[4];
-            hash_pair3(a, b, padded, p, h);
-#pragma unroll
-            for (int w = 0; w < 4; ++w) lds[8 * k + 2 * w + p] = h[w];
-            pair_out(k, h, p);
+        if (sw) {
+            spread_hash(mn - 1, e, o);
+            spread_store(mn - 1, e, o);
         }
     } else {  // one parent per wave
-        const uint32_t w = tid >> 6, L = tid & 63u;
-        const uint32_t i = cst.i;
         uint32_t e = 0u, o = 0u;
-        if (w < mn) {  // wave-uniform
-            const bool right = 2 * w + 1 < m;
-            if (i < 4u) {
-                e = lds[16 * w + 2 * i];
-                o = lds[16 * w + 2 * i + 1];
-            } else if (i < 8u && right) {
-                e = lds[16 * w + 8 + 2 * (i - 4u)];
-                o = lds[16 * w + 8 + 2 * (i - 4u) + 1];
-            }
-            if (!TRIE && !right) {  // K(l || 0^128): 160 bytes, two blocks
-                spread::keccak_f(e, o, cst);
-                if (i == 3u) e ^= 1u;
-            } else if (i == 8u) {
-                e ^= 1u;
-            }
-            if (i == 16u) o ^= 0x80000000u;
-            spread::keccak_f(e, o, cst);
-        }
+        if (w < mn) spread_load(w, e, o);  // wave-uniform
         __syncthreads();
-        if (w < mn && L < 4u) {
-            lds[8 * w + 2 * L] = e;
-            lds[8 * w + 2 * L + 1] = o;
-            wave_out(w, e, o, L);
+        if (w < mn) {
+            spread_hash(w, e, o);
+            spread_store(w, e, o);
         }
     }
     __syncthreads();
@@ -3283,7 +3311,55 @@ __global__ __launch_bounds__(NT) void k_merkle_top_fused(MerkleTopArgs a) {
         m = (m + 1) / 2;
         TOP_STAMP(nst++);
     }
-    if (threadIdx.x < 64) wave3_spread_final(lds, t.n_items, t.out, a.nlists > 1 ? a.pair : nullptr, li, a.epoch);
+    // the length mix-in K(root || le64(n) || 0^24) on wave 0 (spread form)
+    const uint32_t L = threadIdx.x & 63u, i = cst.i;
+    uint32_t e = 0u, o = 0u;
+    if (threadIdx.x < 64) {
+        if (i < 4u) {
+            e = lds[2 * i];
+            o = lds[2 * i + 1];
+        } else if (i == 4u) {
+            e = ilv::to_ilv((uint32_t)t.n_items, (uint32_t)(t.n_items >> 32), 0);
+            o = ilv::to_ilv((uint32_t)t.n_items, (uint32_t)(t.n_items >> 32), 1);
+        } else if (i == 8u) {
+            e = 1u;
+        }
+        if (i == 16u) o ^= 0x80000000u;
+        spread::keccak_f(e, o, cst);
+    }
+    if (a.nlists == 1) {
+        if (threadIdx.x < 64) spread_store_digest(e, o, L, t.out);
+        TOP_STAMP(nst++);
+        return;
+    }
+    // Two lists: publish this list's root to its slot of the pair block
+    // (write-through, drained) and arrive on the pair's counter; the second
+    // list to arrive hashes the struct root K(root 0 || root 1) (hash.go:141-
+    // 159) into pair[64..96).  Both finishers are in this launch, so an
+    // arrival counter does what the epoch-tagged arrival word does between
+    // two launches (wave3_spread_final), without its fences.
+    __syncthreads();
+    if (threadIdx.x < 64 && L < 4u) {
+        lds[2 * L] = e;
+        lds[2 * L + 1] = o;
+    }
+    __syncthreads();
+    wg_store_node0<true>(lds, t.out);
+    if (!wg_arrive_last(a.pair_slot, 2, &flag)) return;
+    if (threadIdx.x < 64) {
+        e = o = 0u;
+        if (i < 8u) {  // lanes of Keccak lanes 0..3: list 0's root, 4..7: list 1's
+            const uint64_t v = __hip_atomic_load(reinterpret_cast<const uint64_t*>(a.pair) + i, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            e = ilv::to_ilv((uint32_t)v, (uint32_t)(v >> 32), 0);
+            o = ilv::to_ilv((uint32_t)v, (uint32_t)(v >> 32), 1);
+        } else if (i == 8u) {
+            e = 1u;  // byte 64
+        }
+        if (i == 16u) o ^= 0x80000000u;
+        spread::keccak_f(e, o, cst);
+        spread_store_digest(e, o, L, a.pair + 16);
+    }
     TOP_STAMP(nst++);
 }
 template __global__ void k_merkle_top_fused<1024>(MerkleTopArgs);

@@ -155,8 +155,8 @@ struct MerkleTopList {
 struct MerkleTopArgs {
     MerkleTopList l[2];
     uint32_t nlists;
-    uint32_t* pair;  // two lists: the pair block (wave3_spread_final), else NULL
-    uint32_t epoch;
+    uint32_t* pair;      // two lists: the pair block (roots at [0, 64), the struct root at [64, 96)), else NULL
+    uint32_t pair_slot;  // two lists: the arrival counter of the two finishers
 };
 template <uint32_t NT>
 __global__ void k_merkle_top_fused(MerkleTopArgs a);

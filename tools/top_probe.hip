@@ -12,7 +12,70 @@
 #include <cstdio>
 #include <vector>
 
+static void print_wgs(const std::vector<uint64_t>& st, uint32_t b0, uint32_t b1, const char* name) {
+    // the workgroup of [b0, b1) with the most stamps (the last arriver), cycles between its stamps
+    uint32_t lb = b0, best = 0;
+    for (uint32_t b = b0; b < b1; ++b) {
+        uint32_t k = 0;
+        while (k < 64 && st[b * 64 + k]) ++k;
+        if (k > best) best = k, lb = b;
+    }
+    printf("\"%s\": {\"wg\": %u, \"level_cycles\": [", name, lb);
+    for (uint32_t k = 1; k < best; ++k)
+        printf("%s%llu", k > 1 ? ", " : "", (unsigned long long)(st[lb * 64 + k] - st[lb * 64 + k - 1]));
+    printf("], \"total\": %llu}", (unsigned long long)(st[lb * 64 + best - 1] - st[lb * 64]));
+}
+
+// C3's fused list top (k_merkle_top_fused): 125,000 registry + 31,250
+// balances level-1 nodes, spans 1024 / 256 (capi.cpp top_plan)
+static int merkle_probe(int iters) {
+    const uint64_t c0 = 125000, c1 = 31250;
+    uint32_t *n0, *n1, *ws, *pair;
+    (void)hipMalloc(&n0, c0 * 32);
+    (void)hipMalloc(&n1, c1 * 32);
+    (void)hipMalloc(&ws, 1 << 16);
+    (void)hipMalloc(&pair, 128);
+    (void)hipMemset(n0, 0x5A, c0 * 32);
+    (void)hipMemset(n1, 0xA5, c1 * 32);
+    (void)hipMemset(pair, 0, 128);
+    mk::MerkleTopArgs a{};
+    a.nlists = 2;
+    a.pair = pair;
+    const uint32_t sl[2] = {10, 8};
+    const uint64_t c[2] = {c0, c1};
+    uint32_t* nodes[2] = {n0, n1};
+    uint32_t wg = 0;
+    for (int l = 0; l < 2; ++l) {
+        a.l[l].nodes = (const uint4*)nodes[l];
+        a.l[l].c = c[l];
+        a.l[l].n_items = 1000000;
+        a.l[l].sub = ws + 8 * wg;
+        a.l[l].out = pair + 8 * l;
+        a.l[l].wg0 = wg;
+        a.l[l].nwg = (uint32_t)((c[l] + (1u << sl[l]) - 1) >> sl[l]);
+        a.l[l].span_log2 = sl[l];
+        wg += a.l[l].nwg;
+    }
+    std::vector<uint64_t> zero(1024 * 64, 0), st(1024 * 64);
+    for (int it = 0; it < iters; ++it) {
+        a.pair_slot = 2000 + it;
+        a.l[0].slot = 2 * it;
+        a.l[1].slot = 2 * it + 1;
+        if (it + 1 == iters) (void)hipMemcpyToSymbol(HIP_SYMBOL(mk::g_top_stamps), zero.data(), zero.size() * 8);
+        hipLaunchKernelGGL(mk::k_merkle_top_fused<1024>, dim3(wg), dim3(1024), 0, 0, a);
+        (void)hipDeviceSynchronize();
+    }
+    (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(mk::g_top_stamps), st.size() * 8);
+    printf("{\"merkle_top\": {");
+    print_wgs(st, 0, a.l[0].nwg, "registry");
+    printf(", ");
+    print_wgs(st, a.l[1].wg0, wg, "balances");
+    printf("}}\n");
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 2) return merkle_probe(atoi(argv[1]));
     const uint64_t n = 1u << 20, cap = n;
     const uint32_t depth = 32, d0 = 2;
     const int iters = argc > 1 ? atoi(argv[1]) : 5;
