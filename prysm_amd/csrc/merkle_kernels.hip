@@ -3111,12 +3111,17 @@ __device__ __forceinline__ void wg_level(uint32_t* lds, uint32_t m, const spread
             spread_store(mn - 1, e, o);
         }
     } else {  // one parent per wave
+        // parent j on wave j: a workgroup's waves go to its SIMDs round-robin
+        // (wave w on SIMD w mod 4), so the first 4 parents get a SIMD each
+        // (parents 0..3 on waves 0, 4, 8, 12 -- one SIMD -- took 15.9 k
+        // cycles a level against 7.8 k, tools/top_probe.hip, profiles/r06/single/)
+        const uint32_t j = w;
         uint32_t e = 0u, o = 0u;
-        if (w < mn) spread_load(w, e, o);  // wave-uniform
+        if (j < mn) spread_load(j, e, o);  // wave-uniform
         __syncthreads();
-        if (w < mn) {
-            spread_hash(w, e, o);
-            spread_store(w, e, o);
+        if (j < mn) {
+            spread_hash(j, e, o);
+            spread_store(j, e, o);
         }
     }
     __syncthreads();
@@ -3218,30 +3223,31 @@ __global__ __launch_bounds__(NT) void k_trie_top_fused(uint32_t* __restrict__ le
         }
         if (d < d_end) {
             // one node left: the zero-sibling levels K(node || 0^32) as a
-            // chain on wave 0, the node kept in registers (no LDS round trip,
-            // no barrier per level)
-            const uint32_t i = cst.i;
-            uint32_t e = 0u, o = 0u;
-            if (w == 0 && i < 4u) {
-                e = lds[2 * i];
-                o = lds[2 * i + 1];
-            }
+            // chain on wave 0, the node kept in registers as plain (lo, hi)
+            // words (no LDS round trip, no barrier, no bit (de)interleave per
+            // level; the lo/hi round, 6.29 k cycles a permutation against
+            // 6.44 k, profiles/r02d/lat_probe_spread.json)
+            const spread::LaneLH ch = spread::lane_consts_lh(L);
+            const uint32_t i = ch.i;
+            uint32_t lo32 = 0u, hi32 = 0u;
+            if (w == 0 && i < 4u) ilv_to_plain(lds[2 * i], lds[2 * i + 1], lo32, hi32);
             for (; d < d_end; ++d) {
                 TOP_STAMP(nst++);
                 if (w == 0) {
-                    if (i >= 4u) e = o = 0u;
-                    if (i == 8u) e ^= 1u;
-                    if (i == 16u) o ^= 0x80000000u;
-                    spread::keccak_f(e, o, cst);
-                    spread_store_digest(e, o, L, levels + 8 * (off + capd + (lo >> 1)));
+                    if (i >= 4u) lo32 = hi32 = 0u;
+                    if (i == 8u) lo32 ^= 1u;
+                    if (i == 16u) hi32 ^= 0x80000000u;
+                    spread::keccak_f_lh(lo32, hi32, ch);
+                    if (L < 4u)
+                        reinterpret_cast<uint2*>(levels + 8 * (off + capd + (lo >> 1)))[L] = make_uint2(lo32, hi32);
                 }
                 lo >>= 1;
                 off += capd;
                 capd = (capd + 1) / 2;
             }
             if (w == 0 && L < 4u) {
-                lds[2 * L] = e;
-                lds[2 * L + 1] = o;
+                lds[2 * L] = ilv::to_ilv(lo32, hi32, 0);
+                lds[2 * L + 1] = ilv::to_ilv(lo32, hi32, 1);
             }
             __syncthreads();
         }
