@@ -32,16 +32,12 @@ namespace {
 constexpr bool kSidePrio = MK_SIDE_PRIO != 0;  // library side/copy streams at high priority
 // a whole trie's top (every level from the first of <= 2^20 nodes) in one
 // launch, k_trie_top_fused (0: the k_trie_level / k_trie_top3 / k_trie_spread chain)
-#ifndef MK_TRIE_TOP_FUSED
 #define MK_TRIE_TOP_FUSED 1
-#endif
 #define MK_TRIE_TOP_MAX_LOG2 17
 constexpr uint64_t kTrieTopMax = 1ull << MK_TRIE_TOP_MAX_LOG2;  // trie levels at or below: k_trie_top3
 constexpr uint64_t kTrieTopWgs = 256;
 constexpr uint64_t kAppendMaxRange = 1020;  // k_trie_append<1024>: one parent per lane pair
-#ifndef MK_STAGE_BYTES
 #define MK_STAGE_BYTES (32ull << 20)
-#endif
 constexpr size_t kStageBytes = MK_STAGE_BYTES;  // H2D chunk of the multi-device upload
 
 #define HIPCHK(x)                                                                            \
@@ -686,9 +682,7 @@ int host_tree_hash_elems_plain(const uint8_t* elems, uint64_t n, uint32_t elem_l
 // crosses PCIe while shard i's passes run, so the compute hides under the
 // copy (8 GiB: copy then compute 162-164 ms) and the device holds
 // two shard regions instead of the whole input.
-#ifndef MK_HOST_OVERLAP_MIN_LOG2
 #define MK_HOST_OVERLAP_MIN_LOG2 28  // bytes; 64 = never
-#endif
 int host_merkle_hash(const uint8_t* items, uint64_t n, uint32_t item_len, uint8_t* out) {
     if (!out || (n && item_len && !items)) return fail(MK_EINVAL, "null pointer");
     const uint64_t inb = n * (uint64_t)item_len;
@@ -902,9 +896,7 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
 
 uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 // host-buffer entries: H2D in up to kH2dChunks pieces of at least kH2dMinChunk records
-#ifndef MK_H2D_CHUNKS
 #define MK_H2D_CHUNKS 8
-#endif
 // (smaller floors measured slower: C1's 16,384 records 0.212 ms in one piece,
 // 0.280 / 0.421 ms in 4 / 8 pieces; the per-piece copy + event cost outweighs
 // the overlap, profiles/r05/h2d_chunk_ab.txt)

@@ -765,9 +765,7 @@ __device__ __forceinline__ void round_lh(uint32_t& lo, uint32_t& hi, const LaneL
     hi = __builtin_amdgcn_bitop3_b32(chi3(bh, dpp<kShl1>(bh), dpp<kShl2>(bh)), c.iota, rch, 0x78);
 }
 
-#ifndef MK_SPREAD_UNROLL
 #define MK_SPREAD_UNROLL 24
-#endif
 __device__ __forceinline__ void keccak_f(uint32_t& e, uint32_t& o, const Lane& c) {
 #pragma unroll MK_SPREAD_UNROLL
     for (int r = 0; r < 24; ++r) round_fn(e, o, c, ilv::kRcE[r], ilv::kRcO[r]);

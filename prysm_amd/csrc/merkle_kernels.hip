@@ -238,9 +238,7 @@ __device__ __forceinline__ void hash_node_lock(uint4 l0, uint4 l1, uint4 r0, uin
 }
 
 // Node-pass inputs (read once; MK_NODE_NT=1: non-temporal)
-#ifndef MK_NODE_NT
 #define MK_NODE_NT 0
-#endif
 __device__ __forceinline__ uint4 ld_node(const uint4* p) {
     if constexpr (MK_NODE_NT) {
         const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
@@ -474,9 +472,7 @@ k_reduce(ReduceArgs a) {
 // repeats unit 7) plus one of unit 8 into rows 576..639 (160 KB of LDS).
 // One process, 2^28 (profiles/r03q): fetch 12.14 -> 8.89 GB per leaf pass
 // (1.41x -> 1.03x the algorithmic 8.59 GB), leaf pass 8.138 -> 8.071 ms.
-#ifndef MK_LOCK_NT
 #define MK_LOCK_NT 1
-#endif
 // The DMA of each phase in three parts spread over a permutation instead of
 // one burst (the C5 front's finding): phase B (the window's
 // second block) 3 + 2 + 2 instructions before round 0 and after rounds B1,
@@ -485,18 +481,14 @@ k_reduce(ReduceArgs a) {
 // process A/B (profiles/r05/leaf_dma_split/, 7-9 interleaved rounds, two
 // boxes): 2^28 tree -0.6..-0.8 % (leaf pass 7.943 -> 7.885 ms at 2/8/14),
 // 2^25 -2.6 %.  0: one burst each (round 4's form).
-#ifndef MK_LOCK_DMA_SPLIT
 #define MK_LOCK_DMA_SPLIT 1
-#endif
 #define MK_LOCK_SPLIT_B1 4
 #define MK_LOCK_SPLIT_B2 8
 #define MK_LOCK_SPLIT_A1 2
 #define MK_LOCK_SPLIT_A2 8
 constexpr int kLockAux = MK_LOCK_NT ? 2 : 0;  // global_load_lds aux: nt
 // the side configs' locked kernels (C2 messages, C3 records): inputs read once
-#ifndef MK_SIDE_NT
 #define MK_SIDE_NT 0
-#endif
 constexpr int kSideAux = MK_SIDE_NT ? 2 : 0;
 template <int NU, int U0, int AUX = 0, int I0 = 0, int I1 = NU>
 __device__ __forceinline__ void lock_dma_c(uint4* Bw, const uint4* __restrict__ Rj, uint32_t lane) {
@@ -1375,9 +1367,7 @@ template __global__ void k_wave3<1024, true>(ReduceArgs);
 // process A/B (profiles/r05/c5_front_ab/ab_knobs.txt): the pipelined stream
 // 0.4386 -> 0.4231 ms/step at priority 1 (0.4239 at 3); 0 = the default
 // wave priority.
-#ifndef MK_TRIE_TOP_PRIO
 #define MK_TRIE_TOP_PRIO 1
-#endif
 // Narrow top of the deposit trie, bit-interleaved lane pairs (mk::ilv): the
 // workgroup owns NT input nodes of level d (NT/2 lane pairs) and writes
 // `levels` levels to the (plain) level array; once the count is 1 it goes on
@@ -2472,18 +2462,12 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 // and 0.4163 -> 0.4092 ms/step (4/10/16 against all after 12), one trie
 // 0.543 -> 0.515 and 0.561 -> 0.534 ms; two parts -1.1 %, one unit per round
 // or two -0.4 to -1.1 %.
-#ifndef MK_TRIE_DMA_SPLIT
 #define MK_TRIE_DMA_SPLIT 4
-#endif
-#ifndef MK_TRIE_DMA_SPLIT3
 #define MK_TRIE_DMA_SPLIT3 10
-#endif
-#ifndef MK_TRIE_DMA_ROUND
 // round of a block's permutation after which the next block's DMA (its last
 // part) goes out; as one part: 12 (mid-permutation) over 0, one trie 1.2-2.3
 // % faster on two boxes (profiles/r04/trie_dma_ab/); in three parts: 16
 #define MK_TRIE_DMA_ROUND 16
-#endif
 
 // PIPE (a stream of tries, pipeline.TriePipeline): workgroup b also takes the
 // previous trie's subtree over its level-2 nodes [1024 b, 1024 b + 1024) up

@@ -27,12 +27,8 @@ __global__ void k_reduce(ReduceArgs a);
 constexpr uint32_t kLockThreads = 1024;
 constexpr uint64_t kLockWindows = 4 * kLockThreads;
 __global__ void k_leaf_lock_sc(ReduceArgs a, uint64_t ngroups);  // coalesced LDS-DMA staging, persistent grid
-#ifndef MK_LOCK_DMA_ROUND
 #define MK_LOCK_DMA_ROUND 14  // k_leaf_lock_sc: round of a window's second permutation after which the last part of the next block 1 is fetched
-#endif
-#ifndef MK_LOCK_GRID
 #define MK_LOCK_GRID 256
-#endif
 template <bool FAST>
 __global__ void k_reduce_elem(ReduceArgs a);
 // phase-locked element windows: nwin window digests (level-1 nodes) of 8 x 32-B elements each
@@ -98,15 +94,9 @@ template <uint32_t NT, int DPT, bool PIPE>
 __global__ void k_trie_rec_lock(const uint2* in, uint64_t ngroups, uint4* L0, uint4* L1, uint4* L2, uint4* L3,
                                 TriePrev prev);
 #define MK_TRIE_LOCK 1
-#ifndef MK_TRIE_LOCK_NT
 #define MK_TRIE_LOCK_NT 1024  // threads per workgroup (one workgroup per CU)
-#endif
-#ifndef MK_TRIE_LOCK_DPT
 #define MK_TRIE_LOCK_DPT 4  // deposits per thread: 4 = levels 1-2 fused, 8 = levels 1-3
-#endif
-#ifndef MK_TRIE_LOCK_GRID
 #define MK_TRIE_LOCK_GRID 256  // persistent grid cap
-#endif
 #define MK_TRIE_LOCK_MIN (1u << 18)  // deposits: at least one group per CU
 
 #define MK_REC_THREADS 256
