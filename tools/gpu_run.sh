@@ -20,6 +20,12 @@
 #   rankstep:LOG2N:WORLD    tools/rank_step_probe.py (one rank's pipelined step, 3 sets)
 #   rehearse8               tools/rehearse8.sh (8 gloo ranks sharing the GPU, golden root)
 #   e2e:LOG2N:MODE          tools/e2e_host.py (host-buffer call incl. PCIe; MODE "tree" or empty)
+#   single:CFGS             tools/single_probe.py (C5 one trie, C3 one state, C1 device-resident;
+#                           CFGS '+'-joined, e.g. c3+c5), 200 steps, then a kernel trace of 30
+#   topprobe                tools/top_probe (built here with -DMK_TOP_STAMPS=1): per-level cycles
+#                           of the fused trie top and of C3's fused list top
+#   pmcsingle:CFG:KERNEL    PMC passes (LDS/waits/VALU, FETCH_SIZE, TCC hit/miss) of the
+#                           single_probe loop of CFG, summarised for the kernel name substring KERNEL
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -74,6 +80,26 @@ for step in "$@"; do
       timeout -k 10 300 python tools/e2e_host.py $a $b > $O/e2e_${a}_$b.json 2> $O/e2e_${a}_$b.err \
         || { tail -5 $O/e2e_${a}_$b.err; exit 1; }
       cat $O/e2e_${a}_$b.json ;;
+    single)
+      timeout -k 10 300 python tools/single_probe.py ${a//+/ } --steps 200 --warmup 40 > $O/single_$name.txt 2>&1 \
+        || { tail -5 $O/single_$name.txt; exit 1; }
+      grep config $O/single_$name.txt
+      timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tr_$name -o run --output-format csv -- \
+        python3 tools/single_probe.py ${a//+/ } --steps 30 --warmup 5 > $O/tr_$name.log 2>&1 || { tail -5 $O/tr_$name.log; exit 1; } ;;
+    topprobe)
+      (cd tools && hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMK_TOP_STAMPS=1 -I../prysm_amd/csrc -I../include \
+        top_probe.hip -o /tmp/top_probe) > $O/topprobe_build.log 2>&1 || { tail -5 $O/topprobe_build.log; exit 1; }
+      timeout -k 5 60 /tmp/top_probe 5 > $O/top_probe_trie.json && timeout -k 5 60 /tmp/top_probe 5 merkle > $O/top_probe_merkle.json \
+        || exit 1
+      cat $O/top_probe_merkle.json ;;
+    pmcsingle)
+      D=$O/pmc_$a
+      for pass in "lds:SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" \
+                  "fetch:FETCH_SIZE" "sq:TCC_HIT_sum TCC_MISS_sum"; do
+        timeout -s KILL 120 rocprofv3 --pmc ${pass#*:} -d $D/${pass%%:*} -o run --output-format csv -- \
+          python3 tools/single_probe.py $a --steps 20 --warmup 5 >> $D.log 2>&1 || { tail -5 $D.log; exit 1; }
+      done
+      KERNEL=$b python3 tools/pmc_summary.py $D > $O/pmc_$a.json && echo "pmc $a ok" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
