@@ -2926,6 +2926,80 @@ template __global__ void k_trie_spread<4>(uint32_t*, uint64_t, uint32_t, uint64_
 template __global__ void k_trie_spread<16>(uint32_t*, uint64_t, uint32_t, uint64_t, uint64_t, uint32_t, uint32_t,
                                            uint32_t*, SpreadLeaves);
 
+// ONE deposit appended to a trie of `count` (powchain's one log at a time,
+// powchain/service.go:379-386 -> UpdateDepositTrie, deposit_trie.go:29-40): the
+// leaf hash and its whole path to the root on one wave as a register chain
+// (lo/hi spread form).  The path's left siblings (node (count >> d) - 1 of
+// level d wherever count >> d is odd; a missing right sibling is 0^32) are all
+// loaded into LDS up front, so no level waits on a global load; the new node
+// moves to the right half of the next message (Keccak lanes 4..7) with one
+// ds_bpermute pair when it is a right child.  Every node of the path is
+// stored (GenerateMerkleBranch reads them).  Replaces k_trie_spread<1> for
+// k = 1 (one LDS exchange, one dependent load of a sibling and a barrier per
+// level there).
+__global__ __launch_bounds__(64) void k_trie_append1(uint32_t* __restrict__ levels, uint64_t cap, uint64_t count,
+                                                     uint32_t depth, uint32_t* __restrict__ root_out,
+                                                     SpreadLeaves lv) {
+    if constexpr (MK_TRIE_TOP_PRIO > 0) __builtin_amdgcn_s_setprio(MK_TRIE_TOP_PRIO);
+    __shared__ uint2 sib[64][4];
+    const uint32_t L = threadIdx.x;
+    const spread::LaneLH cst = spread::lane_consts_lh(L);
+    const uint32_t i = cst.i;
+    const uint2* lv2 = reinterpret_cast<const uint2*>(levels);
+    // the path's left siblings, 4 words per level, one word per thread a pass
+    for (uint32_t q = L; q < 4 * depth; q += 64) {
+        const uint32_t d = q >> 2, w = q & 3u;
+        uint64_t off = 0, capd = cap;
+        for (uint32_t k = 0; k < d; ++k) {
+            off += capd;
+            capd = (capd + 1) / 2;
+        }
+        const uint64_t j = count >> d;
+        sib[d][w] = (j & 1u) ? lv2[4 * (off + j - 1) + w] : make_uint2(0, 0);
+    }
+    uint32_t lo = 0u, hi = 0u;
+    const uint64_t len = lv.offs ? lv.offs[1] - lv.offs[0] : lv.fixed_len;
+    const uint8_t* dep = lv.data + (lv.offs ? lv.offs[0] : 0);
+    if (lv.aligned8)
+        spread_sponge<true>(dep, len, cst, lo, hi);
+    else
+        spread_sponge<false>(dep, len, cst, lo, hi);
+    uint2* lvw = reinterpret_cast<uint2*>(levels);
+    if (L < 4u) lvw[4 * count + L] = make_uint2(lo, hi);
+    __syncthreads();  // the siblings are in LDS
+    uint64_t off = 0, capd = cap;
+    for (uint32_t d = 0; d < depth; ++d) {
+        const uint64_t j = count >> d;
+        const bool right = (j & 1u) != 0;  // wave-uniform
+        // the node, from the digest lanes (Keccak lanes 0..3 = GPU lanes 0..3)
+        // to Keccak lanes 4..7 when it is the right child
+        uint32_t rlo = 0u, rhi = 0u;
+        if (right) {
+            const uint32_t src = 4u * (i >= 4u && i < 8u ? i - 4u : 0u);
+            rlo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)lo);
+            rhi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)hi);
+        }
+        uint32_t mlo = 0u, mhi = 0u;
+        if (i < 4u) {
+            const uint2 sv = sib[d][i];
+            mlo = right ? sv.x : lo;
+            mhi = right ? sv.y : hi;
+        } else if (i < 8u && right) {
+            mlo = rlo;
+            mhi = rhi;
+        }
+        if (i == 8u) mlo ^= 1u;  // byte 64
+        if (i == 16u) mhi ^= 0x80000000u;
+        lo = mlo;
+        hi = mhi;
+        spread::keccak_f_lh(lo, hi, cst);
+        off += capd;
+        capd = (capd + 1) / 2;
+        if (L < 4u) lvw[4 * (off + (j >> 1)) + L] = make_uint2(lo, hi);
+    }
+    if (L < 4u) reinterpret_cast<uint2*>(root_out)[L] = make_uint2(lo, hi);
+}
+
 // ----------------------------------------------------------------------------
 // Fused tree tops (round 6): every level above a complete level of a tree in
 // ONE launch, for the callers that build one tree at a time (one trie from

@@ -150,6 +150,8 @@ struct MerkleTopArgs {
 };
 template <uint32_t NT>
 __global__ void k_merkle_top_fused(MerkleTopArgs a);
+__global__ void k_trie_append1(uint32_t* levels, uint64_t cap, uint64_t count, uint32_t depth, uint32_t* root_out,
+                               SpreadLeaves lv);
 template <uint32_t NW>
 __global__ void k_trie_prefix_roots(const uint4* levels, uint64_t cap, uint64_t count0, uint64_t m, uint32_t depth,
                                     uint4* roots);
