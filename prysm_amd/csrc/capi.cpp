@@ -1060,11 +1060,6 @@ int launch_trie_spread(void* d_levels, uint64_t cap, uint32_t d, uint64_t lo, ui
     return MK_OK;
 }
 
-// Levels d_from+1 .. d_to of the batch build over `n` deposits, level d_from
-// complete; the root (level depth node 0) to d_root32 when d_to == depth.
-// nt_max / spread_max: the largest k_trie_top3 workgroup and k_trie_spread
-// wave count (256 / 4: at most one wave per SIMD, which fits beside a
-// resident k_trie_rec_lock<1024, 4, true> workgroup of 104 VGPRs).
 // Arrival-counter slot of the next fused-top launch (mk::g_arrive, round
 // robin; the kernel's last workgroup resets it).
 uint32_t next_arrive_slot() {
@@ -1072,6 +1067,11 @@ uint32_t next_arrive_slot() {
     return next.fetch_add(1, std::memory_order_relaxed) % mk::kArriveSlots;
 }
 
+// Levels d_from+1 .. d_to of the batch build over `n` deposits, level d_from
+// complete; the root (level depth node 0) to d_root32 when d_to == depth.
+// nt_max / spread_max: the largest k_trie_top3 workgroup and k_trie_spread
+// wave count (256 / 4: at most one wave per SIMD, which fits beside a
+// resident k_trie_rec_lock<1024, 4, true> workgroup of 104 VGPRs).
 int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from, uint32_t d_to, uint32_t depth,
                       void* d_root32, hipStream_t st, uint32_t nt_max = mk::kMidThreads,
                       uint32_t spread_max = mk::kSpreadWavesMax, bool fused = false) {
@@ -1166,7 +1166,7 @@ int trie_suffix_levels(void* d_levels, uint64_t cap, uint64_t n, uint64_t done, 
 // Batch build front over an empty trie: leaf hashes into level 0, then
 // levels 1 .. d_to.  A whole trie in one call (d_to == depth) of 280-B
 // deposits at a 16-B aligned address: whole groups of the phase-locked
-// k_trie_rec_lock (leaves + levels 1..log2(DPT) in one launch), the rest (a
+// k_trie_rec_lock_sm (leaves + levels 1-2 in one launch), the rest (a
 // partial group) k_keccak_rec + k_trie_level.  A front whose top the caller
 // runs elsewhere (d_to < depth: pipeline.TriePipeline overlaps trie i's top
 // with trie i+1's front) keeps the free-running kernels: a locked workgroup
@@ -1175,8 +1175,7 @@ int trie_suffix_levels(void* d_levels, uint64_t cap, uint64_t n, uint64_t done, 
 // tries 0.514 -> 0.604 ms/step).
 int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t* d_offs, uint64_t n,
                uint32_t fixed_len, uint32_t d_to, uint32_t depth, void* d_root32, hipStream_t st) {
-    constexpr uint32_t NT = MK_TRIE_LOCK_NT, DPT = MK_TRIE_LOCK_DPT;
-    constexpr uint32_t nlv = DPT == 8 ? 3 : DPT == 4 ? 2 : 1;
+    constexpr uint32_t NT = 1024, DPT = 4, nlv = 2;  // k_trie_rec_lock_sm: 4 slots per thread, levels 0-2
     const uint64_t ng = (MK_TRIE_LOCK && !d_offs && fixed_len == 280 && ((uintptr_t)d_data % 16) == 0 &&
                          n >= MK_TRIE_LOCK_MIN && d_to == depth && depth >= nlv)
                             ? n / (NT * DPT)
@@ -1187,13 +1186,17 @@ int trie_front(void* d_levels, uint64_t cap, const void* d_data, const uint64_t*
                                  mk::kSpreadWavesMax, d_to == depth);
     }
     if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
-    uint4* L[4] = {nullptr, nullptr, nullptr, nullptr};
+    uint4* L[3];
     for (uint32_t d = 0; d <= nlv; ++d) L[d] = trie_level(d_levels, cap, d);
     // persistent: every workgroup runs the same number of groups where possible
     const uint64_t cap_wg = std::min<uint64_t>(MK_TRIE_LOCK_GRID, lock_grid_cap(st));
     const uint64_t grid = ceil_div(ng, ceil_div(ng, cap_wg));
-    hipLaunchKernelGGL((mk::k_trie_rec_lock<NT, DPT, false>), dim3(grid), dim3(NT), 0, st, (const uint2*)d_data, ng,
-                       L[0], L[1], L[2], L[3], mk::TriePrev{});
+    // slot-major (lane m, slot i: deposit 64 i + m), not the row form of the
+    // stream's k_trie_rec_lock<1024, 4, true> (deposits 4m .. 4m + 3 per
+    // lane): one trie 0.4908-0.4913 -> 0.4781-0.4798 ms, fetch 561 -> 535 MB
+    // (profiles/r06/c5_slot_major/, interleaved on one box)
+    hipLaunchKernelGGL(mk::k_trie_rec_lock_sm<NT>, dim3(grid), dim3(NT), 0, st, (const uint2*)d_data, ng, L[0], L[1],
+                       L[2]);
     HIPCHK(hipGetLastError());
     const uint64_t done = ng * NT * DPT;
     if (done < n) {

@@ -2679,10 +2679,206 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock(const uint2* __restrict
     }
     flush();
 }
-template __global__ void k_trie_rec_lock<MK_TRIE_LOCK_NT, MK_TRIE_LOCK_DPT, false>(const uint2*, uint64_t, uint4*,
-                                                                                  uint4*, uint4*, uint4*, TriePrev);
 template __global__ void k_trie_rec_lock<1024, 4, true>(const uint2*, uint64_t, uint4*, uint4*, uint4*, uint4*,
                                                         TriePrev);
+
+// Slot-major form of the whole-trie front (round 6, the verdict's A/B; the
+// one-trie front since, profiles/r06/c5_slot_major/): lane m of wave w hashes deposits base + 64 i + m
+// (slot i = 0..3, base = the wave's first of 256), so a DMA phase reads 64
+// consecutive deposits and the lines two consecutive deposits share are
+// fetched by adjacent parts, where the row form fetches every fourth such
+// line seven phases apart.  The blocks are staged and read exactly as in
+// k_trie_rec_lock (9 units per lane, rows at stride 9), with the 8-B offset
+// now per lane (deposit parity = lane parity).  An even lane's tail word is
+// the first word of the NEXT lane's block-0 image (read before block 1's
+// copy lands); an odd lane's block-1 image ends with it.  Leaves sit in
+// consecutive lanes, so the folds move them with ds_bpermute: after slots 1
+// and 3 one locked permutation hashes the 64 level-1 nodes of the two slots
+// (lane m: slot pair half m >> 5, pair m & 31), after slot 3 one more the 64
+// level-2 nodes (lane m: level-1 nodes 2m, 2m + 1) -- 15 locked permutations
+// per thread, as in the row form; levels 0-2 are stored as consecutive
+// nodes per wave.
+template <uint32_t NT>
+__global__ __launch_bounds__(NT, 1) void k_trie_rec_lock_sm(const uint2* __restrict__ in, uint64_t ngroups,
+                                                            uint4* __restrict__ L0, uint4* __restrict__ L1,
+                                                            uint4* __restrict__ L2) {
+    constexpr uint32_t NW = 35;  // 8-B words per deposit
+    __shared__ uint4 buf[NT / 64][9 * 64];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint4* Bw = buf[wave];
+    auto first = [&](uint64_t g) { return (g * NT + 64 * wave) * 4; };  // the wave's first deposit
+    // units [k0, k1) of slot i's block b (the slot's 64 deposits start 16-B aligned)
+    auto dma = [&](uint64_t g, int i, int b, int k0, int k1) {
+        const uint8_t* region = reinterpret_cast<const uint8_t*>(in + (first(g) + 64u * i) * NW);
+        uint32_t ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int k = k0; k < k1; ++k) {
+            const uint32_t U = 64u * k + ln;
+            const uint32_t m = U / 9, u = U - m * 9;
+            const uint32_t start = m * (8 * NW) + 136 * b;
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(region + (start & ~15u) + 16 * u),
+                                             (__attribute__((address_space(3))) void*)(Bw + 64 * k), 16, 0,
+                                             MK_TRIE_LOCK_AUX);
+        }
+    };
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;  // a node stored after the next wait
+    uint4* qp = nullptr;
+    auto flush = [&] {
+        if (qp) {
+            qp[0] = q0;
+            qp[1] = q1;
+        }
+        qp = nullptr;
+    };
+    // 17 words of this lane's staged block into st (rows at stride 9; the
+    // block starts o8 words into unit 0); returns word 17
+    auto absorb = [&](State& st, uint32_t o8, auto setc) {
+        constexpr bool SET = decltype(setc)::value;
+        const bool sh = o8 != 0;
+        uint4 prev = Bw[9 * lane];
+        uint2 w17 = make_uint2(0, 0);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const uint4 cur = k + 1 < 9 ? Bw[9 * lane + k + 1] : make_uint4(0, 0, 0, 0);
+            const uint32_t a0 = sh ? prev.z : prev.x, a1 = sh ? prev.w : prev.y;
+            const uint32_t b0 = sh ? cur.x : prev.z, b1 = sh ? cur.y : prev.w;
+            const int wa = 2 * k, wb = 2 * k + 1;
+            st.lo[wa] = SET ? a0 : st.lo[wa] ^ a0;
+            st.hi[wa] = SET ? a1 : st.hi[wa] ^ a1;
+            if (wb < 17) {
+                st.lo[wb] = SET ? b0 : st.lo[wb] ^ b0;
+                st.hi[wb] = SET ? b1 : st.hi[wb] ^ b1;
+            } else {
+                w17 = make_uint2(prev.z, prev.w);
+            }
+            prev = cur;
+            asm volatile("" ::: "memory");
+        }
+        return w17;
+    };
+    // node (x, y of two uint4) of lane `src` (8 bpermutes)
+    auto bperm8 = [](uint32_t src, const uint4& a, const uint4& b, uint4& ra, uint4& rb) {
+        const int ad = (int)(4u * src);
+        ra.x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)a.x);
+        ra.y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)a.y);
+        ra.z = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)a.z);
+        ra.w = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)a.w);
+        rb.x = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)b.x);
+        rb.y = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)b.y);
+        rb.z = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)b.z);
+        rb.w = (uint32_t)__builtin_amdgcn_ds_bpermute(ad, (int)b.w);
+    };
+    auto sel4 = [](bool c, const uint4& a, const uint4& b) {
+        return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+    };
+    // level-1 nodes of slots (i0, i0 + 1) from their leaves in (xa, ya) / (xb, yb):
+    // lane m hashes pair m & 31 of slot i0 + (m >> 5)
+    auto level1 = [&](const uint4& xa, const uint4& ya, const uint4& xb, const uint4& yb, uint4& n0, uint4& n1) {
+        const uint32_t p = lane & 31u;
+        const bool hi_half = lane >= 32u;
+        uint4 la0, la1, lb0, lb1, ra0, ra1, rb0, rb1;
+        bperm8(2 * p, xa, ya, la0, la1);
+        bperm8(2 * p, xb, yb, lb0, lb1);
+        bperm8(2 * p + 1, xa, ya, ra0, ra1);
+        bperm8(2 * p + 1, xb, yb, rb0, rb1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        hash_node_lock(sel4(hi_half, lb0, la0), sel4(hi_half, lb1, la1), sel4(hi_half, rb0, ra0),
+                       sel4(hi_half, rb1, ra1), n0, n1);
+    };
+    using Set = std::true_type;
+    using Xor = std::false_type;
+    uint64_t g = blockIdx.x;
+    if (g < ngroups) {
+        dma(g, 0, 0, 0, 9);
+    }
+#pragma unroll 1
+    for (; g < ngroups; g += gridDim.x) {
+        const uint64_t gn = g + gridDim.x;
+        const uint64_t base = first(g);
+        uint4 xa = make_uint4(0, 0, 0, 0), ya = xa;  // leaf of the even slot of a pair
+        uint4 n10 = xa, n11 = xa;                    // level-1 node of slots 0, 1
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            State s;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 0 landed
+            flush();
+            // an even lane's tail word: the first word of the next lane's block-0 image
+            uint2 te = make_uint2(0, 0);
+            if (!(lane & 1u)) {
+                const uint4 v = Bw[9 * (lane + 1)];
+                te = make_uint2(v.x, v.y);
+            }
+            absorb(s, lane & 1u, Set{});
+#pragma unroll
+            for (int w = 17; w < 25; ++w) s.lo[w] = s.hi[w] = 0;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // rows read: block 1 may land
+            keccak_f_lock_mid3<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_SPLIT3, MK_TRIE_DMA_ROUND>(
+                s, [&] { dma(g, i, 1, 0, 3); }, [&] { dma(g, i, 1, 3, 6); }, [&] { dma(g, i, 1, 6, 9); });
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block 1 landed
+            const uint2 to = absorb(s, (lane + 1) & 1u, Xor{});
+            const uint2 tl = (lane & 1u) ? to : te;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            auto next_dma = [&](int k0, int k1) {
+                if (i + 1 < 4)
+                    dma(g, i + 1, 0, k0, k1);
+                else if (gn < ngroups)
+                    dma(gn, 0, 0, k0, k1);
+            };
+            keccak_f_lock_mid3<MK_TRIE_DMA_SPLIT, MK_TRIE_DMA_SPLIT3, MK_TRIE_DMA_ROUND>(
+                s, [&] { next_dma(0, 3); }, [&] { next_dma(3, 6); }, [&] { next_dma(6, 9); });
+            s.lo[0] ^= tl.x;  // word 34, then the domain pad byte
+            s.hi[0] ^= tl.y;
+            s.lo[1] ^= 1u;
+            s.hi[16] ^= 0x80000000u;
+            keccak_f_digest_lock(s);
+            uint4 d0, d1;
+            digest(s, d0, d1);
+            uint4* leaf = L0 + 2 * (base + 64u * i + lane);
+            if (!(i & 1)) {
+                xa = d0;
+                ya = d1;
+                q0 = d0;  // stored after the next wait
+                q1 = d1;
+                qp = leaf;
+            } else {
+                leaf[0] = d0;  // covered by the node permutation below
+                leaf[1] = d1;
+                uint4 n0, n1;
+                level1(xa, ya, d0, d1, n0, n1);
+                uint4* nd = L1 + 2 * (base / 2 + 64u * (i >> 1) + lane);
+                if (i == 1) {
+                    n10 = n0;
+                    n11 = n1;
+                    q0 = n0;
+                    q1 = n1;
+                    qp = nd;
+                } else {
+                    nd[0] = n0;
+                    nd[1] = n1;
+                    // level 2: lane m hashes level-1 nodes 2m, 2m + 1 (of slots 0-1
+                    // for m < 32, of slots 2-3 after)
+                    const bool hi_half = lane >= 32u;
+                    const uint32_t src = (2u * lane) & 63u;
+                    uint4 la0, la1, lb0, lb1, ra0, ra1, rb0, rb1;
+                    bperm8(src, n10, n11, la0, la1);
+                    bperm8(src, n0, n1, lb0, lb1);
+                    bperm8(src + 1, n10, n11, ra0, ra1);
+                    bperm8(src + 1, n0, n1, rb0, rb1);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    uint4 m0, m1;
+                    hash_node_lock(sel4(hi_half, lb0, la0), sel4(hi_half, lb1, la1), sel4(hi_half, rb0, ra0),
+                                   sel4(hi_half, rb1, ra1), m0, m1);
+                    q0 = m0;
+                    q1 = m1;
+                    qp = L2 + 2 * (base / 4 + lane);
+                }
+            }
+        }
+    }
+    flush();
+}
+template __global__ void k_trie_rec_lock_sm<1024>(const uint2*, uint64_t, uint4*, uint4*, uint4*);
 
 // ----------------------------------------------------------------------------
 // Deposit trie level: node j = K(in[2j] || (2j+1 < cin ? in[2j+1] : 0^32)),
@@ -3031,7 +3227,7 @@ __device__ uint64_t g_top_stamps[1024 * 64];
     do { if (threadIdx.x == 0) g_top_stamps[blockIdx.x * 64 + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define TOP_STAMP(k) \
-    do { } while (0)
+    do { (void)(k); } while (0)
 #endif
 
 namespace {

@@ -93,9 +93,9 @@ struct TriePrev {
 template <uint32_t NT, int DPT, bool PIPE>
 __global__ void k_trie_rec_lock(const uint2* in, uint64_t ngroups, uint4* L0, uint4* L1, uint4* L2, uint4* L3,
                                 TriePrev prev);
+template <uint32_t NT>
+__global__ void k_trie_rec_lock_sm(const uint2* in, uint64_t ngroups, uint4* L0, uint4* L1, uint4* L2);
 #define MK_TRIE_LOCK 1
-#define MK_TRIE_LOCK_NT 1024  // threads per workgroup (one workgroup per CU)
-#define MK_TRIE_LOCK_DPT 4  // deposits per thread: 4 = levels 1-2 fused, 8 = levels 1-3
 #define MK_TRIE_LOCK_GRID 256  // persistent grid cap
 #define MK_TRIE_LOCK_MIN (1u << 18)  // deposits: at least one group per CU
 
