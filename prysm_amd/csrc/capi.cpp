@@ -1060,12 +1060,19 @@ int launch_trie_spread(void* d_levels, uint64_t cap, uint32_t d, uint64_t lo, ui
     return MK_OK;
 }
 
-// Arrival-counter slot of the next fused-top launch (mk::g_arrive, round
-// robin; the kernel's last workgroup resets it).
-uint32_t next_arrive_slot() {
-    static std::atomic<uint32_t> next{0};
-    return next.fetch_add(1, std::memory_order_relaxed) % mk::kArriveSlots;
+// First of `k` consecutive arrival-counter slots for the next fused-top
+// launch (mk::g_arrive, round robin, never running past the last slot; each
+// counter's last arriving workgroup resets it).
+uint32_t next_arrive_slots(uint32_t k) {
+    static std::atomic<uint64_t> next{0};
+    uint64_t cur = next.load(std::memory_order_relaxed), start;
+    do {
+        const uint64_t base = cur % mk::kArriveSlots;
+        start = base + k > mk::kArriveSlots ? cur + (mk::kArriveSlots - base) : cur;
+    } while (!next.compare_exchange_weak(cur, start + k, std::memory_order_relaxed));
+    return (uint32_t)(start % mk::kArriveSlots);
 }
+uint32_t next_arrive_slot() { return next_arrive_slots(1); }
 
 // Levels d_from+1 .. d_to of the batch build over `n` deposits, level d_from
 // complete; the root (level depth node 0) to d_root32 when d_to == depth.
@@ -1094,7 +1101,7 @@ int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from,
             ++d;
         }
         hipLaunchKernelGGL(mk::k_trie_top_fused<NT>, dim3(ceil_div(c, NT)), dim3(NT), 0, st, (uint32_t*)d_levels, cap,
-                           c, d, depth, (uint32_t*)d_root32, next_arrive_slot());
+                           c, d, depth, (uint32_t*)d_root32, next_arrive_slots(mk::kTopGroupSlots));
         HIPCHK(hipGetLastError());
         return MK_OK;
     }

@@ -2462,12 +2462,18 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 // and 0.4163 -> 0.4092 ms/step (4/10/16 against all after 12), one trie
 // 0.543 -> 0.515 and 0.561 -> 0.534 ms; two parts -1.1 %, one unit per round
 // or two -0.4 to -1.1 %.
+#ifndef MK_TRIE_DMA_SPLIT
 #define MK_TRIE_DMA_SPLIT 4
+#endif
+#ifndef MK_TRIE_DMA_SPLIT3
 #define MK_TRIE_DMA_SPLIT3 10
+#endif
 // round of a block's permutation after which the next block's DMA (its last
 // part) goes out; as one part: 12 (mid-permutation) over 0, one trie 1.2-2.3
 // % faster on two boxes (profiles/r04/trie_dma_ab/); in three parts: 16
+#ifndef MK_TRIE_DMA_ROUND
 #define MK_TRIE_DMA_ROUND 16
+#endif
 
 // PIPE (a stream of tries, pipeline.TriePipeline): workgroup b also takes the
 // previous trie's subtree over its level-2 nodes [1024 b, 1024 b + 1024) up
@@ -3436,7 +3442,9 @@ __device__ __forceinline__ bool wg_arrive_last(uint32_t slot, uint32_t total, ui
 // one launch: workgroup b takes level-d0 nodes [NT b, NT b +
 // NT) up to level d0 + log2(NT) (every node stored: GenerateMerkleBranch reads
 // them), the last workgroup to arrive the rest, including the zero-sibling
-// levels (deposit_trie.go:33-38) and the root.  grid = ceil(c0 / NT) <= NT.
+// levels (deposit_trie.go:33-38) and the root.  grid = ceil(c0 / NT) <= NT;
+// a grid of more than kTopGroup workgroups also uses the arrival slots after
+// `slot`, one per group of each stage (kTopGroupSlots in all at most).
 template <uint32_t NT>
 __global__ __launch_bounds__(NT) void k_trie_top_fused(uint32_t* __restrict__ levels, uint64_t cap, uint64_t c0,
                                                        uint32_t d0, uint32_t depth, uint32_t* __restrict__ root_out,
@@ -3512,10 +3520,32 @@ __global__ __launch_bounds__(NT) void k_trie_top_fused(uint32_t* __restrict__ le
         // stored above, again write-through) and arrive
         wg_store_node0<true>(lds, levels + 8 * (off + lo));
         TOP_STAMP(nst++);
-        if (!wg_arrive_last(slot, gridDim.x, &flag)) return;
+        uint32_t parts = gridDim.x;  // nodes of level d, one published per workgroup
+        uint32_t gslot = slot + 1;   // arrival slots of this stage's groups
+        while (kTopGroupLog2 > 0 && parts > kTopGroup) {
+            // the last of each kTopGroup workgroups of a stage takes its
+            // group's nodes log2(kTopGroup) levels up, so those levels run on
+            // many CUs at once, not one after another on a lone workgroup (a
+            // missing right sibling is 0^32 here too)
+            const uint32_t b = (uint32_t)lo;  // this workgroup's node of level d
+            const uint32_t grp = b / kTopGroup, g0 = grp * kTopGroup;
+            const uint32_t members = parts - g0 < kTopGroup ? parts - g0 : kTopGroup;
+            const uint32_t groups = (parts + kTopGroup - 1) / kTopGroup;
+            if (!wg_arrive_last(gslot + grp, members, &flag)) return;
+            TOP_STAMP(nst++);
+            lo = g0;
+            m = members;
+            wg_load_nodes<true>(lds, levels + 8 * (off + lo), m);
+            run(d + kTopGroupLog2);
+            wg_store_node0<true>(lds, levels + 8 * (off + lo));
+            TOP_STAMP(nst++);
+            gslot += groups;
+            parts = groups;
+        }
+        if (!wg_arrive_last(slot, parts, &flag)) return;
         TOP_STAMP(nst++);
         lo = 0;
-        m = gridDim.x;
+        m = parts;
         wg_load_nodes<true>(lds, levels + 8 * off, m);
     }
     run(depth);

@@ -128,6 +128,15 @@ __global__ void k_trie_spread(uint32_t* levels, uint64_t cap, uint32_t d0, uint6
                               uint32_t depth, uint32_t* root_out, SpreadLeaves lv);
 // fused tree tops: arrival counter slots (one per fused launch in flight)
 constexpr uint32_t kArriveSlots = 4096;
+// k_trie_top_fused: the last of each kTopGroup workgroups reduces the group's
+// nodes before the last group finishes the top
+// nodes before the next stage / the last group finishes the top (0: the last
+// workgroup alone reduces all the grid's nodes)
+#ifndef MK_TOP_GROUP_LOG2
+#define MK_TOP_GROUP_LOG2 4
+#endif
+constexpr uint32_t kTopGroupLog2 = MK_TOP_GROUP_LOG2, kTopGroup = 1u << kTopGroupLog2;
+constexpr uint32_t kTopGroupSlots = kTopGroupLog2 ? 1 + 2 * 1024 / kTopGroup : 1;  // arrival slots of one launch
 template <uint32_t NT>
 __global__ void k_trie_top_fused(uint32_t* levels, uint64_t cap, uint64_t c0, uint32_t d0, uint32_t depth,
                                  uint32_t* root_out, uint32_t slot);

@@ -102,7 +102,7 @@ int main(int argc, char** argv) {
     for (int it = 0; it < iters; ++it) {
         if (it + 1 == iters) (void)hipMemcpyToSymbol(HIP_SYMBOL(mk::g_top_stamps), zero.data(), zero.size() * 8);
         hipLaunchKernelGGL(mk::k_trie_top_fused<1024>, dim3(grid), dim3(1024), 0, 0, lv, cap, c0, d0, depth, root,
-                           (uint32_t)it);
+                           (uint32_t)(it % 30) * mk::kTopGroupSlots);
         (void)hipDeviceSynchronize();
     }
     std::vector<uint64_t> st(1024 * 64);
