@@ -1997,7 +1997,7 @@ static int launch_top_fused(const TopPlan& p, uint32_t nl, const void* const* no
         t.wg0 = wg;
         t.nwg = p.nwg[l];
         t.span_log2 = p.span_log2[l];
-        t.slot = next_arrive_slot();
+        t.slot = next_arrive_slots(mk::kTopGroupSlots);
         wg += t.nwg;
         sub += 8 * t.nwg;
     }

@@ -3387,13 +3387,14 @@ __device__ __forceinline__ void wg_level(uint32_t* lds, uint32_t m, const spread
     __syncthreads();
 }
 
-// plain node j of `in` (32 B) -> lds as ilv words, thread t loading node t;
-// SC1: agent-scope loads (nodes another CU published in this launch)
+// plain node j of `in` (32 B, `stride` nodes apart) -> lds as ilv words,
+// thread t loading node t; SC1: agent-scope loads (nodes another CU
+// published in this launch)
 template <bool SC1>
-__device__ __forceinline__ void wg_load_nodes(uint32_t* lds, const uint32_t* in, uint32_t m) {
+__device__ __forceinline__ void wg_load_nodes(uint32_t* lds, const uint32_t* in, uint32_t m, uint32_t stride = 1) {
     const uint32_t t = threadIdx.x;
     if (t < m) {
-        const uint64_t* q = reinterpret_cast<const uint64_t*>(in) + 4 * (uint64_t)t;
+        const uint64_t* q = reinterpret_cast<const uint64_t*>(in) + 4 * (uint64_t)t * stride;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
             const uint64_t v = SC1 ? __hip_atomic_load(q + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : q[w];
@@ -3591,9 +3592,35 @@ __global__ __launch_bounds__(NT) void k_merkle_top_fused(MerkleTopArgs a) {
             TOP_STAMP(nst++);
         }
         wg_store_node0<true>(lds, t.sub + 8 * b);
-        if (!wg_arrive_last(t.slot, t.nwg, &flag)) return;
-        m = t.nwg;
-        wg_load_nodes<true>(lds, t.sub, m);
+        // groups of kTopGroup parts first, as in k_trie_top_fused: the last of
+        // each group takes the group's nodes log2(kTopGroup) levels up and
+        // stores its node over the group's first (node idx of a stage at
+        // sub[8 stride idx]).  Every group but a ragged last one is even at
+        // each of those levels, so the ragged group's count has the level's
+        // parity and a lone node there is the level's unpaired last node,
+        // K(l || 0^128), as wg_level hashes it.
+        uint32_t parts = t.nwg, stride = 1, idx = b, gslot = t.slot + 1;
+        while (kTopGroupLog2 > 0 && parts > kTopGroup) {
+            const uint32_t grp = idx / kTopGroup, g0 = grp * kTopGroup;
+            const uint32_t members = parts - g0 < kTopGroup ? parts - g0 : kTopGroup;
+            const uint32_t groups = (parts + kTopGroup - 1) / kTopGroup;
+            if (!wg_arrive_last(gslot + grp, members, &flag)) return;
+            m = members;
+            wg_load_nodes<true>(lds, t.sub + 8 * stride * g0, m, stride);
+            for (uint32_t k = 0; k < kTopGroupLog2; ++k) {
+                wg_level<NT, false>(lds, m, cst, none3, none_p, none_w);
+                m = (m + 1) / 2;
+            }
+            stride *= kTopGroup;
+            idx = grp;
+            wg_store_node0<true>(lds, t.sub + 8 * stride * idx);
+            TOP_STAMP(nst++);
+            gslot += groups;
+            parts = groups;
+        }
+        if (!wg_arrive_last(t.slot, parts, &flag)) return;
+        m = parts;
+        wg_load_nodes<true>(lds, t.sub, m, stride);
         TOP_STAMP(nst++);
     }
     while (m > 1) {

@@ -58,9 +58,9 @@ static int merkle_probe(int iters) {
     }
     std::vector<uint64_t> zero(1024 * 64, 0), st(1024 * 64);
     for (int it = 0; it < iters; ++it) {
-        a.pair_slot = 2000 + it;
-        a.l[0].slot = 2 * it;
-        a.l[1].slot = 2 * it + 1;
+        a.pair_slot = 4000 + it % 30;
+        a.l[0].slot = (2 * (it % 10)) * mk::kTopGroupSlots;
+        a.l[1].slot = (2 * (it % 10) + 1) * mk::kTopGroupSlots;
         if (it + 1 == iters) (void)hipMemcpyToSymbol(HIP_SYMBOL(mk::g_top_stamps), zero.data(), zero.size() * 8);
         hipLaunchKernelGGL(mk::k_merkle_top_fused<1024>, dim3(wg), dim3(1024), 0, 0, a);
         (void)hipDeviceSynchronize();
