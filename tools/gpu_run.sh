@@ -24,6 +24,9 @@
 #                           CFGS '+'-joined, e.g. c3+c5), 200 steps, then a kernel trace of 30
 #   topprobe                tools/top_probe (built here with -DMK_TOP_STAMPS=1): per-level cycles
 #                           of the fused trie top and of C3's fused list top
+#   singleab:CFGS:VARIANTS  tools/single_probe.py CFGS ('+'-joined) against library variants
+#                           (VARIANTS '+'-joined; main = the default build, else
+#                           prysm_amd/lib/variants/libprysm_merkle_<v>.so), 3 interleaved rounds
 #   pmcsingle:CFG:KERNEL    PMC passes (LDS/waits/VALU, FETCH_SIZE, TCC hit/miss) of the
 #                           single_probe loop of CFG, summarised for the kernel name substring KERNEL
 set -u
@@ -92,6 +95,15 @@ for step in "$@"; do
       timeout -k 5 60 /tmp/top_probe 5 > $O/top_probe_trie.json && timeout -k 5 60 /tmp/top_probe 5 merkle > $O/top_probe_merkle.json \
         || exit 1
       cat $O/top_probe_merkle.json ;;
+    singleab)
+      for r in 1 2 3; do
+        for v in ${b//+/ }; do
+          if [ "$v" = main ]; then L=prysm_amd/lib/libprysm_merkle.so; else L=prysm_amd/lib/variants/libprysm_merkle_$v.so; fi
+          PRYSM_MERKLE_LIB=$L timeout -k 10 200 python tools/single_probe.py ${a//+/ } --steps 200 --warmup 40 \
+            > $O/ab_${v}_$r.txt 2>&1 || { tail -5 $O/ab_${v}_$r.txt; exit 1; }
+          sed "s/^/$v /" $O/ab_${v}_$r.txt | tee -a $O/singleab.txt
+        done
+      done ;;
     pmcsingle)
       D=$O/pmc_$a
       for pass in "lds:SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE" \
