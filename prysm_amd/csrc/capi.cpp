@@ -332,7 +332,7 @@ int launch_plan(const Plan& p, const uint8_t* d_items, uint8_t* d_out32, uint8_t
         if (ps.sp) {
             a.wg_base = 0;
             const uint32_t w8 = (((uintptr_t)a.items % 8) == 0 && a.cb % 8 == 0) ? 1u : 0u;
-            hipLaunchKernelGGL(mk::k_spread_leaf, dim3(ps.nwg), dim3(1024), 0, st, a, w8);
+            hipLaunchKernelGGL(mk::k_spread_leaf<16>, dim3(ps.nwg), dim3(1024), 0, st, a, w8);
             HIPCHK(hipGetLastError());
         } else if (ps.wave) {
             a.wg_base = 0;
@@ -952,10 +952,23 @@ int dev_struct_list_root_win(const void* d_rec, uint64_t n, void* d_roots, void*
     return dev_finish_nodes(d_wins, c1, n, d_out32, d_ws, ws_bytes, st);
 }
 
+// The latency form of a small list's tree (dev_list_tree_32): merkleHash of
+// n 32-B items whose first level has 16 < windows <= 2^12.
+static uint64_t latency_windows(uint64_t n) { return ceil_div(ceil_div(32 * n, 128), 2); }
+static bool latency_tree_ok(uint64_t n, const void* d_items) {
+    const uint64_t c1 = latency_windows(n);
+    return c1 > 16 && c1 <= 4096 && (uintptr_t)d_items % 16 == 0;
+}
+static uint64_t latency_tree_ws(uint64_t n) {
+    const uint64_t c4 = ceil_div(latency_windows(n), 8);
+    return align256(32 * c4) + align256(32 * ceil_div(c4, 16));
+}
+
 uint64_t struct_list_ws(uint64_t n, const mk::StructSpec& sp) {
     Plan p;
     uint64_t mws = 256;
     if (mk::make_plan(n, 32, false, 0, false, true, p) == MK_OK && !p.small) mws = mk::plan_ws_bytes(p);
+    if (latency_windows(n) > 16 && latency_windows(n) <= 4096) mws = std::max(mws, latency_tree_ws(n));
     return align256(n * sp.msg_len) + align256(32 * n) + mws;
 }
 
@@ -2006,6 +2019,45 @@ static int launch_top_fused(const TopPlan& p, uint32_t nl, const void* const* no
     return MK_OK;
 }
 
+// merkleHash of n 32-B items (a list's element roots, hash.go:118-139 ->
+// 194-239).  Small lists (16 < windows <= 2^12, C1's 16,384 ValidatorRecord
+// roots: 2,048 windows) in the latency form: k_spread_leaf<8> hashes the
+// windows one per wave, 8 per workgroup (two waves per SIMD, where 16 put
+// four on each: 2 x ~9.8 k cycles against 2 x ~17.8 k), and folds each
+// workgroup's 8 to one node 3 levels up; k_merkle_top_fused takes those nodes
+// 16 per workgroup (4 levels in the spread form), groups of 16 workgroups,
+// and the last to the root and the length mix-in -- where the general plan
+// ran 16 windows per workgroup and one 1024-thread k_wave3 over the last 128
+// nodes, whose widest levels run as lane pairs (~14 k cycles each).
+// Everything else: the general plan (dev_merkle_hash).
+static int dev_list_tree_32(const void* d_items, uint64_t n, void* d_out32, uint8_t* ws, uint64_t ws_bytes,
+                            hipStream_t st) {
+    if (!latency_tree_ok(n, d_items) || ws_bytes < latency_tree_ws(n) || (uintptr_t)ws % 16)
+        return dev_merkle_hash(d_items, n, 32, d_out32, ws, ws_bytes, st);
+    if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
+    const uint64_t total = 32 * n, nchunks = ceil_div(total, 128), c1 = ceil_div(nchunks, 2);
+    mk::ReduceArgs a{};
+    a.items = (const uint8_t*)d_items;
+    a.total = total;
+    a.cb = 128;
+    a.nchunks = nchunks;
+    a.c1 = c1;
+    a.c1_full = total / 256;
+    a.out = ws;
+    a.n_items = n;
+    a.levels = 4;  // the windows + 3 levels: one node per workgroup
+    hipLaunchKernelGGL(mk::k_spread_leaf<8>, dim3(ceil_div(c1, 8)), dim3(1024), 0, st, a, 1u);
+    HIPCHK(hipGetLastError());
+    const uint64_t c4 = ceil_div(c1, 8);
+    TopPlan p;
+    p.span_log2[0] = 4;
+    p.nwg[0] = (uint32_t)ceil_div(c4, 16);
+    p.ws = align256(32 * (uint64_t)p.nwg[0]);
+    const void* nodes[1] = {ws};
+    const uint64_t c[1] = {c4}, nit[1] = {n};
+    return launch_top_fused(p, 1, nodes, c, nit, d_out32, 0, ws + align256(32 * c4), st);
+}
+
 int mk_dev_ssz_merkle_finish_nodes_pair(mk_call* call, const void* d_nodes, uint64_t count, uint64_t n_total,
                                         void* d_pair_block, uint32_t slot, uint32_t epoch, void* d_ws,
                                         uint64_t ws_bytes, void* stream) {
@@ -2075,7 +2127,7 @@ int mk_dev_ssz_struct_list_root(mk_call* call, const void* d_records, uint64_t n
                                                ws_bytes - (uint64_t)(mws - ws), st));
     rc = launch_struct_roots(d_records, n, sp, msg, roots, st);
     if (rc) return S.done(rc);
-    return S.done(dev_merkle_hash(roots, n, 32, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), st));
+    return S.done(dev_list_tree_32(roots, n, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), st));
 }
 
 int mk_ssz_struct_list_level1_ok(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
@@ -2323,7 +2375,7 @@ static int host_struct_list_root(const uint8_t* records, uint64_t n, uint32_t re
         HIPCHK(hipStreamWaitEvent(st, c->h2d, 0));
         TRY(launch_struct_roots(din + off * record_len, cnt, sp, msg + off * sp.msg_len, roots + 32 * off, st));
     }
-    TRY(dev_merkle_hash(roots, n, 32, c->out.p, mws, wsb - (uint64_t)(mws - ws), st));
+    TRY(dev_list_tree_32(roots, n, c->out.p, mws, wsb - (uint64_t)(mws - ws), st));
     HIPCHK(hipMemcpyAsync(out, c->out.p, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return MK_OK;

@@ -3689,13 +3689,15 @@ template __global__ void k_merkle_top_fused<1024>(MerkleTopArgs);
 // windows) continues to the root and the length mix-in.  Where a tree's
 // first level has few windows every wave runs nearly alone, and a window
 // costs 2 x 6.3 k cycles here against 2 x 12.8 k in a lane pair.
+template <uint32_t SPAN>
 __global__ __launch_bounds__(1024) void k_spread_leaf(ReduceArgs a, uint32_t w8) {
+    static_assert(SPAN == 8 || SPAN == 16, "windows per workgroup");
     __shared__ uint2 nodes[16 * 4];
     const uint32_t w = threadIdx.x >> 6, L = threadIdx.x & 63u;
     const spread::LaneLH cst = spread::lane_consts_lh(L);
     const uint32_t i = cst.i;
-    const uint64_t lo1 = (a.wg_base + blockIdx.x) * 16ull;
-    const uint64_t m1 = a.c1 - lo1 < 16 ? a.c1 - lo1 : 16;
+    const uint64_t lo1 = (a.wg_base + blockIdx.x) * (uint64_t)SPAN;
+    const uint64_t m1 = a.c1 - lo1 < SPAN ? a.c1 - lo1 : SPAN;
     if (w < m1) {  // wave-uniform
         const uint64_t j = lo1 + w;
         const uint64_t lo = j * 2 * a.cb;
@@ -3772,6 +3774,8 @@ __global__ __launch_bounds__(1024) void k_spread_leaf(ReduceArgs a, uint32_t w8)
         out[4 * ((lo1 >> done) + w) + L] = nodes[4 * w + L];
     }
 }
+template __global__ void k_spread_leaf<16>(ReduceArgs, uint32_t);
+template __global__ void k_spread_leaf<8>(ReduceArgs, uint32_t);
 
 // Root() after each of m deposits appended at count0 (powchain's saveInTrie
 // reads Root() before every UpdateDepositTrie, service.go:379-386): wave g

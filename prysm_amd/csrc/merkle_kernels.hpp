@@ -114,6 +114,7 @@ __global__ void k_trie_append(uint32_t* levels, uint64_t cap, uint32_t d0, uint6
 #define MK_TRIE_SPREAD 1
 #define MK_SPREAD_WAVES_MAX 16
 constexpr uint32_t kSpreadWavesMax = MK_SPREAD_WAVES_MAX;  // k_trie_spread: one state per wave (<= 4 per SIMD)
+template <uint32_t SPAN>
 __global__ void k_spread_leaf(ReduceArgs a, uint32_t w8);
 // new deposits k_trie_spread hashes into level 0 first (k == 0: none)
 struct SpreadLeaves {
