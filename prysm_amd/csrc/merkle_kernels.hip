@@ -2232,9 +2232,10 @@ template __global__ void k_struct_reg<2, 0>(const uint8_t*, uint64_t, StructSpec
 // where every wave runs alone on its SIMD and the cost is the chain of
 // permutation latencies, not throughput: four lanes per record.  Lanes
 // 0..NB-1 of a record hash its NB bytes fields side by side (one
-// permutation of latency instead of NB), the digests meet in LDS, and lane 0
-// hashes the struct message (2 blocks): 3 serial permutations per record
-// instead of 5.  The host takes this form while 4 lanes per record still fit
+// permutation of latency instead of NB), the digests meet in LDS, and lanes
+// 0 and 1 hash the struct message (2 blocks) as a lo/hi lane pair (round 6:
+// C1's struct roots 29.6 -> see DESIGN §4.5): 3 serial permutations per
+// record instead of 5, the last two at lane-pair latency.  The host takes this form while 4 lanes per record still fit
 // the chip once (n <= kStructSplitMaxN).
 template <int NB, int NRAW>
 __global__ __launch_bounds__(256) void k_struct_split(const uint8_t* __restrict__ rec, uint64_t n, StructSpec sp,
@@ -2272,40 +2273,35 @@ __global__ __launch_bounds__(256) void k_struct_split(const uint8_t* __restrict_
         for (int w = 0; w < 8; ++w) dg[8 * role + w][v] = dw[w];
     }
     __syncthreads();
-    if (!live || role != 0) return;
-    uint32_t raw[2 * NRAW > 0 ? 2 * NRAW : 1];
+    // the struct message (the digests, then the raw scalars) on lanes 0 and 1
+    // of the record as a lo/hi lane pair (mk::pair: lane p holds half p of
+    // every Keccak lane, so message dword 2k + p is its word k and no
+    // conversion is needed): 2 x ~12.8 k cycles of latency for the two
+    // blocks against 2 x ~21 k on one lane
+    if (!live || role > 1u) return;
+    const uint32_t p = role;
+    uint32_t raw[NRAW > 0 ? NRAW : 1];
 #pragma unroll
-    for (int k = 0; k < NRAW; ++k) {
-        const uint32_t* A32 = reinterpret_cast<const uint32_t*>(r + sp.off[NB + k]);
-        raw[2 * k] = A32[0];
-        raw[2 * k + 1] = A32[1];
-    }
+    for (int k = 0; k < NRAW; ++k) raw[k] = reinterpret_cast<const uint32_t*>(r + sp.off[NB + k])[p];
     constexpr int MW = 8 * NB + 2 * NRAW;  // message dwords
     constexpr int NBLK = 4 * MW / 136 + 1;
-    State s;
-    zero(s);
+    pair::Half s;
+    pair::zero(s);
 #pragma unroll
     for (int b = 0; b < NBLK; ++b) {
 #pragma unroll
-        for (int w = 0; w < 34; ++w) {
-            const int q = 34 * b + w;
-            uint32_t x = q < 8 * NB ? dg[q][v] : (q < MW ? raw[q - 8 * NB] : 0u);
-            if (q == MW) x ^= 1u;
-            if (b == NBLK - 1 && w == 33) x ^= 0x80000000u;
-            if (w & 1)
-                s.hi[w / 2] ^= x;
-            else
-                s.lo[w / 2] ^= x;
+        for (int k = 0; k < 17; ++k) {
+            const int q0 = 34 * b + 2 * k;  // this Keccak lane's lo dword (MW and 8 NB are even)
+            uint32_t x = q0 < 8 * NB ? dg[q0 + p][v] : (q0 < MW ? raw[(q0 - 8 * NB) / 2] : 0u);
+            if (q0 == MW && p == 0u) x ^= 1u;
+            if (b == NBLK - 1 && k == 16 && p == 1u) x ^= 0x80000000u;
+            s.v[k] ^= x;
         }
-        if (b + 1 < NBLK)
-            keccak_f(s);
-        else
-            keccak_f_digest(s);
+        pair::keccak_f(s, p != 0u);
     }
-    uint4 d0, d1;
-    digest(s, d0, d1);
-    roots[2 * i] = d0;
-    roots[2 * i + 1] = d1;
+    uint32_t* out = reinterpret_cast<uint32_t*>(roots) + 8 * i;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[2 * k + p] = s.v[k];
 }
 template __global__ void k_struct_split<3, 6>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
 template __global__ void k_struct_split<2, 0>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
