@@ -1086,6 +1086,19 @@ uint32_t next_arrive_slots(uint32_t k) {
     return (uint32_t)(start % mk::kArriveSlots);
 }
 uint32_t next_arrive_slot() { return next_arrive_slots(1); }
+// Arrival slots one fused top of `parts` workgroups uses (k_trie_top_fused,
+// k_merkle_top_fused): the final counter plus one per group of each grouping
+// stage.  Reserving only those, not kTopGroupSlots, keeps ~1,300 small fused
+// tops (C1's list tree: 16 workgroups, one slot) in flight on a device
+// before a slot comes round again, where a fixed 129 allowed 31.
+uint32_t top_arrive_slots(uint64_t parts) {
+    uint32_t k = 1;
+    while (mk::kTopGroupLog2 > 0 && parts > mk::kTopGroup) {
+        parts = ceil_div(parts, (uint64_t)mk::kTopGroup);
+        k += (uint32_t)parts;
+    }
+    return k;
+}
 
 // Levels d_from+1 .. d_to of the batch build over `n` deposits, level d_from
 // complete; the root (level depth node 0) to d_root32 when d_to == depth.
@@ -1114,7 +1127,7 @@ int trie_levels_range(void* d_levels, uint64_t cap, uint64_t n, uint32_t d_from,
             ++d;
         }
         hipLaunchKernelGGL(mk::k_trie_top_fused<NT>, dim3(ceil_div(c, NT)), dim3(NT), 0, st, (uint32_t*)d_levels, cap,
-                           c, d, depth, (uint32_t*)d_root32, next_arrive_slots(mk::kTopGroupSlots));
+                           c, d, depth, (uint32_t*)d_root32, next_arrive_slots(top_arrive_slots(ceil_div(c, NT))));
         HIPCHK(hipGetLastError());
         return MK_OK;
     }
@@ -2010,7 +2023,7 @@ static int launch_top_fused(const TopPlan& p, uint32_t nl, const void* const* no
         t.wg0 = wg;
         t.nwg = p.nwg[l];
         t.span_log2 = p.span_log2[l];
-        t.slot = next_arrive_slots(mk::kTopGroupSlots);
+        t.slot = next_arrive_slots(top_arrive_slots(t.nwg));
         wg += t.nwg;
         sub += 8 * t.nwg;
     }

@@ -150,7 +150,7 @@ struct MerkleTopList {
     uint32_t* out;       // the list root (32 B; with a pair: its slot of the pair block)
     uint32_t wg0, nwg;   // this list's workgroups
     uint32_t span_log2;  // level nodes per workgroup
-    uint32_t slot;       // first of kTopGroupSlots arrival counters (g_arrive)
+    uint32_t slot;       // first of its arrival counters (g_arrive; capi.cpp top_arrive_slots)
 };
 struct MerkleTopArgs {
     MerkleTopList l[2];
