@@ -469,9 +469,57 @@ int64_t uniform_len(const uint64_t* offs, uint64_t n) {
 }
 
 // ---- merkleHash entry bodies -------------------------------------------------------
+// The latency form of a small list's tree (round 6): merkleHash of n items
+// whose first level has 16 < windows <= 2^12 (C1's 16,384 ValidatorRecord
+// roots: 2,048 windows).  k_spread_leaf<8> hashes the windows one per wave, 8
+// per workgroup (two waves per SIMD, where the general plan's 16 put four on
+// each: 2 x ~9.8 k cycles against 2 x ~17.8 k -- a lone wave is issue-bound,
+// DESIGN §4.5), and folds each workgroup's 8 to one node 3 levels up;
+// k_merkle_top_fused takes those nodes 16 per workgroup (4 levels in the
+// spread form), groups of 16 workgroups, and the last to the root and the
+// length mix-in -- where the general plan ran one 1024-thread k_wave3 over
+// the last <= 256 nodes, whose widest levels run as lane pairs at ~14 k
+// cycles each.  C1 0.095 -> 0.085 ms (profiles/r06/c1/).
+uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
+static uint64_t list_tree_windows(uint64_t n, uint32_t item_len) {
+    if (n == 0 || item_len == 0 || n > (UINT64_MAX / 4) / item_len) return 0;
+    return ceil_div(ceil_div(n * (uint64_t)item_len, mk::chunk_bytes(item_len)), 2);
+}
+static bool list_tree_ok(uint64_t n, uint32_t item_len) {
+    const uint64_t c1 = list_tree_windows(n, item_len);
+    return c1 > 16 && c1 <= 4096;
+}
+static uint64_t list_tree_ws(uint64_t n, uint32_t item_len) {
+    if (!list_tree_ok(n, item_len)) return 0;
+    const uint64_t c4 = ceil_div(list_tree_windows(n, item_len), 8);
+    return align256(32 * c4) + align256(32 * ceil_div(c4, 16));
+}
+static int launch_top_span(const void* d_nodes, uint64_t c, uint64_t n_items, uint32_t span_log2, void* d_out32,
+                           uint8_t* d_ws, hipStream_t st);
+static int dev_list_tree(const void* d_items, uint64_t n, uint32_t item_len, void* d_out32, uint8_t* ws,
+                         hipStream_t st) {
+    if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
+    mk::ReduceArgs a{};
+    a.cb = mk::chunk_bytes(item_len);
+    a.total = n * (uint64_t)item_len;
+    a.nchunks = ceil_div(a.total, a.cb);
+    a.c1 = ceil_div(a.nchunks, 2);
+    a.items = (const uint8_t*)d_items;
+    a.out = ws;
+    a.n_items = n;
+    a.levels = 4;  // the windows + 3 levels: one node per workgroup
+    const uint32_t w8 = (((uintptr_t)d_items % 8) == 0 && a.cb % 8 == 0) ? 1u : 0u;
+    hipLaunchKernelGGL(mk::k_spread_leaf<8>, dim3(ceil_div(a.c1, 8)), dim3(1024), 0, st, a, w8);
+    HIPCHK(hipGetLastError());
+    const uint64_t c4 = ceil_div(a.c1, 8);
+    return launch_top_span(ws, c4, n, 4, d_out32, ws + align256(32 * c4), st);
+}
+
 int dev_merkle_hash(const void* d_items, uint64_t n, uint32_t item_len, void* d_out32, void* d_ws, uint64_t ws_bytes,
                     hipStream_t st) {
     if (!d_out32 || (n && item_len && !d_items)) return fail(MK_EINVAL, "null pointer");
+    if (list_tree_ok(n, item_len) && ws_bytes >= list_tree_ws(n, item_len) && (uintptr_t)d_ws % 16 == 0)
+        return dev_list_tree(d_items, n, item_len, d_out32, (uint8_t*)d_ws, st);
     Plan p;
     TRY(mk::make_plan(n, item_len, false, 0, false, ((uintptr_t)d_items % 16) == 0, p));
     return launch_plan(p, (const uint8_t*)d_items, (uint8_t*)d_out32, (uint8_t*)d_ws, ws_bytes, st);
@@ -664,10 +712,13 @@ int host_merkle_hash_plain(const uint8_t* items, uint64_t n, uint32_t item_len, 
     const size_t inb = n * (size_t)item_len;
     TRY(grow(c->in, inb));
     TRY(grow(c->out, 32));
-    TRY(grow(c->ws, p.small ? 256 : mk::plan_ws_bytes(p)));
+    TRY(grow(c->ws, std::max<uint64_t>(p.small ? 256 : mk::plan_ws_bytes(p), list_tree_ws(n, item_len))));
     hipStream_t st = c->stream;
     if (inb) HIPCHK(hipMemcpyAsync(c->in.p, items, inb, hipMemcpyHostToDevice, st));
-    TRY(launch_plan(p, (const uint8_t*)c->in.p, (uint8_t*)c->out.p, (uint8_t*)c->ws.p, c->ws.cap, st));
+    if (list_tree_ok(n, item_len))
+        TRY(dev_list_tree(c->in.p, n, item_len, c->out.p, (uint8_t*)c->ws.p, st));
+    else
+        TRY(launch_plan(p, (const uint8_t*)c->in.p, (uint8_t*)c->out.p, (uint8_t*)c->ws.p, c->ws.cap, st));
     HIPCHK(hipMemcpyAsync(out, c->out.p, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return MK_OK;
@@ -894,7 +945,6 @@ int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp,
     return MK_OK;
 }
 
-uint64_t align256(uint64_t x) { return (x + 255) & ~255ull; }
 // host-buffer entries: H2D in up to kH2dChunks pieces of at least kH2dMinChunk records
 #define MK_H2D_CHUNKS 8
 // (smaller floors measured slower: C1's 16,384 records 0.212 ms in one piece,
@@ -952,23 +1002,11 @@ int dev_struct_list_root_win(const void* d_rec, uint64_t n, void* d_roots, void*
     return dev_finish_nodes(d_wins, c1, n, d_out32, d_ws, ws_bytes, st);
 }
 
-// The latency form of a small list's tree (dev_list_tree_32): merkleHash of
-// n 32-B items whose first level has 16 < windows <= 2^12.
-static uint64_t latency_windows(uint64_t n) { return ceil_div(ceil_div(32 * n, 128), 2); }
-static bool latency_tree_ok(uint64_t n, const void* d_items) {
-    const uint64_t c1 = latency_windows(n);
-    return c1 > 16 && c1 <= 4096 && (uintptr_t)d_items % 16 == 0;
-}
-static uint64_t latency_tree_ws(uint64_t n) {
-    const uint64_t c4 = ceil_div(latency_windows(n), 8);
-    return align256(32 * c4) + align256(32 * ceil_div(c4, 16));
-}
-
 uint64_t struct_list_ws(uint64_t n, const mk::StructSpec& sp) {
     Plan p;
     uint64_t mws = 256;
     if (mk::make_plan(n, 32, false, 0, false, true, p) == MK_OK && !p.small) mws = mk::plan_ws_bytes(p);
-    if (latency_windows(n) > 16 && latency_windows(n) <= 4096) mws = std::max(mws, latency_tree_ws(n));
+    mws = std::max(mws, list_tree_ws(n, 32));
     return align256(n * sp.msg_len) + align256(32 * n) + mws;
 }
 
@@ -1764,7 +1802,7 @@ uint64_t mk_ssz_merkle_workspace_bytes(uint64_t n, uint32_t item_len) {
     Scope S(nullptr, false);
     Plan p;
     if (mk::make_plan(n, item_len, false, 0, false, true, p) != MK_OK) return 0;
-    return p.small ? 256 : mk::plan_ws_bytes(p);
+    return std::max<uint64_t>(p.small ? 256 : mk::plan_ws_bytes(p), list_tree_ws(n, item_len));
 }
 
 int mk_dev_ssz_merkle_hash(mk_call* call, const void* d_items, uint64_t n, uint32_t item_len, void* d_out32,
@@ -2032,44 +2070,21 @@ static int launch_top_fused(const TopPlan& p, uint32_t nl, const void* const* no
     return MK_OK;
 }
 
-// merkleHash of n 32-B items (a list's element roots, hash.go:118-139 ->
-// 194-239).  Small lists (16 < windows <= 2^12, C1's 16,384 ValidatorRecord
-// roots: 2,048 windows) in the latency form: k_spread_leaf<8> hashes the
-// windows one per wave, 8 per workgroup (two waves per SIMD, where 16 put
-// four on each: 2 x ~9.8 k cycles against 2 x ~17.8 k), and folds each
-// workgroup's 8 to one node 3 levels up; k_merkle_top_fused takes those nodes
-// 16 per workgroup (4 levels in the spread form), groups of 16 workgroups,
-// and the last to the root and the length mix-in -- where the general plan
-// ran 16 windows per workgroup and one 1024-thread k_wave3 over the last 128
-// nodes, whose widest levels run as lane pairs (~14 k cycles each).
-// Everything else: the general plan (dev_merkle_hash).
-static int dev_list_tree_32(const void* d_items, uint64_t n, void* d_out32, uint8_t* ws, uint64_t ws_bytes,
-                            hipStream_t st) {
-    if (!latency_tree_ok(n, d_items) || ws_bytes < latency_tree_ws(n) || (uintptr_t)ws % 16)
-        return dev_merkle_hash(d_items, n, 32, d_out32, ws, ws_bytes, st);
-    if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
-    const uint64_t total = 32 * n, nchunks = ceil_div(total, 128), c1 = ceil_div(nchunks, 2);
-    mk::ReduceArgs a{};
-    a.items = (const uint8_t*)d_items;
-    a.total = total;
-    a.cb = 128;
-    a.nchunks = nchunks;
-    a.c1 = c1;
-    a.c1_full = total / 256;
-    a.out = ws;
-    a.n_items = n;
-    a.levels = 4;  // the windows + 3 levels: one node per workgroup
-    hipLaunchKernelGGL(mk::k_spread_leaf<8>, dim3(ceil_div(c1, 8)), dim3(1024), 0, st, a, 1u);
-    HIPCHK(hipGetLastError());
-    const uint64_t c4 = ceil_div(c1, 8);
+// k_merkle_top_fused over one list's complete level of c nodes in spans of
+// 2^span_log2 nodes per workgroup, to the root with the length mix-in
+// (dev_list_tree, declared in the anonymous namespace above)
+namespace {
+static int launch_top_span(const void* d_nodes, uint64_t c, uint64_t n_items, uint32_t span_log2, void* d_out32,
+                           uint8_t* d_ws, hipStream_t st) {
     TopPlan p;
-    p.span_log2[0] = 4;
-    p.nwg[0] = (uint32_t)ceil_div(c4, 16);
+    p.span_log2[0] = span_log2;
+    p.nwg[0] = (uint32_t)ceil_div(c, 1ull << span_log2);
     p.ws = align256(32 * (uint64_t)p.nwg[0]);
-    const void* nodes[1] = {ws};
-    const uint64_t c[1] = {c4}, nit[1] = {n};
-    return launch_top_fused(p, 1, nodes, c, nit, d_out32, 0, ws + align256(32 * c4), st);
+    const void* nodes[1] = {d_nodes};
+    const uint64_t cc[1] = {c}, nit[1] = {n_items};
+    return launch_top_fused(p, 1, nodes, cc, nit, d_out32, 0, d_ws, st);
 }
+}  // namespace
 
 int mk_dev_ssz_merkle_finish_nodes_pair(mk_call* call, const void* d_nodes, uint64_t count, uint64_t n_total,
                                         void* d_pair_block, uint32_t slot, uint32_t epoch, void* d_ws,
@@ -2140,7 +2155,7 @@ int mk_dev_ssz_struct_list_root(mk_call* call, const void* d_records, uint64_t n
                                                ws_bytes - (uint64_t)(mws - ws), st));
     rc = launch_struct_roots(d_records, n, sp, msg, roots, st);
     if (rc) return S.done(rc);
-    return S.done(dev_list_tree_32(roots, n, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), st));
+    return S.done(dev_merkle_hash(roots, n, 32, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), st));
 }
 
 int mk_ssz_struct_list_level1_ok(const void* d_records, uint64_t n, uint32_t record_len, const mk_field* fields,
@@ -2388,7 +2403,7 @@ static int host_struct_list_root(const uint8_t* records, uint64_t n, uint32_t re
         HIPCHK(hipStreamWaitEvent(st, c->h2d, 0));
         TRY(launch_struct_roots(din + off * record_len, cnt, sp, msg + off * sp.msg_len, roots + 32 * off, st));
     }
-    TRY(dev_list_tree_32(roots, n, c->out.p, mws, wsb - (uint64_t)(mws - ws), st));
+    TRY(dev_merkle_hash(roots, n, 32, c->out.p, mws, wsb - (uint64_t)(mws - ws), st));
     HIPCHK(hipMemcpyAsync(out, c->out.p, 32, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     return MK_OK;

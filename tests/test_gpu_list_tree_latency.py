@@ -44,3 +44,37 @@ def test_dev_struct_list_root_latency_form(gpu, n):
         torch.cuda.synchronize()
         assert bytes(got.cpu().numpy()) == want
     assert reg.tree_hash_ssz() == want  # the host-records entry, same plan
+
+
+# item sizes that pack 32 / 16 / 8 / 4 items per 128-B chunk, one item per
+# chunk (48, 128, 200 B) and odd sizes (7, 24: a chunk of whole items short
+# of 128 B); n at the form's first (17) and last (4,096) window counts, one
+# either side of them, and ragged in between
+_ITEM_CASES = [(8, 16 * 32 + 15), (8, 16 * 33), (8, 16 * 33 + 1), (8, 16 * 8192), (8, 16 * 8192 + 1), (16, 300),
+               (32, 4097), (32, 8 * 4096 + 1), (4, 2000), (48, 35), (48, 8191), (128, 4000), (200, 33), (200, 999),
+               (24, 5000), (7, 3333)]
+
+
+@pytest.mark.parametrize("item_len,n", _ITEM_CASES)
+def test_dev_merkle_hash_latency_form(gpu, item_len, n):
+    """mk_dev_ssz_merkle_hash and the host entry through the latency form
+    (and just outside it) against the oracle's merkleHash restatement."""
+    import torch
+
+    from oracle import oracle as O
+    from prysm_amd import device as D
+    from prysm_amd import ssz
+
+    raw = O.splitmix_bytes(n * item_len, SEED + 7 * item_len + n)
+    want = O.merkle_hash_flat(raw, n, item_len, nthreads=16)
+    dev = torch.from_numpy(raw.copy()).to("cuda:0")
+    for _ in range(2):
+        got = D.merkle_hash(dev, n, item_len)
+        torch.cuda.synchronize()
+        assert bytes(got.cpu().numpy()) == want
+    assert ssz.merkle_hash_flat(raw, n, item_len) == want
+    if n > 1:  # unaligned start: the byte-wise sponge
+        dev2 = torch.from_numpy(np.concatenate([np.zeros(3, np.uint8), raw])).to("cuda:0")[3:]
+        got = D.merkle_hash(dev2, n, item_len)
+        torch.cuda.synchronize()
+        assert bytes(got.cpu().numpy()) == want
