@@ -2458,18 +2458,12 @@ template __global__ void k_keccak_rec<35>(const uint2*, uint64_t, uint4*);
 // and 0.4163 -> 0.4092 ms/step (4/10/16 against all after 12), one trie
 // 0.543 -> 0.515 and 0.561 -> 0.534 ms; two parts -1.1 %, one unit per round
 // or two -0.4 to -1.1 %.
-#ifndef MK_TRIE_DMA_SPLIT
 #define MK_TRIE_DMA_SPLIT 4
-#endif
-#ifndef MK_TRIE_DMA_SPLIT3
 #define MK_TRIE_DMA_SPLIT3 10
-#endif
 // round of a block's permutation after which the next block's DMA (its last
 // part) goes out; as one part: 12 (mid-permutation) over 0, one trie 1.2-2.3
 // % faster on two boxes (profiles/r04/trie_dma_ab/); in three parts: 16
-#ifndef MK_TRIE_DMA_ROUND
 #define MK_TRIE_DMA_ROUND 16
-#endif
 
 // PIPE (a stream of tries, pipeline.TriePipeline): workgroup b also takes the
 // previous trie's subtree over its level-2 nodes [1024 b, 1024 b + 1024) up

@@ -133,9 +133,7 @@ constexpr uint32_t kArriveSlots = 4096;
 // nodes before the last group finishes the top
 // nodes before the next stage / the last group finishes the top (0: the last
 // workgroup alone reduces all the grid's nodes)
-#ifndef MK_TOP_GROUP_LOG2
 #define MK_TOP_GROUP_LOG2 4
-#endif
 constexpr uint32_t kTopGroupLog2 = MK_TOP_GROUP_LOG2, kTopGroup = 1u << kTopGroupLog2;
 constexpr uint32_t kTopGroupSlots = kTopGroupLog2 ? 1 + 2 * 1024 / kTopGroup : 1;  // arrival slots of one launch
 template <uint32_t NT>
