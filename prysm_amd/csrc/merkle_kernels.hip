@@ -2694,10 +2694,18 @@ template __global__ void k_trie_rec_lock<1024, 4, true>(const uint2*, uint64_t, 
 // level-2 nodes (lane m: level-1 nodes 2m, 2m + 1) -- 15 locked permutations
 // per thread, as in the row form; levels 0-2 are stored as consecutive
 // nodes per wave.
+#if MK_TOP_STAMPS
+// diagnostic build only (tools/top_probe.hip): s_memrealtime at the start and
+// the end of each workgroup of the slot-major front
+__device__ uint64_t g_front_stamps[2 * 1024];
+#endif
 template <uint32_t NT>
 __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock_sm(const uint2* __restrict__ in, uint64_t ngroups,
                                                             uint4* __restrict__ L0, uint4* __restrict__ L1,
                                                             uint4* __restrict__ L2) {
+#if MK_TOP_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_front_stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
     constexpr uint32_t NW = 35;  // 8-B words per deposit
     __shared__ uint4 buf[NT / 64][9 * 64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -2873,6 +2881,10 @@ __global__ __launch_bounds__(NT, 1) void k_trie_rec_lock_sm(const uint2* __restr
         }
     }
     flush();
+#if MK_TOP_STAMPS
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_front_stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 template __global__ void k_trie_rec_lock_sm<1024>(const uint2*, uint64_t, uint4*, uint4*, uint4*);
 

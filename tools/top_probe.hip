@@ -74,7 +74,48 @@ static int merkle_probe(int iters) {
     return 0;
 }
 
+// The whole-trie front (k_trie_rec_lock_sm) over 2^20 random 280-B
+// deposits, `iters` times: per workgroup its start and end on the 100-MHz
+// s_memrealtime clock (g_front_stamps), to see how far apart the workgroups
+// finish -- the time a top fused into the front could start early.
+static int front_probe(int iters) {
+    const uint64_t n = 1u << 20;
+    uint2* in;
+    uint4 *l0, *l1, *l2;
+    (void)hipMalloc(&in, n * 280);
+    (void)hipMalloc(&l0, n * 32);
+    (void)hipMalloc(&l1, n * 16);
+    (void)hipMalloc(&l2, n * 8);
+    (void)hipMemset(in, 0x3C, n * 280);
+    const uint64_t ngroups = n / 4096;
+    std::vector<uint64_t> st(2 * 1024);
+    for (int it = 0; it < iters; ++it) {
+        hipLaunchKernelGGL(mk::k_trie_rec_lock_sm<1024>, dim3((uint32_t)ngroups), dim3(1024), 0, 0, in, ngroups, l0,
+                           l1, l2);
+        (void)hipDeviceSynchronize();
+    }
+    (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(mk::g_front_stamps), st.size() * 8);
+    std::vector<uint64_t> s0, s1, dur;
+    for (uint64_t b = 0; b < ngroups; ++b) {
+        s0.push_back(st[2 * b]);
+        s1.push_back(st[2 * b + 1]);
+        dur.push_back(st[2 * b + 1] - st[2 * b]);
+    }
+    const uint64_t t0 = *std::min_element(s0.begin(), s0.end());
+    std::sort(s0.begin(), s0.end());
+    std::sort(s1.begin(), s1.end());
+    std::sort(dur.begin(), dur.end());
+    auto us = [](uint64_t t) { return t / 100.0; };  // 100-MHz ticks -> us
+    printf("{\"front_wgs\": %llu, \"start_us\": [%.2f, %.2f, %.2f], \"end_us\": [%.2f, %.2f, %.2f, %.2f], "
+           "\"dur_us\": [%.2f, %.2f, %.2f]}\n",
+           (unsigned long long)ngroups, us(s0.front() - t0), us(s0[s0.size() / 2] - t0), us(s0.back() - t0),
+           us(s1.front() - t0), us(s1[s1.size() / 10] - t0), us(s1[s1.size() / 2] - t0), us(s1.back() - t0),
+           us(dur.front()), us(dur[dur.size() / 2]), us(dur.back()));
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 2 && argv[2][0] == 'f') return front_probe(atoi(argv[1]));
     if (argc > 2) return merkle_probe(atoi(argv[1]));
     const uint64_t n = 1u << 20, cap = n;
     const uint32_t depth = 32, d0 = 2;
