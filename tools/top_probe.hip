@@ -111,6 +111,20 @@ static int front_probe(int iters) {
            (unsigned long long)ngroups, us(s0.front() - t0), us(s0[s0.size() / 2] - t0), us(s0.back() - t0),
            us(s1.front() - t0), us(s1[s1.size() / 10] - t0), us(s1[s1.size() / 2] - t0), us(s1.back() - t0),
            us(dur.front()), us(dur[dur.size() / 2]), us(dur.back()));
+    // mean end (us after the first start) per XCD (workgroup b on XCD b mod 8)
+    printf("{\"end_us_by_xcd\": [");
+    for (int x = 0; x < 8; ++x) {
+        double sum = 0;
+        int k = 0;
+        for (uint64_t b = x; b < ngroups; b += 8, ++k) sum += us(st[2 * b + 1] - t0);
+        printf("%s%.2f", x ? ", " : "", sum / k);
+    }
+    printf("], \"slowest_wgs\": [");
+    std::vector<std::pair<uint64_t, uint64_t>> e;
+    for (uint64_t b = 0; b < ngroups; ++b) e.push_back({st[2 * b + 1], b});
+    std::sort(e.begin(), e.end());
+    for (int k = 0; k < 16; ++k) printf("%s%llu", k ? ", " : "", (unsigned long long)e[e.size() - 1 - k].second);
+    printf("]}\n");
     return 0;
 }
 
