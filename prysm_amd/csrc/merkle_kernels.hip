@@ -588,7 +588,15 @@ __device__ __forceinline__ void hash_window_sc(uint4* Bw, uint32_t lane, const u
     digest(s, d0, d1);
 }
 
+#if MK_TOP_STAMPS
+// diagnostic build only (tools/top_probe.hip): s_memrealtime at the start and
+// the end of each workgroup of the leaf pass
+__device__ uint64_t g_leaf_stamps[2 * 1024];
+#endif
 __global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock_sc(ReduceArgs a, uint64_t ngroups) {
+#if MK_TOP_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_leaf_stamps[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
     __shared__ uint4 buf[kLockThreads / 64][(MK_LOCK_NT ? 10 : 9) * 64];
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
     uint4* Bw = buf[wave];
@@ -625,6 +633,10 @@ __global__ __launch_bounds__(kLockThreads, 1) void k_leaf_lock_sc(ReduceArgs a, 
         pend = true;
     }
     flush();
+#if MK_TOP_STAMPS
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_leaf_stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 template __global__ void k_reduce<true, true, 2>(ReduceArgs);

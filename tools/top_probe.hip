@@ -128,7 +128,50 @@ static int front_probe(int iters) {
     return 0;
 }
 
+// The C4 leaf pass (k_leaf_lock_sc) over 2^28 32-B items, one workgroup per
+// CU (256, 32 groups of 4,096 windows each, statically strided): per
+// workgroup its end on the 100-MHz clock, per XCD the mean, to see whether a
+// slow XCD leaves a tail behind a static group assignment.
+static int leaf_probe(int iters) {
+    const uint64_t n = 1ull << 28, windows = n * 32 / 256, ngroups = windows / 4096;
+    uint8_t* items;
+    uint8_t* out;
+    if (hipMalloc(&items, n * 32) != hipSuccess || hipMalloc(&out, ngroups * 1024 * 32) != hipSuccess) return 1;
+    (void)hipMemset(items, 0x5A, n * 32);
+    mk::ReduceArgs a{};
+    a.items = items;
+    a.out = out;
+    const uint32_t grid = 256;
+    std::vector<uint64_t> st(2 * 1024);
+    for (int it = 0; it < iters; ++it) {
+        hipLaunchKernelGGL(mk::k_leaf_lock_sc, dim3(grid), dim3(1024), 0, 0, a, ngroups);
+        (void)hipDeviceSynchronize();
+        (void)hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(mk::g_leaf_stamps), st.size() * 8);
+        uint64_t t0 = ~0ull, e0 = ~0ull, e1 = 0;
+        for (uint32_t b = 0; b < grid; ++b) {
+            t0 = std::min(t0, st[2 * b]);
+            e0 = std::min(e0, st[2 * b + 1]);
+            e1 = std::max(e1, st[2 * b + 1]);
+        }
+        printf("{\"leaf_wgs\": %u, \"groups\": %llu, \"first_end_us\": %.1f, \"last_end_us\": %.1f, \"end_us_by_xcd\": [",
+               grid, (unsigned long long)ngroups, (e0 - t0) / 100.0, (e1 - t0) / 100.0);
+        for (int x = 0; x < 8; ++x) {
+            double sum = 0, mx = 0;
+            int k = 0;
+            for (uint32_t b = x; b < grid; b += 8, ++k) {
+                sum += (st[2 * b + 1] - t0) / 100.0;
+                mx = std::max(mx, (st[2 * b + 1] - t0) / 100.0);
+            }
+            printf("%s[%.1f, %.1f]", x ? ", " : "", sum / k, mx);
+        }
+        printf("]}\n");
+        fflush(stdout);
+    }
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 2 && argv[2][0] == 'l') return leaf_probe(atoi(argv[1]));
     if (argc > 2 && argv[2][0] == 'f') return front_probe(atoi(argv[1]));
     if (argc > 2) return merkle_probe(atoi(argv[1]));
     const uint64_t n = 1u << 20, cap = n;
