@@ -860,32 +860,43 @@ bool validator_layout(const mk::StructSpec& sp) {
     return true;
 }
 
-// roots of n records into d_roots (n x 32); d_msg holds n x msg_len bytes
-int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp, void* d_msg, void* d_roots,
-                        hipStream_t st) {
-    if (n == 0) return MK_OK;
+// The struct kernels' selectors for n records of layout sp at d_rec
+struct StructForm {
+    bool fused, vec16, layout, split;
+    uint32_t nb, nraw;
+};
+static StructForm struct_form(const void* d_rec, uint64_t n, const mk::StructSpec& sp) {
+    StructForm f{};
     // fused path: dword-granular single-block fields, dword-aligned message
-    bool fused = sp.msg_len % 4 == 0 && sp.msg_len <= mk::kStructFusedMaxMsg &&
-                 ((uintptr_t)d_rec % 4) == 0;
-    bool vec16 = ((uintptr_t)d_rec % 16) == 0 && sp.rec_len % 16 == 0;
-    for (uint32_t f = 0; f < sp.nfields; ++f) {
-        if (sp.out_off[f] % 4) fused = false;
-        if (sp.kind[f] == MK_FIELD_BYTES) {
-            if ((sp.len[f] % 4) != 0 || sp.len[f] > mk::kStructFusedMaxField) fused = false;
-            if (sp.off[f] % 16 || sp.off[f] + ((sp.len[f] + 15) & ~15u) > sp.rec_len) vec16 = false;
-        } else if (sp.len[f] % 4 || sp.off[f] % 4) {
-            fused = false;
+    f.fused = sp.msg_len % 4 == 0 && sp.msg_len <= mk::kStructFusedMaxMsg && ((uintptr_t)d_rec % 4) == 0;
+    f.vec16 = ((uintptr_t)d_rec % 16) == 0 && sp.rec_len % 16 == 0;
+    for (uint32_t k = 0; k < sp.nfields; ++k) {
+        if (sp.out_off[k] % 4) f.fused = false;
+        if (sp.kind[k] == MK_FIELD_BYTES) {
+            if ((sp.len[k] % 4) != 0 || sp.len[k] > mk::kStructFusedMaxField) f.fused = false;
+            if (sp.off[k] % 16 || sp.off[k] + ((sp.len[k] + 15) & ~15u) > sp.rec_len) f.vec16 = false;
+        } else if (sp.len[k] % 4 || sp.off[k] % 4) {
+            f.fused = false;
         }
     }
     // compile-time message layout: NB dword-granular bytes fields (<= 64 B)
     // first, then NRAW 8-byte scalars, at 4-byte aligned record offsets
-    uint32_t nb = 0;
-    while (nb < sp.nfields && sp.kind[nb] == MK_FIELD_BYTES) ++nb;
-    bool layout = fused && nb > 0;
-    for (uint32_t f = nb; f < sp.nfields; ++f)
-        if (sp.kind[f] != MK_FIELD_RAW || sp.len[f] != 8) layout = false;
-    const uint32_t nraw = sp.nfields - nb;
-    const bool split = n <= mk::kStructSplitMaxN;  // latency-bound: 4 lanes per record
+    while (f.nb < sp.nfields && sp.kind[f.nb] == MK_FIELD_BYTES) ++f.nb;
+    f.layout = f.fused && f.nb > 0;
+    for (uint32_t k = f.nb; k < sp.nfields; ++k)
+        if (sp.kind[k] != MK_FIELD_RAW || sp.len[k] != 8) f.layout = false;
+    f.nraw = sp.nfields - f.nb;
+    f.split = n <= mk::kStructSplitMaxN;  // latency-bound: 4 lanes per record
+    return f;
+}
+
+// roots of n records into d_roots (n x 32); d_msg holds n x msg_len bytes
+int launch_struct_roots(const void* d_rec, uint64_t n, const mk::StructSpec& sp, void* d_msg, void* d_roots,
+                        hipStream_t st) {
+    if (n == 0) return MK_OK;
+    const StructForm sf = struct_form(d_rec, n, sp);
+    const bool fused = sf.fused, vec16 = sf.vec16, layout = sf.layout, split = sf.split;
+    const uint32_t nb = sf.nb, nraw = sf.nraw;
     if (layout && split && nb == 3 && nraw == 6) {
         hipLaunchKernelGGL((mk::k_struct_split<3, 6>), dim3(ceil_div(n, 64)), dim3(256), 0, st, (const uint8_t*)d_rec,
                            n, sp, vec16 ? 1u : 0u, (uint4*)d_roots);
@@ -1000,6 +1011,36 @@ int dev_struct_list_root_win(const void* d_rec, uint64_t n, void* d_roots, void*
     const uint64_t c1 = ceil_div(n, 8);  // windows: ceil(ceil(n / 4) / 2) chunk pairs
     if (ws_bytes < finish_ws_bytes(c1)) return fail(MK_ENOMEM, "workspace too small for the registry top");
     return dev_finish_nodes(d_wins, c1, n, d_out32, d_ws, ws_bytes, st);
+}
+
+// A small list of ValidatorRecord-shaped structs (3 bytes fields, 6 8-byte
+// scalars: C1) in ONE launch, k_struct_list_fused<3, 6>: the k_struct_split
+// records, the latency list tree's windows and levels, and the fused top's
+// groups and mix-in, where they were three launches (round 6)
+uint32_t next_arrive_slots(uint32_t k);
+uint32_t top_arrive_slots(uint64_t parts);
+static bool struct_list_fused_ok(const void* d_rec, uint64_t n, const mk::StructSpec& sp) {
+    const StructForm f = struct_form(d_rec, n, sp);
+    return n && f.layout && f.split && f.nb == 3 && f.nraw == 6 && list_tree_ok(n, 32);
+}
+static int launch_struct_list_fused(const void* d_rec, uint64_t n, const mk::StructSpec& sp, uint8_t* d_roots,
+                                    uint8_t* d_sub, void* d_out32, hipStream_t st) {
+    if (inject_ehip()) return fail(MK_EHIP, "hipLaunchKernelGGL: injected failure (MK_INJECT_EHIP)");
+    const StructForm f = struct_form(d_rec, n, sp);
+    mk::ReduceArgs a{};  // the window pass over the roots, as dev_list_tree's
+    a.cb = 128;
+    a.total = 32 * n;
+    a.nchunks = ceil_div(a.total, a.cb);
+    a.c1 = ceil_div(a.nchunks, 2);
+    a.items = d_roots;
+    a.n_items = n;
+    a.levels = 4;
+    const uint64_t nwg = ceil_div(n, 64);  // = the level-4 nodes, ceil(c1 / 8)
+    hipLaunchKernelGGL((mk::k_struct_list_fused<3, 6>), dim3((uint32_t)nwg), dim3(1024), 0, st, (const uint8_t*)d_rec,
+                       n, sp, f.vec16 ? 1u : 0u, (uint4*)d_roots, a, (uint32_t*)d_sub, (uint32_t*)d_out32,
+                       next_arrive_slots(top_arrive_slots(nwg)));
+    HIPCHK(hipGetLastError());
+    return MK_OK;
 }
 
 uint64_t struct_list_ws(uint64_t n, const mk::StructSpec& sp) {
@@ -2153,6 +2194,8 @@ int mk_dev_ssz_struct_list_root(mk_call* call, const void* d_records, uint64_t n
     if (struct_win_ok(d_records, n, sp))  // the windows go where the two-launch path keeps its messages
         return S.done(dev_struct_list_root_win(d_records, n, roots, msg, d_out32, mws,
                                                ws_bytes - (uint64_t)(mws - ws), st));
+    if (struct_list_fused_ok(d_records, n, sp) && ws_bytes - (uint64_t)(mws - ws) >= list_tree_ws(n, 32))
+        return S.done(launch_struct_list_fused(d_records, n, sp, roots, mws, d_out32, st));
     rc = launch_struct_roots(d_records, n, sp, msg, roots, st);
     if (rc) return S.done(rc);
     return S.done(dev_merkle_hash(roots, n, 32, d_out32, mws, ws_bytes - (uint64_t)(mws - ws), st));
@@ -2395,6 +2438,16 @@ static int host_struct_list_root(const uint8_t* records, uint64_t n, uint32_t re
     const uint8_t* din = (const uint8_t*)c->in.p;
     uint64_t chunk = std::max<uint64_t>(kH2dMinChunk, ceil_div(n, kH2dChunks));
     chunk = (chunk + 15) & ~15ull;  // chunk starts keep the records' 16-B alignment
+    if (n <= chunk && struct_list_fused_ok(din, n, sp) && wsb - (uint64_t)(mws - ws) >= list_tree_ws(n, 32)) {
+        // one piece: the records cross PCIe, then the whole list in one launch
+        HIPCHK(hipMemcpyAsync((uint8_t*)c->in.p, records, n * (size_t)record_len, hipMemcpyHostToDevice, c->copy));
+        HIPCHK(hipEventRecord(c->h2d, c->copy));
+        HIPCHK(hipStreamWaitEvent(st, c->h2d, 0));
+        TRY(launch_struct_list_fused(din, n, sp, roots, mws, c->out.p, st));
+        HIPCHK(hipMemcpyAsync(out, c->out.p, 32, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return MK_OK;
+    }
     for (uint64_t off = 0; off < n; off += chunk) {
         const uint64_t cnt = std::min(chunk, n - off);
         HIPCHK(hipMemcpyAsync((uint8_t*)c->in.p + off * record_len, records + off * record_len,

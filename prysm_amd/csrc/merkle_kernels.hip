@@ -2249,15 +2249,18 @@ template __global__ void k_struct_reg<2, 0>(const uint8_t*, uint64_t, StructSpec
 // C1's struct roots 29.6 -> see DESIGN §4.5): 3 serial permutations per
 // record instead of 5, the last two at lane-pair latency.  The host takes this form while 4 lanes per record still fit
 // the chip once (n <= kStructSplitMaxN).
+// The body, for the first 256 threads of the calling workgroup (every
+// thread of it must call: the digests meet in LDS behind a barrier):
+// records [64 blk, 64 blk + 64), roots to roots[].
 template <int NB, int NRAW>
-__global__ __launch_bounds__(256) void k_struct_split(const uint8_t* __restrict__ rec, uint64_t n, StructSpec sp,
-                                                      uint32_t vec16, uint4* __restrict__ roots) {
+__device__ __forceinline__ void struct_split_body(const uint8_t* __restrict__ rec, uint64_t n, const StructSpec& sp,
+                                                  uint32_t vec16, uint4* __restrict__ roots, uint64_t blk,
+                                                  uint32_t (&dg)[NB * 8][64]) {
     static_assert(NB <= 4, "one lane per bytes field");
     constexpr uint32_t kV = 256 / 4;  // records per workgroup
-    __shared__ uint32_t dg[NB * 8][kV];
-    const uint32_t tid = threadIdx.x, v = tid >> 2, role = tid & 3u;
-    const uint64_t i = (uint64_t)blockIdx.x * kV + v;
-    const bool live = i < n;
+    const uint32_t tid = threadIdx.x, v = (tid >> 2) & (kV - 1), role = tid & 3u;
+    const uint64_t i = blk * kV + v;
+    const bool live = tid < 256u && i < n;
     const uint8_t* r = rec + (live ? i : 0) * sp.rec_len;
     if (live && role < (uint32_t)NB) {  // Keccak(le32(len) || bytes), one block
         const uint32_t off = role == 0 ? sp.off[0] : role == 1 ? sp.off[1 % NB] : sp.off[2 % NB];
@@ -2314,6 +2317,13 @@ __global__ __launch_bounds__(256) void k_struct_split(const uint8_t* __restrict_
     uint32_t* out = reinterpret_cast<uint32_t*>(roots) + 8 * i;
 #pragma unroll
     for (int k = 0; k < 4; ++k) out[2 * k + p] = s.v[k];
+}
+
+template <int NB, int NRAW>
+__global__ __launch_bounds__(256) void k_struct_split(const uint8_t* __restrict__ rec, uint64_t n, StructSpec sp,
+                                                      uint32_t vec16, uint4* __restrict__ roots) {
+    __shared__ uint32_t dg[NB * 8][64];
+    struct_split_body<NB, NRAW>(rec, n, sp, vec16, roots, blockIdx.x, dg);
 }
 template __global__ void k_struct_split<3, 6>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
 template __global__ void k_struct_split<2, 0>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*);
@@ -3703,14 +3713,16 @@ template __global__ void k_merkle_top_fused<1024>(MerkleTopArgs);
 // windows) continues to the root and the length mix-in.  Where a tree's
 // first level has few windows every wave runs nearly alone, and a window
 // costs 2 x 6.3 k cycles here against 2 x 12.8 k in a lane pair.
-template <uint32_t SPAN>
-__global__ __launch_bounds__(1024) void k_spread_leaf(ReduceArgs a, uint32_t w8) {
+// The body (every thread of the workgroup calls it): windows [SPAN blk,
+// SPAN blk + SPAN); with STORE the pass's nodes go to a.out, else the
+// workgroup's node (a.levels = 1 + log2 SPAN) is left in nodes[0..3].
+template <uint32_t SPAN, bool STORE>
+__device__ __forceinline__ void spread_leaf_body(const ReduceArgs& a, uint32_t w8, uint64_t blk, uint2 (&nodes)[64]) {
     static_assert(SPAN == 8 || SPAN == 16, "windows per workgroup");
-    __shared__ uint2 nodes[16 * 4];
     const uint32_t w = threadIdx.x >> 6, L = threadIdx.x & 63u;
     const spread::LaneLH cst = spread::lane_consts_lh(L);
     const uint32_t i = cst.i;
-    const uint64_t lo1 = (a.wg_base + blockIdx.x) * (uint64_t)SPAN;
+    const uint64_t lo1 = (a.wg_base + blk) * (uint64_t)SPAN;
     const uint64_t m1 = a.c1 - lo1 < SPAN ? a.c1 - lo1 : SPAN;
     if (w < m1) {  // wave-uniform
         const uint64_t j = lo1 + w;
@@ -3784,12 +3796,104 @@ __global__ __launch_bounds__(1024) void k_spread_leaf(ReduceArgs a, uint32_t w8)
             spread::keccak_f_lh(slo, shi, cst);
             if (L < 4u) out[L] = make_uint2(slo, shi);
         }
-    } else if (w < m && L < 4u) {
+    } else if (STORE && w < m && L < 4u) {
         out[4 * ((lo1 >> done) + w) + L] = nodes[4 * w + L];
     }
 }
+template <uint32_t SPAN>
+__global__ __launch_bounds__(1024) void k_spread_leaf(ReduceArgs a, uint32_t w8) {
+    __shared__ uint2 nodes[16 * 4];
+    spread_leaf_body<SPAN, true>(a, w8, blockIdx.x, nodes);
+}
 template __global__ void k_spread_leaf<16>(ReduceArgs, uint32_t);
 template __global__ void k_spread_leaf<8>(ReduceArgs, uint32_t);
+
+// TreeHash of a small list of structs in ONE launch (round 6: C1, 16,384
+// ValidatorRecords, hash.go:118-159 -> 194-239): workgroup b hashes records
+// [64 b, 64 b + 64) as k_struct_split does (the fields side by side, the
+// struct message on a lane pair; roots to `roots`), then their 8 windows
+// and 3 levels as k_spread_leaf<8> does (one window per wave), publishes
+// its node (write-through, drained) and arrives; groups of kTopGroup
+// workgroups and the last one take the nodes to the list root and the
+// length mix-in as k_merkle_top_fused does.  Three launches' boundaries
+// and the roots' trip through a second kernel go away.  `a` is the window
+// pass over `roots` (a.levels = 4); sub: one published node per workgroup.
+template <int NB, int NRAW>
+__global__ __launch_bounds__(1024) void k_struct_list_fused(const uint8_t* __restrict__ rec, uint64_t n, StructSpec sp,
+                                                            uint32_t vec16, uint4* __restrict__ roots, ReduceArgs a,
+                                                            uint32_t* __restrict__ sub, uint32_t* __restrict__ out,
+                                                            uint32_t slot) {
+    __shared__ uint32_t dg[NB * 8][64];
+    __shared__ uint2 nodes[16 * 4];
+    __shared__ uint32_t lds[8 * 1024];
+    __shared__ uint32_t flag;
+    constexpr uint32_t NT = 1024;
+    const uint32_t b = blockIdx.x, nwg = gridDim.x;
+    struct_split_body<NB, NRAW>(rec, n, sp, vec16, roots, b, dg);
+    __threadfence_block();  // this workgroup's roots, read back by its own waves below
+    __syncthreads();
+    spread_leaf_body<8, false>(a, 1u, b, nodes);
+    // publish node b: plain (lo, hi) words of lanes 0..3, write-through, drained
+    if (threadIdx.x < 4u) {
+        const uint2 v = nodes[threadIdx.x];
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(sub) + 4 * b + threadIdx.x,
+                           (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const spread::Lane cst = spread::lane_consts(threadIdx.x & 63u);
+    auto none3 = [](uint32_t, const uint4&, const uint4&) {};
+    auto none_p = [](uint32_t, const uint32_t(&)[4], uint32_t) {};
+    auto none_w = [](uint32_t, uint32_t, uint32_t, uint32_t) {};
+    uint32_t m = 1;
+    // as k_merkle_top_fused: groups of kTopGroup parts first, each group's
+    // last arriver takes its nodes log2(kTopGroup) levels up (a ragged last
+    // group's count has the level's parity: a lone node is the level's
+    // unpaired last node, K(l || 0^128))
+    uint32_t parts = nwg, stride = 1, idx = b, gslot = slot + 1;
+    while (kTopGroupLog2 > 0 && parts > kTopGroup) {
+        const uint32_t grp = idx / kTopGroup, g0 = grp * kTopGroup;
+        const uint32_t members = parts - g0 < kTopGroup ? parts - g0 : kTopGroup;
+        const uint32_t groups = (parts + kTopGroup - 1) / kTopGroup;
+        if (!wg_arrive_last(gslot + grp, members, &flag)) return;
+        m = members;
+        wg_load_nodes<true>(lds, sub + 8 * stride * g0, m, stride);
+        for (uint32_t k = 0; k < kTopGroupLog2; ++k) {
+            wg_level<NT, false>(lds, m, cst, none3, none_p, none_w);
+            m = (m + 1) / 2;
+        }
+        stride *= kTopGroup;
+        idx = grp;
+        wg_store_node0<true>(lds, sub + 8 * stride * idx);
+        gslot += groups;
+        parts = groups;
+    }
+    if (!wg_arrive_last(slot, parts, &flag)) return;
+    m = parts;
+    wg_load_nodes<true>(lds, sub, m, stride);
+    while (m > 1) {
+        wg_level<NT, false>(lds, m, cst, none3, none_p, none_w);
+        m = (m + 1) / 2;
+    }
+    // the length mix-in K(root || le64(n) || 0^24) on wave 0 (spread form)
+    if (threadIdx.x < 64) {
+        const uint32_t L = threadIdx.x, i = cst.i;
+        uint32_t e = 0u, o = 0u;
+        if (i < 4u) {
+            e = lds[2 * i];
+            o = lds[2 * i + 1];
+        } else if (i == 4u) {
+            e = ilv::to_ilv((uint32_t)n, (uint32_t)(n >> 32), 0);
+            o = ilv::to_ilv((uint32_t)n, (uint32_t)(n >> 32), 1);
+        } else if (i == 8u) {
+            e = 1u;
+        }
+        if (i == 16u) o ^= 0x80000000u;
+        spread::keccak_f(e, o, cst);
+        spread_store_digest(e, o, L, out);
+    }
+}
+template __global__ void k_struct_list_fused<3, 6>(const uint8_t*, uint64_t, StructSpec, uint32_t, uint4*, ReduceArgs,
+                                                   uint32_t*, uint32_t*, uint32_t);
 
 // Root() after each of m deposits appended at count0 (powchain's saveInTrie
 // reads Root() before every UpdateDepositTrie, service.go:379-386): wave g

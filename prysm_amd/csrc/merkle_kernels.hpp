@@ -116,6 +116,9 @@ __global__ void k_trie_append(uint32_t* levels, uint64_t cap, uint32_t d0, uint6
 constexpr uint32_t kSpreadWavesMax = MK_SPREAD_WAVES_MAX;  // k_trie_spread: one state per wave (<= 4 per SIMD)
 template <uint32_t SPAN>
 __global__ void k_spread_leaf(ReduceArgs a, uint32_t w8);
+template <int NB, int NRAW>
+__global__ void k_struct_list_fused(const uint8_t* rec, uint64_t n, StructSpec sp, uint32_t vec16, uint4* roots,
+                                    ReduceArgs a, uint32_t* sub, uint32_t* out, uint32_t slot);
 // new deposits k_trie_spread hashes into level 0 first (k == 0: none)
 struct SpreadLeaves {
     const uint8_t* data;
