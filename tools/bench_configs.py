@@ -127,7 +127,7 @@ def measure_c1(dev, steps, warmup):
     ok = want.hex() == g["root"] and dev_root == want
     return {"metric": "ssz.TreeHash of a 16,384-entry []ValidatorRecord (host buffers)", "unit": "validators/s",
             "value": n / sec, "sec": sec, "perms": perms, "hashes": hashes,
-            "dominant_kernel": "k_struct_split<3,6> (4 lanes per record: the 3 field hashes side by side, the 2-block struct message on a lo/hi lane pair), then the list tree in the latency form (k_spread_leaf<8> + k_merkle_top_fused)",
+            "dominant_kernel": "k_struct_list_fused<3,6> (the whole list in one launch: 4 lanes per record -- the 3 field hashes side by side, the 2-block struct message on a lo/hi lane pair --, 8 windows per workgroup one per wave, 3 levels, then groups of 16 workgroups to the root and the mix-in)",
             "root": want.hex(), "root_matches_golden": ok,
             "config": {"workload": "C1: TreeHash([]*ValidatorRecord), 16,384 synthetic validators, host records",
                        "n": n, "root": want.hex(), "root_matches_golden": ok,
