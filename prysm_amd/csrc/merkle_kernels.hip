@@ -3274,8 +3274,11 @@ __device__ __forceinline__ void ilv_to_plain(uint32_t e, uint32_t o, uint32_t& l
 // (deposit_trie.go:33-38); otherwise merkleHash's rule: the unpaired last
 // node is K(l || 0^128), 160 B (hash.go:229-236).  The form follows the
 // parent count (cycles per level measured in-kernel, tools/top_probe.hip):
-//   >= 256 parents: one state per lane (>= one wave per SIMD; 512 parents
-//       ~39 k cycles, against ~44 k as lane pairs at four waves per SIMD);
+//   > 256 parents: one state per lane (two waves per SIMD; 512 parents
+//       ~39 k cycles, against ~44 k as lane pairs at four waves per SIMD;
+//       256 parents as lane pairs at two waves per SIMD: one trie -0.6 us,
+//       one state -0.9 us against one state per lane at one wave per SIMD,
+//       3 interleaved rounds, profiles/r06/lane257/);
 //   > NT/128: bit-interleaved lane pairs (mk::ilv: ~13 k cycles a level for
 //       up to one wave per SIMD; 16 parents in one wave 12.8 k, against
 //       17.8 k as 16 spread waves, four per SIMD);
@@ -3283,6 +3286,8 @@ __device__ __forceinline__ void ilv_to_plain(uint32_t e, uint32_t o, uint32_t& l
 // Each parent also goes to lane_out(j, d0, d1) (plain digest), pair_out(j,
 // words, p) (ilv words of a lane pair) or wave_out(j, e, o, L) (lanes 0..3
 // of the wave hold the digest's ilv words).
+// parents from which a level runs one state per lane (below: lane pairs)
+constexpr uint32_t kTopLaneMin = 257;
 template <uint32_t NT, bool TRIE, typename LaneOut, typename PairOut, typename WaveOut>
 __device__ __forceinline__ void wg_level(uint32_t* lds, uint32_t m, const spread::Lane& cst, LaneOut&& lane_out,
                                          PairOut&& pair_out, WaveOut&& wave_out) {
@@ -3329,7 +3334,7 @@ __device__ __forceinline__ void wg_level(uint32_t* lds, uint32_t m, const spread
         const bool sw = side && w == NT / 64 - 1;
         uint32_t e = 0u, o = 0u;
         if (sw) spread_load(mn - 1, e, o);
-        if (mh >= 256) {  // one state per lane
+        if (mh >= kTopLaneMin) {  // one state per lane
             const bool act = tid < mh;
             const bool right = 2 * tid + 1 < m;
             State s;
